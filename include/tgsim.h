@@ -1,0 +1,173 @@
+/*
+ * tgsim.h -- C-ABI of libtgsim.so, the MI355X-native articulated-body
+ * simulator that replaces the IsaacGym/PhysX tensor API as the reference task
+ * code uses it.  Plain C types only (device pointers are passed as raw
+ * pointers, sizes as ints); no torch or HIP types appear in any signature.
+ *
+ * Reference interface each entry point replaces (paths relative to
+ * /root/reference/isaacgymenvs/):
+ *
+ *   tg_sim_create            gym.create_sim + load_asset + create_env/actor loop
+ *                            + prepare_sim   (tasks/base/vec_task.py:51-57,217;
+ *                            tasks/gogoro_new.py:155-162,196-294)
+ *   tg_sim_destroy           (process teardown)
+ *   tg_state_ptrs            acquire_actor_root_state_tensor /
+ *                            acquire_dof_state_tensor + gymtorch.wrap_tensor
+ *                            (tasks/gogoro_new.py:125-130)
+ *   tg_refresh               refresh_actor_root_state_tensor /
+ *                            refresh_dof_state_tensor (gogoro_new.py:141-142,426-427)
+ *                            -- a stream-ordered no-op: the views are the live state
+ *   tg_set_dof_position_targets / tg_set_dof_velocity_targets
+ *                            set_dof_position_target_tensor /
+ *                            set_dof_velocity_target_tensor (gogoro_new.py:364,369)
+ *   tg_set_actor_root_state_indexed
+ *                            set_actor_root_state_tensor_indexed (gogoro_new.py:547)
+ *   tg_set_dof_state_indexed set_dof_state_tensor_indexed (gogoro_new.py:552)
+ *   tg_set_dof_properties_indexed
+ *                            set_actor_dof_properties per env (gogoro_new.py:294,601)
+ *   tg_set_body_mass_scale_indexed / tg_set_gravity
+ *                            rigid_body_properties.mass / sim_params.gravity
+ *                            domain randomisation (vec_task.py:538-768)
+ *   tg_set_shape_friction_indexed
+ *                            set_actor_rigid_shape_properties (gogoro_new.py:284-293)
+ *   tg_apply_body_forces     apply_rigid_body_force_tensors
+ *                            (tasks/gogoro_realistic_turning_sim_paper.py:457)
+ *   tg_simulate              gym.simulate (vec_task.py:335): sim.substeps substeps
+ *   tg_sync                  fetch_results(sim, True) (vec_task.py:339)
+ *   tg_last_error            (replaces the reference's bool returns + assert,
+ *                            gogoro_new.py:547,552, and quit() on creation
+ *                            failure, vec_task.py:291-293)
+ *
+ * Every call returns 0 on success and a negative code on error; the message
+ * is available from tg_last_error() (thread-local).  Calls are asynchronous
+ * on the stream given by tg_set_stream(); inputs are caller-owned device
+ * pointers read in stream order and never retained.
+ */
+#ifndef TGSIM_H
+#define TGSIM_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TG_OK 0
+#define TG_ERR_ARG -1
+#define TG_ERR_HIP -2
+#define TG_ERR_MODEL -3
+#define TG_ERR_STATE -4
+
+#define TG_JOINT_FIXED 0
+#define TG_JOINT_REVOLUTE 1
+#define TG_JOINT_PRISMATIC 2
+
+#define TG_SHAPE_TORUS 0   /* params: R_major, r_minor; torus axis = shape z */
+#define TG_SHAPE_BOX 1     /* params: half extents x,y,z                     */
+#define TG_SHAPE_SPHERE 2  /* params: radius                                 */
+
+/* DOF drive modes (gymapi.DOF_MODE_*) */
+#define TG_DOF_MODE_NONE 0
+#define TG_DOF_MODE_POS 1
+#define TG_DOF_MODE_VEL 2
+#define TG_DOF_MODE_EFFORT 3
+
+/* per-env DOF property fields for tg_set_dof_properties_indexed */
+#define TG_PROP_STIFFNESS 0
+#define TG_PROP_DAMPING 1
+#define TG_PROP_EFFORT 2
+#define TG_PROP_VELOCITY 3
+#define TG_PROP_LOWER 4
+#define TG_PROP_UPPER 5
+#define TG_PROP_DRIVE_MODE 6  /* values passed as float, rounded */
+#define TG_PROP_ARMATURE 7
+#define TG_NUM_PROPS 8
+
+/* Articulation model, links in depth-first order (parents before children).
+ * Link frames follow URDF: a link's frame is its incoming joint frame.
+ * A "group" is a group-root link plus all descendants reached through fixed
+ * or locked joints (locked = position fixed per env between resets, the
+ * reference's limit-locked joints, tasks/gogoro_new.py:257-262,562-572). */
+typedef struct tg_model_desc {
+    int32_t num_links;
+    int32_t num_dofs;
+    int32_t num_groups;
+    int32_t num_shapes;
+    const int32_t *link_parent;   /* [L] parent link, -1 for the root       */
+    const int32_t *link_group;    /* [L] group of each link                 */
+    const int32_t *link_dof;      /* [L] dof of the incoming joint, -1 fixed */
+    const int32_t *link_jtype;    /* [L] TG_JOINT_*                          */
+    const float *link_origin;     /* [L,12] incoming joint origin in parent link frame: R row-major (9), p (3) */
+    const float *link_axis;       /* [L,3] joint axis in the link frame      */
+    const float *link_inertia;    /* [L,10] mass, com xyz, ixx iyy izz ixy ixz iyz (about com, link axes) */
+    const int32_t *group_root;    /* [G] root link of each group             */
+    const int32_t *group_parent;  /* [G] parent group, -1 for the floating root */
+    const int32_t *dof_locked;    /* [D] 1 if the dof is locked              */
+    const int32_t *shape_link;    /* [S] */
+    const int32_t *shape_kind;    /* [S] TG_SHAPE_* */
+    const float *shape_pose;      /* [S,12] R row-major, p in the link frame */
+    const float *shape_params;    /* [S,4] */
+    const float *shape_friction;  /* [S] */
+    uint64_t model_hash;          /* selects the compiled kernel specialisation */
+} tg_model_desc;
+
+/* sim_params (cfg/task/<Task>.yaml "sim" + "physx" blocks, vec_task.py:442-490) */
+typedef struct tg_sim_params {
+    float dt;                     /* control dt (sim.dt)                   */
+    int32_t substeps;             /* sim.substeps                          */
+    float gravity[3];             /* sim.gravity                           */
+    float linear_damping;         /* AssetOptions.linear_damping           */
+    float angular_damping;        /* AssetOptions.angular_damping          */
+    float max_depenetration_velocity; /* physx.max_depenetration_velocity  */
+    float rest_offset;            /* physx.rest_offset                     */
+    float contact_margin;         /* speculative contact distance          */
+    float ground_friction;        /* PlaneParams.static_friction           */
+    float baumgarte;              /* penetration push-out factor per substep */
+    float limit_stiffness;        /* implicit limit spring, fraction of joint inertia / h^2 */
+    float limit_damping;          /* implicit limit damper, fraction of joint inertia / h   */
+    int32_t contact_iterations;   /* projected Gauss-Seidel sweeps per substep */
+    int32_t fix_base;             /* AssetOptions.fix_base_link            */
+    float env_spacing;            /* create_env spacing (env origins grid) */
+    int32_t envs_per_row;
+} tg_sim_params;
+
+/* zero-copy device views (gymtorch.wrap_tensor equivalents) */
+typedef struct tg_state_view {
+    float *root_state;            /* [N,13] pos(3) quat xyzw(4) linvel(3) angvel(3), world frame */
+    float *dof_state;             /* [N*D,2] pos, vel */
+    float *dof_pos_target;        /* [N,D] */
+    float *dof_vel_target;        /* [N,D] */
+    float *dof_actuation;         /* [N,D] effort-mode forces */
+    float *dof_props;             /* [TG_NUM_PROPS,N,D] */
+    float *body_force;            /* [N,G,6] external wrench per group, world frame (force, torque at group COM) */
+    float *env_origin;            /* [N,3] */
+    uint8_t *env_dirty;           /* [N] */
+    int32_t num_envs, num_dofs, num_groups, num_links;
+} tg_state_view;
+
+typedef struct tg_sim tg_sim;
+
+int tg_sim_create(const tg_model_desc *model, const tg_sim_params *params, int32_t num_envs, int32_t device,
+                  tg_sim **out);
+int tg_sim_destroy(tg_sim *sim);
+int tg_set_stream(tg_sim *sim, void *hip_stream);
+int tg_state_ptrs(tg_sim *sim, tg_state_view *view);
+int tg_refresh(tg_sim *sim);
+int tg_set_dof_position_targets(tg_sim *sim, const float *pos);
+int tg_set_dof_velocity_targets(tg_sim *sim, const float *vel);
+int tg_set_dof_actuation_forces(tg_sim *sim, const float *effort);
+int tg_set_actor_root_state_indexed(tg_sim *sim, const float *root, const int32_t *ids, int32_t n);
+int tg_set_dof_state_indexed(tg_sim *sim, const float *dof, const int32_t *ids, int32_t n);
+int tg_set_dof_properties_indexed(tg_sim *sim, int32_t field, const float *vals, const int32_t *ids, int32_t n);
+int tg_set_body_mass_scale_indexed(tg_sim *sim, const float *scale, const int32_t *ids, int32_t n);
+int tg_set_shape_friction_indexed(tg_sim *sim, const float *mu, const int32_t *ids, int32_t n);
+int tg_set_gravity(tg_sim *sim, const float *g3);
+int tg_apply_body_forces(tg_sim *sim, const float *wrench);
+int tg_simulate(tg_sim *sim);
+int tg_sync(tg_sim *sim);
+const char *tg_last_error(void);
+uint64_t tg_compiled_model_hashes(uint64_t *out, int32_t cap); /* returns count */
+
+#ifdef __cplusplus
+}
+#endif
+#endif

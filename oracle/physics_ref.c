@@ -1,0 +1,780 @@
+/*
+ * oracle/physics_ref.c -- fp64 CPU restatement of the articulated-body step.
+ *
+ * TEST INFRASTRUCTURE ONLY: the parity checker for the HIP step kernel
+ * (thormang_isaacgym_amd/csrc/articulation.hip) and the cpu_baseline leg of
+ * bench.py.  The product path never loads it.
+ *
+ * PARITY STATUS.  The reference's physics is the closed IsaacGym/PhysX binary
+ * (gym.simulate, isaacgymenvs/tasks/base/vec_task.py:335), absent from
+ * /root/reference and unavailable offline: physics parity with
+ * PhysX is UNPINNED.  This file restates the algorithm the build implements
+ * (Featherstone articulated-body algorithm over the URDF joint tree, implicit
+ * joint-space PD drives, implicit limit springs, speculative velocity-level
+ * ground contact solved by projected Gauss-Seidel, semi-implicit Euler) from
+ * the published algorithm (Featherstone, "Rigid Body Dynamics Algorithms",
+ * 2008, ch. 2, 7, 9) with the reference's parameters.  It
+ * is pinned by analytic known-answer tests in tests/test_physics_oracle.py
+ * (free fall, pendulum period, torque-free momentum/energy, drive steady
+ * state, resting contact).  It deliberately uses a different data layout from
+ * the HIP kernel: dense 6x6 double matrices, table-driven loops, no
+ * specialisation.
+ *
+ * Spatial conventions: motion [w; v], force [n; f]; X = child-from-parent.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/tgsim.h"
+
+#define MAXG 64
+#define MAXL 96
+#define MAXD 64
+#define MAXC 32
+
+typedef double real;
+typedef real V3[3];
+typedef real M3[9];
+typedef real V6[6];
+typedef real M6[36];
+
+static void m3_mul(const M3 a, const M3 b, M3 o) {
+    M3 t;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) t[3 * i + j] = a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j] + a[3 * i + 2] * b[6 + j];
+    memcpy(o, t, sizeof t);
+}
+static void m3_T(const M3 a, M3 o) {
+    M3 t;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) t[3 * i + j] = a[3 * j + i];
+    memcpy(o, t, sizeof t);
+}
+static void m3_v(const M3 a, const V3 v, V3 o) {
+    V3 t = {a[0] * v[0] + a[1] * v[1] + a[2] * v[2], a[3] * v[0] + a[4] * v[1] + a[5] * v[2],
+            a[6] * v[0] + a[7] * v[1] + a[8] * v[2]};
+    memcpy(o, t, sizeof t);
+}
+static void m3T_v(const M3 a, const V3 v, V3 o) {
+    V3 t = {a[0] * v[0] + a[3] * v[1] + a[6] * v[2], a[1] * v[0] + a[4] * v[1] + a[7] * v[2],
+            a[2] * v[0] + a[5] * v[1] + a[8] * v[2]};
+    memcpy(o, t, sizeof t);
+}
+static void cross3(const V3 a, const V3 b, V3 o) {
+    V3 t = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+    memcpy(o, t, sizeof t);
+}
+static real dot3(const V3 a, const V3 b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static void axis_angle(const V3 a, real q, M3 R) {
+    real c = cos(q), s = sin(q), t = 1 - c, x = a[0], y = a[1], z = a[2];
+    R[0] = t * x * x + c; R[1] = t * x * y - s * z; R[2] = t * x * z + s * y;
+    R[3] = t * x * y + s * z; R[4] = t * y * y + c; R[5] = t * y * z - s * x;
+    R[6] = t * x * z - s * y; R[7] = t * y * z + s * x; R[8] = t * z * z + c;
+}
+static void quat_to_m3(const real *q, M3 R) {   /* xyzw, body->world */
+    real x = q[0], y = q[1], z = q[2], w = q[3];
+    R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - z * w); R[2] = 2 * (x * z + y * w);
+    R[3] = 2 * (x * y + z * w); R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - x * w);
+    R[6] = 2 * (x * z - y * w); R[7] = 2 * (y * z + x * w); R[8] = 1 - 2 * (x * x + y * y);
+}
+
+/* ---------------------------------------------------------------- spatial */
+typedef struct { M3 E; V3 r; } Xform;   /* child-from-parent: E parent->child coords, r child origin in parent */
+
+static void X_motion(const Xform *X, const V6 v, V6 o) {   /* o = X v */
+    V3 w = {v[0], v[1], v[2]}, lin = {v[3], v[4], v[5]}, rxw, t;
+    cross3(X->r, w, rxw);
+    for (int k = 0; k < 3; ++k) t[k] = lin[k] - rxw[k];
+    V3 ow, ol;
+    m3_v(X->E, w, ow);
+    m3_v(X->E, t, ol);
+    o[0] = ow[0]; o[1] = ow[1]; o[2] = ow[2]; o[3] = ol[0]; o[4] = ol[1]; o[5] = ol[2];
+}
+static void XT_force(const Xform *X, const V6 f, V6 o) {   /* o = X^T f  (child force -> parent) */
+    V3 n = {f[0], f[1], f[2]}, fl = {f[3], f[4], f[5]}, En, Ef, rxf;
+    m3T_v(X->E, n, En);
+    m3T_v(X->E, fl, Ef);
+    cross3(X->r, Ef, rxf);
+    o[0] = En[0] + rxf[0]; o[1] = En[1] + rxf[1]; o[2] = En[2] + rxf[2];
+    o[3] = Ef[0]; o[4] = Ef[1]; o[5] = Ef[2];
+}
+static void X_dense(const Xform *X, M6 M) {   /* dense motion transform */
+    memset(M, 0, sizeof(M6));
+    real rx[9] = {0, -X->r[2], X->r[1], X->r[2], 0, -X->r[0], -X->r[1], X->r[0], 0};
+    M3 Erx;
+    m3_mul(X->E, rx, Erx);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            M[6 * i + j] = X->E[3 * i + j];
+            M[6 * (i + 3) + j + 3] = X->E[3 * i + j];
+            M[6 * (i + 3) + j] = -Erx[3 * i + j];
+        }
+}
+static void m6_v(const M6 A, const V6 v, V6 o) {
+    V6 t;
+    for (int i = 0; i < 6; ++i) {
+        real s = 0;
+        for (int j = 0; j < 6; ++j) s += A[6 * i + j] * v[j];
+        t[i] = s;
+    }
+    memcpy(o, t, sizeof t);
+}
+static void crm(const V6 v, const V6 m, V6 o) {   /* v x m */
+    V3 w = {v[0], v[1], v[2]}, vl = {v[3], v[4], v[5]}, mw = {m[0], m[1], m[2]}, ml = {m[3], m[4], m[5]}, a, b, c;
+    cross3(w, mw, a);
+    cross3(w, ml, b);
+    cross3(vl, mw, c);
+    o[0] = a[0]; o[1] = a[1]; o[2] = a[2]; o[3] = b[0] + c[0]; o[4] = b[1] + c[1]; o[5] = b[2] + c[2];
+}
+static void crf(const V6 v, const V6 f, V6 o) {   /* v x* f */
+    V3 w = {v[0], v[1], v[2]}, vl = {v[3], v[4], v[5]}, fn = {f[0], f[1], f[2]}, ff = {f[3], f[4], f[5]}, a, b, c;
+    cross3(w, fn, a);
+    cross3(vl, ff, b);
+    cross3(w, ff, c);
+    o[0] = a[0] + b[0]; o[1] = a[1] + b[1]; o[2] = a[2] + b[2]; o[3] = c[0]; o[4] = c[1]; o[5] = c[2];
+}
+/* rigid-body spatial inertia at frame origin from mass, com, rotational inertia about com (3x3) */
+static void rb_inertia(real m, const V3 c, const M3 Ic, M6 I) {
+    memset(I, 0, sizeof(M6));
+    real cx[9] = {0, -c[2], c[1], c[2], 0, -c[0], -c[1], c[0], 0};
+    M3 cxcxT;
+    real cxT[9];
+    m3_T(cx, cxT);
+    m3_mul(cx, cxT, cxcxT);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            I[6 * i + j] = Ic[3 * i + j] + m * cxcxT[3 * i + j];
+            I[6 * i + j + 3] = m * cx[3 * i + j];
+            I[6 * (i + 3) + j] = m * cxT[3 * i + j];
+            I[6 * (i + 3) + j + 3] = (i == j) ? m : 0;
+        }
+}
+/* solve 6x6 SPD system by Gaussian elimination with partial pivoting */
+static void solve6(const M6 A, const V6 b, V6 x) {
+    real M[6][7];
+    for (int i = 0; i < 6; ++i) {
+        for (int j = 0; j < 6; ++j) M[i][j] = A[6 * i + j];
+        M[i][6] = b[i];
+    }
+    for (int c = 0; c < 6; ++c) {
+        int p = c;
+        for (int r = c + 1; r < 6; ++r)
+            if (fabs(M[r][c]) > fabs(M[p][c])) p = r;
+        if (p != c)
+            for (int k = 0; k < 7; ++k) { real t = M[c][k]; M[c][k] = M[p][k]; M[p][k] = t; }
+        for (int r = c + 1; r < 6; ++r) {
+            real f = M[r][c] / M[c][c];
+            for (int k = c; k < 7; ++k) M[r][k] -= f * M[c][k];
+        }
+    }
+    for (int r = 5; r >= 0; --r) {
+        real s = M[r][6];
+        for (int k = r + 1; k < 6; ++k) s -= M[r][k] * x[k];
+        x[r] = s / M[r][r];
+    }
+}
+
+/* ---------------------------------------------------------------- per-env workspace */
+typedef struct {
+    /* composite (per env, from locked positions + mass scale) */
+    real gm[MAXG];
+    V3 gc[MAXG];
+    M3 gI[MAXG];
+    M3 xtR[MAXG];      /* joint origin of each group, in parent group frame */
+    V3 xtp[MAXG];
+    V3 gaxis[MAXG];    /* joint axis in group frame */
+    int gtype[MAXG];
+    int gdof[MAXG];
+    M3 shR[MAXC];      /* shape pose in its group frame */
+    V3 shp[MAXC];
+    int shg[MAXC];
+    /* per substep */
+    Xform X[MAXG];
+    M3 Rw[MAXG];
+    V3 pw[MAXG];
+    V6 v[MAXG], c[MAXG], pA[MAXG], U[MAXG], S[MAXG];
+    M6 IA[MAXG];
+    real D[MAXG], u[MAXG];
+} Work;
+
+/* compose: per-env group composites (tgsim.h model grouping). lockq[D] = locked positions. */
+static void compose(const tg_model_desc *m, const real *lockq, const float *mass_scale, Work *w) {
+    M3 TR[MAXL];
+    V3 Tp[MAXL];
+    int G = m->num_groups;
+    for (int g = 0; g < G; ++g) {
+        w->gm[g] = 0;
+        memset(w->gc[g], 0, sizeof(V3));
+        memset(w->gI[g], 0, sizeof(M3));
+    }
+    /* pass A: link poses in group frames, mass and first moment */
+    for (int l = 0; l < m->num_links; ++l) {
+        int g = m->link_group[l];
+        if (m->group_root[g] == l) {
+            M3 I = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+            memcpy(TR[l], I, sizeof I);
+            memset(Tp[l], 0, sizeof(V3));
+        } else {
+            int p = m->link_parent[l];
+            const float *o = m->link_origin + 12 * l;
+            M3 Ro, Rj;
+            V3 to = {o[9], o[10], o[11]}, ax = {m->link_axis[3 * l], m->link_axis[3 * l + 1], m->link_axis[3 * l + 2]};
+            for (int k = 0; k < 9; ++k) Ro[k] = o[k];
+            int d = m->link_dof[l];
+            real q = d >= 0 ? lockq[d] : 0.0;
+            if (m->link_jtype[l] == TG_JOINT_REVOLUTE) {
+                axis_angle(ax, q, Rj);
+                m3_mul(Ro, Rj, Ro);
+            } else if (m->link_jtype[l] == TG_JOINT_PRISMATIC) {
+                V3 s;
+                m3_v(Ro, ax, s);
+                for (int k = 0; k < 3; ++k) to[k] += s[k] * q;
+            }
+            /* T_l = T_p * (Ro, to) */
+            m3_mul(TR[p], Ro, TR[l]);
+            V3 t;
+            m3_v(TR[p], to, t);
+            for (int k = 0; k < 3; ++k) Tp[l][k] = Tp[p][k] + t[k];
+        }
+        const float *in = m->link_inertia + 10 * l;
+        real s = mass_scale ? mass_scale[l] : 1.0;
+        real ml = in[0] * s;
+        V3 cl = {in[1], in[2], in[3]}, cg;
+        m3_v(TR[l], cl, cg);
+        for (int k = 0; k < 3; ++k) cg[k] += Tp[l][k];
+        w->gm[g] += ml;
+        for (int k = 0; k < 3; ++k) w->gc[g][k] += ml * cg[k];
+    }
+    for (int g = 0; g < G; ++g)
+        if (w->gm[g] > 0)
+            for (int k = 0; k < 3; ++k) w->gc[g][k] /= w->gm[g];
+    /* pass B: rotational inertia about group com */
+    for (int l = 0; l < m->num_links; ++l) {
+        int g = m->link_group[l];
+        const float *in = m->link_inertia + 10 * l;
+        real s = mass_scale ? mass_scale[l] : 1.0;
+        real ml = in[0] * s;
+        M3 Il = {in[4] * s, in[7] * s, in[8] * s, in[7] * s, in[5] * s, in[9] * s, in[8] * s, in[9] * s, in[6] * s};
+        M3 RI, RIRt, RT;
+        m3_mul(TR[l], Il, RI);
+        m3_T(TR[l], RT);
+        m3_mul(RI, RT, RIRt);
+        V3 cl = {in[1], in[2], in[3]}, cg;
+        m3_v(TR[l], cl, cg);
+        V3 dd;
+        for (int k = 0; k < 3; ++k) dd[k] = cg[k] + Tp[l][k] - w->gc[g][k];
+        real d2 = dot3(dd, dd);
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                w->gI[g][3 * i + j] += RIRt[3 * i + j] + ml * ((i == j ? d2 : 0) - dd[i] * dd[j]);
+    }
+    /* joint placements and axes of active joints */
+    for (int g = 0; g < G; ++g) {
+        int r = m->group_root[g];
+        w->gdof[g] = m->link_dof[r];
+        w->gtype[g] = (g == 0) ? -1 : m->link_jtype[r];
+        for (int k = 0; k < 3; ++k) w->gaxis[g][k] = m->link_axis[3 * r + k];
+        if (g == 0) continue;
+        int p = m->link_parent[r];
+        const float *o = m->link_origin + 12 * r;
+        M3 Ro;
+        for (int k = 0; k < 9; ++k) Ro[k] = o[k];
+        V3 to = {o[9], o[10], o[11]}, t;
+        m3_mul(TR[p], Ro, w->xtR[g]);
+        m3_v(TR[p], to, t);
+        for (int k = 0; k < 3; ++k) w->xtp[g][k] = Tp[p][k] + t[k];
+    }
+    for (int s = 0; s < m->num_shapes; ++s) {
+        int l = m->shape_link[s];
+        const float *o = m->shape_pose + 12 * s;
+        M3 Ro;
+        for (int k = 0; k < 9; ++k) Ro[k] = o[k];
+        V3 to = {o[9], o[10], o[11]}, t;
+        m3_mul(TR[l], Ro, w->shR[s]);
+        m3_v(TR[l], to, t);
+        for (int k = 0; k < 3; ++k) w->shp[s][k] = Tp[l][k] + t[k];
+        w->shg[s] = m->link_group[l];
+    }
+}
+
+typedef struct {
+    const tg_model_desc *m;
+    const tg_sim_params *sp;
+    const float *props;       /* [TG_NUM_PROPS][D] for this env (strided) */
+    long prop_stride;         /* stride between prop fields */
+    const float *pos_tgt, *vel_tgt, *act;
+    const float *force;       /* [G,6] world wrench at group com or NULL */
+    const float *mu;          /* [S] shape friction for this env */
+    real g[3];
+} Env;
+
+static real prop(const Env *e, int f, int d) { return e->props[f * e->prop_stride + d]; }
+
+/* ABA pass 1+2+3 with the given generalised state; fills qdd (dof-indexed) and a0. */
+static void aba(const Env *e, Work *w, real h, const real *q, const real *qd, const V6 v0, real *qdd, V6 a0,
+                int with_bias) {
+    const tg_model_desc *m = e->m;
+    int G = m->num_groups;
+    for (int g = 0; g < G; ++g) {
+        int d = w->gdof[g];
+        /* joint transform */
+        if (g == 0) {
+            memcpy(w->v[0], v0, sizeof(V6));
+            memset(w->c[0], 0, sizeof(V6));
+            memset(w->S[0], 0, sizeof(V6));
+        } else {
+            int p = m->group_parent[g];
+            M3 Rpc;
+            V3 t;
+            memcpy(t, w->xtp[g], sizeof t);
+            if (w->gtype[g] == TG_JOINT_REVOLUTE) {
+                M3 Rj;
+                axis_angle(w->gaxis[g], q[d], Rj);
+                m3_mul(w->xtR[g], Rj, Rpc);
+            } else {
+                memcpy(Rpc, w->xtR[g], sizeof(M3));
+                V3 s;
+                m3_v(w->xtR[g], w->gaxis[g], s);
+                for (int k = 0; k < 3; ++k) t[k] += s[k] * q[d];
+            }
+            m3_T(Rpc, w->X[g].E);
+            memcpy(w->X[g].r, t, sizeof t);
+            V6 S = {0};
+            if (w->gtype[g] == TG_JOINT_REVOLUTE) { S[0] = w->gaxis[g][0]; S[1] = w->gaxis[g][1]; S[2] = w->gaxis[g][2]; }
+            else { S[3] = w->gaxis[g][0]; S[4] = w->gaxis[g][1]; S[5] = w->gaxis[g][2]; }
+            memcpy(w->S[g], S, sizeof S);
+            V6 vp, vJ;
+            X_motion(&w->X[g], w->v[p], vp);
+            for (int k = 0; k < 6; ++k) { vJ[k] = S[k] * qd[d]; w->v[g][k] = vp[k] + vJ[k]; }
+            crm(w->v[g], vJ, w->c[g]);
+            /* world pose */
+            m3_mul(w->Rw[p], Rpc, w->Rw[g]);
+            V3 tw;
+            m3_v(w->Rw[p], t, tw);
+            for (int k = 0; k < 3; ++k) w->pw[g][k] = w->pw[p][k] + tw[k];
+        }
+        rb_inertia(w->gm[g], w->gc[g], w->gI[g], w->IA[g]);
+        memset(w->pA[g], 0, sizeof(V6));
+        if (with_bias) {
+            V6 Iv, b;
+            m6_v(w->IA[g], w->v[g], Iv);
+            crf(w->v[g], Iv, b);
+            /* gravity + damping + applied wrench (group frame, about group origin) */
+            V3 gl, F, n;
+            m3T_v(w->Rw[g], e->g, gl);
+            for (int k = 0; k < 3; ++k) F[k] = w->gm[g] * gl[k];
+            V3 wv = {w->v[g][0], w->v[g][1], w->v[g][2]}, vo = {w->v[g][3], w->v[g][4], w->v[g][5]}, vc, wxc;
+            cross3(wv, w->gc[g], wxc);
+            for (int k = 0; k < 3; ++k) vc[k] = vo[k] + wxc[k];
+            for (int k = 0; k < 3; ++k) F[k] -= e->sp->linear_damping * w->gm[g] * vc[k];
+            V3 Iw;
+            m3_v(w->gI[g], wv, Iw);
+            cross3(w->gc[g], F, n);
+            for (int k = 0; k < 3; ++k) n[k] -= e->sp->angular_damping * Iw[k];
+            if (e->force) {
+                const float *fw = e->force + 6 * g;
+                V3 fwv = {fw[0], fw[1], fw[2]}, twv = {fw[3], fw[4], fw[5]}, fl, tl, cxf;
+                m3T_v(w->Rw[g], fwv, fl);
+                m3T_v(w->Rw[g], twv, tl);
+                cross3(w->gc[g], fl, cxf);
+                for (int k = 0; k < 3; ++k) { F[k] += fl[k]; n[k] += tl[k] + cxf[k]; }
+            }
+            for (int k = 0; k < 3; ++k) { b[k] -= n[k]; b[3 + k] -= F[k]; }
+            memcpy(w->pA[g], b, sizeof b);
+        }
+    }
+    /* pass 2 */
+    for (int g = G - 1; g >= 1; --g) {
+        int d = w->gdof[g], p = m->group_parent[g];
+        m6_v(w->IA[g], w->S[g], w->U[g]);
+        real D0 = 0;
+        for (int k = 0; k < 6; ++k) D0 += w->S[g][k] * w->U[g][k];
+        D0 += prop(e, TG_PROP_ARMATURE, d);
+        real Dimp = 0, tau = 0;
+        if (with_bias) {
+            int mode = (int)lrint(prop(e, TG_PROP_DRIVE_MODE, d));
+            real kp = prop(e, TG_PROP_STIFFNESS, d), kd = prop(e, TG_PROP_DAMPING, d), eff = prop(e, TG_PROP_EFFORT, d);
+            if (mode == TG_DOF_MODE_POS || mode == TG_DOF_MODE_VEL) {
+                real te = kp * (e->pos_tgt[d] - q[d] - h * qd[d]) + kd * (e->vel_tgt[d] - qd[d]);
+                if (fabs(te) <= eff) { tau += te; Dimp += h * kd + h * h * kp; }
+                else tau += te > 0 ? eff : -eff;
+            } else if (mode == TG_DOF_MODE_EFFORT && e->act) {
+                real a = e->act[d];
+                tau += a > eff ? eff : (a < -eff ? -eff : a);
+            }
+            real lo = prop(e, TG_PROP_LOWER, d), hi = prop(e, TG_PROP_UPPER, d);
+            real qp = q[d] + h * qd[d];
+            real kl = e->sp->limit_stiffness * D0 / (h * h), cl = e->sp->limit_damping * D0 / h;
+            if (qp < lo && lo > -1e30) { tau += kl * (lo - qp) - cl * qd[d]; Dimp += h * cl + h * h * kl; }
+            else if (qp > hi && hi < 1e30) { tau += kl * (hi - qp) - cl * qd[d]; Dimp += h * cl + h * h * kl; }
+        } else {
+            /* impulse response: same effective inertia as the dynamics pass */
+            Dimp = w->D[g] - D0;
+        }
+        w->D[g] = D0 + Dimp;
+        real sp = 0;
+        for (int k = 0; k < 6; ++k) sp += w->S[g][k] * w->pA[g][k];
+        w->u[g] = tau - sp;
+        M6 Ia;
+        V6 pa, Iac;
+        for (int i = 0; i < 6; ++i)
+            for (int j = 0; j < 6; ++j) Ia[6 * i + j] = w->IA[g][6 * i + j] - w->U[g][i] * w->U[g][j] / w->D[g];
+        m6_v(Ia, w->c[g], Iac);
+        for (int k = 0; k < 6; ++k) pa[k] = w->pA[g][k] + (with_bias ? Iac[k] : 0) + w->U[g][k] * w->u[g] / w->D[g];
+        /* parent += X^T Ia X ; X^T pa */
+        M6 X, T, XT;
+        X_dense(&w->X[g], X);
+        for (int i = 0; i < 6; ++i)
+            for (int j = 0; j < 6; ++j) XT[6 * i + j] = X[6 * j + i];
+        for (int i = 0; i < 6; ++i)
+            for (int j = 0; j < 6; ++j) {
+                real s = 0;
+                for (int k = 0; k < 6; ++k) s += Ia[6 * i + k] * X[6 * k + j];
+                T[6 * i + j] = s;
+            }
+        for (int i = 0; i < 6; ++i)
+            for (int j = 0; j < 6; ++j) {
+                real s = 0;
+                for (int k = 0; k < 6; ++k) s += XT[6 * i + k] * T[6 * k + j];
+                w->IA[p][6 * i + j] += s;
+            }
+        V6 pp;
+        XT_force(&w->X[g], pa, pp);
+        for (int k = 0; k < 6; ++k) w->pA[p][k] += pp[k];
+    }
+    /* pass 3 */
+    if (e->sp->fix_base) memset(a0, 0, sizeof(V6));
+    else {
+        V6 mp;
+        for (int k = 0; k < 6; ++k) mp[k] = -w->pA[0][k];
+        solve6(w->IA[0], mp, a0);
+    }
+    V6 a[MAXG];
+    memcpy(a[0], a0, sizeof(V6));
+    for (int g = 1; g < G; ++g) {
+        int d = w->gdof[g], p = m->group_parent[g];
+        V6 ap;
+        X_motion(&w->X[g], a[p], ap);
+        for (int k = 0; k < 6; ++k) ap[k] += with_bias ? w->c[g][k] : 0;
+        real ua = 0;
+        for (int k = 0; k < 6; ++k) ua += w->U[g][k] * ap[k];
+        qdd[d] = (w->u[g] - ua) / w->D[g];
+        for (int k = 0; k < 6; ++k) a[g][k] = ap[k] + w->S[g][k] * qdd[d];
+    }
+}
+
+/* velocity of group g's spatial velocity for generalised velocity (qd, v0) with current X */
+static void group_vels(const tg_model_desc *m, Work *w, const real *qd, const V6 v0, V6 *vg) {
+    memcpy(vg[0], v0, sizeof(V6));
+    for (int g = 1; g < m->num_groups; ++g) {
+        V6 vp;
+        X_motion(&w->X[g], vg[m->group_parent[g]], vp);
+        for (int k = 0; k < 6; ++k) vg[g][k] = vp[k] + w->S[g][k] * qd[w->gdof[g]];
+    }
+}
+
+/* impulse response: spatial impulses fi[G] (group frames) -> dqd, dv0 */
+static void impulse_response(const Env *e, Work *w, const V6 *fi, real *dqd, V6 dv0) {
+    const tg_model_desc *m = e->m;
+    int G = m->num_groups;
+    V6 p[MAXG];
+    for (int g = 0; g < G; ++g)
+        for (int k = 0; k < 6; ++k) p[g][k] = -fi[g][k];
+    real u[MAXG];
+    for (int g = G - 1; g >= 1; --g) {
+        real sp = 0;
+        for (int k = 0; k < 6; ++k) sp += w->S[g][k] * p[g][k];
+        u[g] = -sp;
+        V6 pa, pp;
+        for (int k = 0; k < 6; ++k) pa[k] = p[g][k] + w->U[g][k] * u[g] / w->D[g];
+        XT_force(&w->X[g], pa, pp);
+        for (int k = 0; k < 6; ++k) p[m->group_parent[g]][k] += pp[k];
+    }
+    V6 a[MAXG];
+    if (e->sp->fix_base) memset(a[0], 0, sizeof(V6));
+    else {
+        V6 mp;
+        for (int k = 0; k < 6; ++k) mp[k] = -p[0][k];
+        solve6(w->IA[0], mp, a[0]);
+    }
+    memcpy(dv0, a[0], sizeof(V6));
+    for (int g = 1; g < G; ++g) {
+        V6 ap;
+        X_motion(&w->X[g], a[m->group_parent[g]], ap);
+        real ua = 0;
+        for (int k = 0; k < 6; ++k) ua += w->U[g][k] * ap[k];
+        real x = (u[g] - ua) / w->D[g];
+        dqd[w->gdof[g]] = x;
+        for (int k = 0; k < 6; ++k) a[g][k] = ap[k] + w->S[g][k] * x;
+    }
+}
+
+typedef struct {
+    int g;           /* group */
+    V3 r;            /* contact point in group frame */
+    V3 dir[3];       /* world: normal, t1, t2 */
+    real target;     /* normal velocity lower bound */
+    real mu;
+} Contact;
+
+static int collect_contacts(const Env *e, Work *w, real h, Contact *cs) {
+    const tg_model_desc *m = e->m;
+    int nc = 0;
+    for (int s = 0; s < m->num_shapes; ++s) {
+        int g = w->shg[s];
+        M3 R;
+        V3 c;
+        m3_mul(w->Rw[g], w->shR[s], R);
+        m3_v(w->Rw[g], w->shp[s], c);
+        for (int k = 0; k < 3; ++k) c[k] += w->pw[g][k];
+        real mu = 0.5 * (e->mu[s] + e->sp->ground_friction);
+        V3 pts[8];
+        int np = 0;
+        if (m->shape_kind[s] == TG_SHAPE_TORUS) {
+            real Rm = m->shape_params[4 * s], rm = m->shape_params[4 * s + 1];
+            V3 a = {R[2], R[5], R[8]};
+            V3 d = {-a[2] * a[0], -a[2] * a[1], 1 - a[2] * a[2]};
+            real nd = sqrt(dot3(d, d));
+            if (nd < 1e-9) { d[0] = 1; d[1] = 0; d[2] = 0; nd = 1; }
+            for (int k = 0; k < 3; ++k) pts[0][k] = c[k] - Rm * d[k] / nd;
+            pts[0][2] -= rm;
+            np = 1;
+        } else if (m->shape_kind[s] == TG_SHAPE_SPHERE) {
+            memcpy(pts[0], c, sizeof(V3));
+            pts[0][2] -= m->shape_params[4 * s];
+            np = 1;
+        } else if (m->shape_kind[s] == TG_SHAPE_BOX) {
+            for (int k = 0; k < 8; ++k) {
+                V3 l = {(k & 1 ? 1 : -1) * m->shape_params[4 * s], (k & 2 ? 1 : -1) * m->shape_params[4 * s + 1],
+                        (k & 4 ? 1 : -1) * m->shape_params[4 * s + 2]}, wv;
+                m3_v(R, l, wv);
+                for (int j = 0; j < 3; ++j) pts[np][j] = c[j] + wv[j];
+                ++np;
+            }
+        }
+        for (int k = 0; k < np && nc < MAXC; ++k) {
+            real phi = pts[k][2];
+            if (phi > e->sp->contact_margin) continue;
+            Contact *C = &cs[nc++];
+            C->g = g;
+            V3 rel;
+            for (int j = 0; j < 3; ++j) rel[j] = pts[k][j] - w->pw[g][j];
+            m3T_v(w->Rw[g], rel, C->r);
+            C->dir[0][0] = 0; C->dir[0][1] = 0; C->dir[0][2] = 1;
+            /* t1: rolling direction for tori (axis x n), else world x */
+            V3 t1 = {1, 0, 0};
+            if (m->shape_kind[s] == TG_SHAPE_TORUS) {
+                V3 a = {R[2], R[5], R[8]}, n = {0, 0, 1}, x;
+                cross3(a, n, x);
+                real nx = sqrt(dot3(x, x));
+                if (nx > 1e-6) for (int j = 0; j < 3; ++j) t1[j] = x[j] / nx;
+            }
+            memcpy(C->dir[1], t1, sizeof t1);
+            V3 n = {0, 0, 1};
+            cross3(n, t1, C->dir[2]);
+            real rest = e->sp->rest_offset;
+            if (phi > rest) C->target = -(phi - rest) / h;
+            else {
+                C->target = e->sp->baumgarte * (rest - phi) / h;
+                if (C->target > e->sp->max_depenetration_velocity) C->target = e->sp->max_depenetration_velocity;
+            }
+            C->mu = mu;
+        }
+    }
+    return nc;
+}
+
+/* world-frame velocity of a contact point for group velocities vg */
+static void point_vel(const Work *w, const Contact *C, const V6 *vg, V3 out) {
+    V3 om = {vg[C->g][0], vg[C->g][1], vg[C->g][2]}, vl = {vg[C->g][3], vg[C->g][4], vg[C->g][5]}, wxr, loc;
+    cross3(om, C->r, wxr);
+    for (int k = 0; k < 3; ++k) loc[k] = vl[k] + wxr[k];
+    m3_v(w->Rw[C->g], loc, out);
+}
+
+/* One env, one control step (all substeps).  root[13], dof[2D] updated in place. */
+void oracle_physics_step_env(const tg_model_desc *m, const tg_sim_params *sp, float *root, float *dof,
+                             const float *props, long prop_stride, const float *pos_tgt, const float *vel_tgt,
+                             const float *act, const float *force, const float *mass_scale, const float *mu,
+                             const float *gravity) {
+    static __thread Work w;   /* large; per thread */
+    Env e = {m, sp, props, prop_stride, pos_tgt, vel_tgt, act, force, mu, {gravity[0], gravity[1], gravity[2]}};
+    int D = m->num_dofs, G = m->num_groups;
+    real lockq[MAXD], q[MAXD], qd[MAXD], qdd[MAXD];
+    for (int d = 0; d < D; ++d) {
+        lockq[d] = m->dof_locked[d] ? 0.5 * ((real)props[TG_PROP_LOWER * prop_stride + d] + props[TG_PROP_UPPER * prop_stride + d]) : 0;
+        q[d] = dof[2 * d];
+        qd[d] = dof[2 * d + 1];
+        qdd[d] = 0;
+    }
+    compose(m, lockq, mass_scale, &w);
+    real h = sp->dt / sp->substeps;
+    /* floating base state */
+    real pos[3] = {root[0], root[1], root[2]}, quat[4] = {root[3], root[4], root[5], root[6]};
+    real qn = sqrt(quat[0] * quat[0] + quat[1] * quat[1] + quat[2] * quat[2] + quat[3] * quat[3]);
+    for (int k = 0; k < 4; ++k) quat[k] /= qn;
+    M3 R;
+    quat_to_m3(quat, R);
+    const float *li0 = m->link_inertia;
+    V3 c0 = {li0[1], li0[2], li0[3]}, c0w, ww = {root[10], root[11], root[12]}, wxc, vo;
+    m3_v(R, c0, c0w);
+    cross3(ww, c0w, wxc);
+    for (int k = 0; k < 3; ++k) vo[k] = root[7 + k] - wxc[k];
+    V6 v0;
+    V3 wb, vb;
+    m3T_v(R, ww, wb);
+    m3T_v(R, vo, vb);
+    for (int k = 0; k < 3; ++k) { v0[k] = wb[k]; v0[3 + k] = vb[k]; }
+    if (sp->fix_base) memset(v0, 0, sizeof v0);
+
+    for (int s = 0; s < sp->substeps; ++s) {
+        memcpy(w.Rw[0], R, sizeof(M3));
+        memcpy(w.pw[0], pos, sizeof(V3));
+        V6 a0;
+        aba(&e, &w, h, q, qd, v0, qdd, a0, 1);
+        real qds[MAXD];
+        V6 v0s;
+        memcpy(qds, qd, sizeof(real) * D);
+        for (int g = 1; g < G; ++g) qds[w.gdof[g]] = qd[w.gdof[g]] + h * qdd[w.gdof[g]];
+        for (int k = 0; k < 6; ++k) v0s[k] = v0[k] + h * a0[k];
+        /* contacts */
+        Contact cs[MAXC];
+        int nc = collect_contacts(&e, &w, h, cs);
+        if (nc > 0) {
+            int K = 3 * nc;
+            static __thread real W[3 * MAXC][3 * MAXC];
+            real vfree[3 * MAXC], lam[3 * MAXC];
+            V6 vg[MAXG];
+            group_vels(m, &w, qds, v0s, vg);
+            for (int c = 0; c < nc; ++c) {
+                V3 pv;
+                point_vel(&w, &cs[c], vg, pv);
+                for (int k = 0; k < 3; ++k) vfree[3 * c + k] = dot3(pv, cs[c].dir[k]);
+            }
+            for (int col = 0; col < K; ++col) {
+                const Contact *C = &cs[col / 3];
+                V6 fi[MAXG];
+                memset(fi, 0, sizeof(V6) * G);
+                V3 dl, rxd;
+                m3T_v(w.Rw[C->g], C->dir[col % 3], dl);
+                cross3(C->r, dl, rxd);
+                for (int k = 0; k < 3; ++k) { fi[C->g][k] = rxd[k]; fi[C->g][3 + k] = dl[k]; }
+                real dqd[MAXD] = {0};
+                V6 dv0, dvg[MAXG];
+                impulse_response(&e, &w, fi, dqd, dv0);
+                group_vels(m, &w, dqd, dv0, dvg);
+                for (int c = 0; c < nc; ++c) {
+                    V3 pv;
+                    point_vel(&w, &cs[c], dvg, pv);
+                    for (int k = 0; k < 3; ++k) W[3 * c + k][col] = dot3(pv, cs[c].dir[k]);
+                }
+            }
+            memset(lam, 0, sizeof(real) * K);
+            for (int it = 0; it < sp->contact_iterations; ++it) {
+                for (int c = 0; c < nc; ++c) {
+                    int i = 3 * c;
+                    real vn = vfree[i];
+                    for (int j = 0; j < K; ++j) vn += W[i][j] * lam[j];
+                    real ln = lam[i] + (cs[c].target - vn) / W[i][i];
+                    lam[i] = ln > 0 ? ln : 0;
+                    for (int t = 1; t < 3; ++t) {
+                        real vt = vfree[i + t];
+                        for (int j = 0; j < K; ++j) vt += W[i + t][j] * lam[j];
+                        lam[i + t] -= vt / W[i + t][i + t];
+                    }
+                    real lt = sqrt(lam[i + 1] * lam[i + 1] + lam[i + 2] * lam[i + 2]), lim = cs[c].mu * lam[i];
+                    if (lt > lim) {
+                        real sc = lt > 0 ? lim / lt : 0;
+                        lam[i + 1] *= sc;
+                        lam[i + 2] *= sc;
+                    }
+                }
+            }
+            V6 fi[MAXG];
+            memset(fi, 0, sizeof(V6) * G);
+            for (int c = 0; c < nc; ++c) {
+                V3 dw = {0, 0, 0}, dl, rxd;
+                for (int k = 0; k < 3; ++k)
+                    for (int j = 0; j < 3; ++j) dw[j] += lam[3 * c + k] * cs[c].dir[k][j];
+                m3T_v(w.Rw[cs[c].g], dw, dl);
+                cross3(cs[c].r, dl, rxd);
+                for (int k = 0; k < 3; ++k) { fi[cs[c].g][k] += rxd[k]; fi[cs[c].g][3 + k] += dl[k]; }
+            }
+            real dqd[MAXD] = {0};
+            V6 dv0;
+            impulse_response(&e, &w, fi, dqd, dv0);
+            for (int g = 1; g < G; ++g) qds[w.gdof[g]] += dqd[w.gdof[g]];
+            for (int k = 0; k < 6; ++k) v0s[k] += dv0[k];
+        }
+        /* velocity limits, integrate */
+        for (int g = 1; g < G; ++g) {
+            int d = w.gdof[g];
+            real vl = props[TG_PROP_VELOCITY * prop_stride + d];
+            if (vl > 0) qds[d] = qds[d] > vl ? vl : (qds[d] < -vl ? -vl : qds[d]);
+            qd[d] = qds[d];
+            q[d] += h * qd[d];
+        }
+        if (!sp->fix_base) {
+            memcpy(v0, v0s, sizeof v0);
+            V3 vbw, vbl = {v0[3], v0[4], v0[5]};
+            m3_v(R, vbl, vbw);
+            for (int k = 0; k < 3; ++k) pos[k] += h * vbw[k];
+            /* q <- q * exp(h w_b / 2) */
+            real wx = v0[0], wy = v0[1], wz = v0[2], an = sqrt(wx * wx + wy * wy + wz * wz) * h;
+            real dq[4] = {0, 0, 0, 1};
+            if (an > 1e-12) {
+                real sa = sin(an / 2) / (an / h);
+                dq[0] = wx * sa; dq[1] = wy * sa; dq[2] = wz * sa; dq[3] = cos(an / 2);
+            }
+            real x1 = quat[0], y1 = quat[1], z1 = quat[2], w1 = quat[3];
+            real x2 = dq[0], y2 = dq[1], z2 = dq[2], w2 = dq[3];
+            quat[0] = w1 * x2 + x1 * w2 + y1 * z2 - z1 * y2;
+            quat[1] = w1 * y2 - x1 * z2 + y1 * w2 + z1 * x2;
+            quat[2] = w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2;
+            quat[3] = w1 * w2 - x1 * x2 - y1 * y2 - z1 * z2;
+            qn = sqrt(quat[0] * quat[0] + quat[1] * quat[1] + quat[2] * quat[2] + quat[3] * quat[3]);
+            for (int k = 0; k < 4; ++k) quat[k] /= qn;
+            quat_to_m3(quat, R);
+        }
+    }
+    /* write back: root pose, com velocity (world), angular velocity (world) */
+    V3 wbw, vow, wb2 = {v0[0], v0[1], v0[2]}, vb2 = {v0[3], v0[4], v0[5]};
+    m3_v(R, wb2, wbw);
+    m3_v(R, vb2, vow);
+    m3_v(R, c0, c0w);
+    cross3(wbw, c0w, wxc);
+    for (int k = 0; k < 3; ++k) {
+        root[k] = (float)pos[k];
+        root[7 + k] = (float)(vow[k] + wxc[k]);
+        root[10 + k] = (float)wbw[k];
+    }
+    for (int k = 0; k < 4; ++k) root[3 + k] = (float)quat[k];
+    for (int d = 0; d < D; ++d) {
+        if (m->dof_locked[d]) {
+            dof[2 * d] = (float)lockq[d];
+            dof[2 * d + 1] = 0.0f;
+        } else {
+            dof[2 * d] = (float)q[d];
+            dof[2 * d + 1] = (float)qd[d];
+        }
+    }
+}
+
+/* Batched driver: state arrays in the tgsim.h layouts. */
+void oracle_physics_step(const tg_model_desc *m, const tg_sim_params *sp, int n, float *root, float *dof,
+                         const float *props, const float *pos_tgt, const float *vel_tgt, const float *act,
+                         const float *force, const float *mass_scale, const float *mu, const float *gravity,
+                         int nthreads) {
+    int D = m->num_dofs;
+    long stride = (long)n * D;   /* props are [F][N][D] */
+#pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1)
+    for (int e = 0; e < n; ++e) {
+        oracle_physics_step_env(m, sp, root + 13 * (long)e, dof + 2 * (long)e * D, props + (long)e * D, stride,
+                                pos_tgt + (long)e * D, vel_tgt + (long)e * D, act ? act + (long)e * D : NULL,
+                                force ? force + 6L * e * m->num_groups : NULL,
+                                mass_scale ? mass_scale + (long)e * m->num_links : NULL, mu + (long)e * m->num_shapes,
+                                gravity);
+    }
+}

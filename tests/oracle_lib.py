@@ -1,0 +1,53 @@
+"""ctypes loader for the CPU oracle (oracle/_build/liboracle.so) -- test infrastructure.
+
+Builds the oracle with ``make -C oracle`` on first use if the shared object is
+missing.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+import this module."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(REPO, "oracle", "_build", "liboracle.so")
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        srcs = [os.path.join(REPO, "oracle", f) for f in ("gogoro_task.c", "physics_ref.c")]
+        if not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in srcs):
+            subprocess.run(["make", "-C", os.path.join(REPO, "oracle")], check=True, capture_output=True)
+        _lib = C.CDLL(LIB)
+        vp = C.c_void_p
+        _lib.oracle_gogoro_observations.argtypes = [C.c_int, vp, vp, vp, vp]
+        _lib.oracle_gogoro_reward.argtypes = [C.c_int, vp, vp, vp, C.c_int64, vp, vp]
+        _lib.oracle_gogoro_pre_physics.argtypes = [vp, vp, vp, vp]
+        _lib.oracle_gogoro_post_physics.argtypes = [vp, vp, vp, vp, vp, vp]
+        _lib.oracle_physics_step.argtypes = [vp, vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_int]
+    return _lib
+
+
+def ptr(a):
+    if a is None:
+        return None
+    assert isinstance(a, np.ndarray) and a.flags.c_contiguous, "oracle arrays must be C-contiguous numpy"
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def physics_step(desc, sp, root, dof, props, pos_tgt, vel_tgt, act=None, force=None, mass_scale=None, mu=None,
+                 gravity=None, threads=1):
+    """One control step of the fp64 oracle engine, in place on root/dof."""
+    n = root.shape[0]
+    if mu is None:
+        mu = np.ascontiguousarray(np.broadcast_to(desc.arrays["shape_friction"], (n, len(desc.arrays["shape_friction"]))),
+                                  dtype=np.float32)
+    if gravity is None:
+        gravity = np.array(list(sp.gravity), np.float32)
+    lib().oracle_physics_step(C.byref(desc.desc), C.byref(sp), n, ptr(root), ptr(dof), ptr(props), ptr(pos_tgt),
+                              ptr(vel_tgt), ptr(act), ptr(force), ptr(mass_scale), ptr(mu), ptr(gravity), threads)

@@ -1,0 +1,65 @@
+"""Gogoro cfg -> kernel parameter block (include/tg_gogoro.h), library-free.
+
+Mirrors how the reference reads its cfg in ``Gogoro.__init__``
+(tasks/gogoro_new.py:38-68) and fills the locked reset pose in
+``_create_envs`` (:233-262)."""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from ..abi import tg_gogoro_params
+
+NOISE_KEYS = {
+    "steering_action_noise": "steering_action_noise", "imu_filter_noise": "imu_filter_noise",
+    "imu_noise": "imu_noise", "speed_sensor_noise": "speed_sensor_noise", "speed_range": "speed_range",
+    "steering_offset": "steering_offset", "speed_sensor_offset": "speed_sensor_offset",
+    "seat_offset_x_range": "seat_offset_x_range", "seat_offset_y_range": "seat_offset_y_range",
+    "seat_offset_z_range": "seat_offset_z_range", "seat_offset_xr_range": "seat_offset_xr_range",
+    "steering_damping_range": "steering_damping_range",
+}
+
+
+def gogoro_params(cfg: dict, dof_name_to_id: dict, num_envs: int, seed: int = 0) -> tg_gogoro_params:
+    nz = cfg["noises"]
+    p = tg_gogoro_params()
+    p.max_steering, p.max_steering_change = 0.5, 0.2            # gogoro_new.py:86-87
+    for field, key in NOISE_KEYS.items():
+        getattr(p, field)[:] = [float(x) for x in nz[key]]
+    p.spawn_z = 0.03                                            # :537
+    p.steer_stiffness, p.steer_effort, p.steer_velocity = 3000.0, 100.0, 200.0   # :578,599,600
+    env = cfg["env"]
+    p.clip_obs = float(env.get("clipObservations", math.inf))   # vec_task.py:107
+    p.clip_actions = float(env.get("clipActions", math.inf))    # vec_task.py:108
+    p.max_episode_length = int(env["max_steps"])
+    p.speed_freq_update = int(nz["speed_freq_update"])
+    p.yaw_freq_update = int(nz["yaw_freq_update"])
+    p.num_envs = int(num_envs)
+    p.num_dof = len(dof_name_to_id)
+    p.dof_steer = int(dof_name_to_id["steering_joint"])
+    p.dof_rear = int(dof_name_to_id["rear_wheel_joint"])
+    p.dof_base_x = int(dof_name_to_id["base_x"])
+    p.dof_base_y = int(dof_name_to_id["base_y"])
+    p.dof_base_z = int(dof_name_to_id["base_z"])
+    p.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    return p
+
+
+def thormang_pose(cfg: dict, dof_name_to_id: dict) -> np.ndarray:
+    """Reset DOF pose: lower + 0.0001/2 for every locked joint (gogoro_new.py:257-262),
+    in the reference's float32 arithmetic; 0 elsewhere."""
+    pose = np.zeros(len(dof_name_to_id), np.float32)
+    for name, val in cfg["joints_pos"].items():
+        lower = np.float32(val)
+        pose[dof_name_to_id[name]] = lower + np.float32(0.0001 / 2)
+    return pose
+
+
+def lock_window(cfg: dict, dof_name_to_id: dict, lower: np.ndarray, upper: np.ndarray) -> None:
+    """Apply the joints_pos lock windows [v, v+1e-4] to [.., D] limit arrays in place (:257-261)."""
+    for name, val in cfg["joints_pos"].items():
+        d = dof_name_to_id[name]
+        lo = np.float32(val)
+        lower[..., d] = lo
+        upper[..., d] = lo + np.float32(0.0001)
