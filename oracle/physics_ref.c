@@ -511,17 +511,51 @@ static void impulse_response(const Env *e, Work *w, const V6 *fi, real *dqd, V6 
     }
 }
 
+/* Contact rows.  Per shape, the active points (closest torus point, sphere
+ * bottom, box corners within the speculative margin) each get a NORMAL row;
+ * the shape's points form one friction patch (PhysX-style patch friction)
+ * with two tangent rows at the patch centroid, coupled by a Coulomb cone
+ * mu*sum(normal), and one torsional row about the normal limited by
+ * mu*sum(normal)*r_eff. */
+enum { ROW_NORMAL = 0, ROW_T1 = 1, ROW_T2 = 2, ROW_TORSION = 3 };
 typedef struct {
-    int g;           /* group */
-    V3 r;            /* contact point in group frame */
-    V3 dir[3];       /* world: normal, t1, t2 */
-    real target;     /* normal velocity lower bound */
-    real mu;
-} Contact;
+    int g, type, angular, patch;
+    V3 r;            /* application point in group frame (linear rows) */
+    V3 d;            /* world direction (force) or axis (moment) */
+    real target;     /* normal rows: velocity lower bound */
+} Row;
+typedef struct {
+    int n0, nn;      /* first normal row, number of normal rows */
+    int f0;          /* first of the 3 friction rows */
+    real mu, reff;
+} Patch;
 
-static int collect_contacts(const Env *e, Work *w, real h, Contact *cs) {
+static void row_force(const Work *w, const Row *r, real lam, V6 *fi) {
+    V3 dl, rxd;
+    m3T_v(w->Rw[r->g], r->d, dl);
+    if (r->angular) {
+        for (int k = 0; k < 3; ++k) fi[r->g][k] += lam * dl[k];
+    } else {
+        cross3(r->r, dl, rxd);
+        for (int k = 0; k < 3; ++k) { fi[r->g][k] += lam * rxd[k]; fi[r->g][3 + k] += lam * dl[k]; }
+    }
+}
+static real row_vel(const Work *w, const Row *r, const V6 *vg) {
+    V3 om = {vg[r->g][0], vg[r->g][1], vg[r->g][2]}, vl = {vg[r->g][3], vg[r->g][4], vg[r->g][5]}, loc, out;
+    if (r->angular) {
+        m3_v(w->Rw[r->g], om, out);
+    } else {
+        V3 wxr;
+        cross3(om, r->r, wxr);
+        for (int k = 0; k < 3; ++k) loc[k] = vl[k] + wxr[k];
+        m3_v(w->Rw[r->g], loc, out);
+    }
+    return dot3(out, r->d);
+}
+
+static int collect_rows(const Env *e, Work *w, real h, Row *rows, Patch *patches, int *npatch) {
     const tg_model_desc *m = e->m;
-    int nc = 0;
+    int nr = 0, np_ = 0;
     for (int s = 0; s < m->num_shapes; ++s) {
         int g = w->shg[s];
         M3 R;
@@ -529,7 +563,6 @@ static int collect_contacts(const Env *e, Work *w, real h, Contact *cs) {
         m3_mul(w->Rw[g], w->shR[s], R);
         m3_v(w->Rw[g], w->shp[s], c);
         for (int k = 0; k < 3; ++k) c[k] += w->pw[g][k];
-        real mu = 0.5 * (e->mu[s] + e->sp->ground_friction);
         V3 pts[8];
         int np = 0;
         if (m->shape_kind[s] == TG_SHAPE_TORUS) {
@@ -554,44 +587,119 @@ static int collect_contacts(const Env *e, Work *w, real h, Contact *cs) {
                 ++np;
             }
         }
-        for (int k = 0; k < np && nc < MAXC; ++k) {
+        Patch *P = &patches[np_];
+        P->n0 = nr;
+        P->nn = 0;
+        V3 cen = {0, 0, 0};
+        for (int k = 0; k < np; ++k) {
             real phi = pts[k][2];
             if (phi > e->sp->contact_margin) continue;
-            Contact *C = &cs[nc++];
-            C->g = g;
+            Row *r = &rows[nr++];
+            r->g = g; r->type = ROW_NORMAL; r->angular = 0; r->patch = np_;
             V3 rel;
             for (int j = 0; j < 3; ++j) rel[j] = pts[k][j] - w->pw[g][j];
-            m3T_v(w->Rw[g], rel, C->r);
-            C->dir[0][0] = 0; C->dir[0][1] = 0; C->dir[0][2] = 1;
-            /* t1: rolling direction for tori (axis x n), else world x */
-            V3 t1 = {1, 0, 0};
-            if (m->shape_kind[s] == TG_SHAPE_TORUS) {
-                V3 a = {R[2], R[5], R[8]}, n = {0, 0, 1}, x;
-                cross3(a, n, x);
-                real nx = sqrt(dot3(x, x));
-                if (nx > 1e-6) for (int j = 0; j < 3; ++j) t1[j] = x[j] / nx;
-            }
-            memcpy(C->dir[1], t1, sizeof t1);
-            V3 n = {0, 0, 1};
-            cross3(n, t1, C->dir[2]);
+            m3T_v(w->Rw[g], rel, r->r);
+            r->d[0] = 0; r->d[1] = 0; r->d[2] = 1;
             real rest = e->sp->rest_offset;
-            if (phi > rest) C->target = -(phi - rest) / h;
+            if (phi > rest) r->target = -(phi - rest) / h;
             else {
-                C->target = e->sp->baumgarte * (rest - phi) / h;
-                if (C->target > e->sp->max_depenetration_velocity) C->target = e->sp->max_depenetration_velocity;
+                r->target = e->sp->baumgarte * (rest - phi) / h;
+                if (r->target > e->sp->max_depenetration_velocity) r->target = e->sp->max_depenetration_velocity;
             }
-            C->mu = mu;
+            for (int j = 0; j < 3; ++j) cen[j] += pts[k][j];
+            P->nn++;
         }
+        if (P->nn == 0) continue;
+        for (int j = 0; j < 3; ++j) cen[j] /= P->nn;
+        P->reff = 0;
+        for (int k = P->n0; k < P->n0 + P->nn; ++k) {
+            V3 pw_;
+            m3_v(w->Rw[g], rows[k].r, pw_);
+            real dx = pw_[0] + w->pw[g][0] - cen[0], dy = pw_[1] + w->pw[g][1] - cen[1];
+            P->reff += sqrt(dx * dx + dy * dy) / P->nn;
+        }
+        P->mu = 0.5 * (e->mu[s] + e->sp->ground_friction);
+        /* tangent basis: rolling direction for tori (axis x n), else world x */
+        V3 t1 = {1, 0, 0}, n = {0, 0, 1}, t2;
+        if (m->shape_kind[s] == TG_SHAPE_TORUS) {
+            V3 a = {R[2], R[5], R[8]}, x;
+            cross3(a, n, x);
+            real nx = sqrt(dot3(x, x));
+            if (nx > 1e-6) for (int j = 0; j < 3; ++j) t1[j] = x[j] / nx;
+        }
+        cross3(n, t1, t2);
+        P->f0 = nr;
+        V3 rel, rl;
+        for (int j = 0; j < 3; ++j) rel[j] = cen[j] - w->pw[g][j];
+        m3T_v(w->Rw[g], rel, rl);
+        for (int t = 0; t < 3; ++t) {
+            Row *r = &rows[nr++];
+            r->g = g; r->type = ROW_T1 + t; r->angular = (t == 2); r->patch = np_; r->target = 0;
+            memcpy(r->r, rl, sizeof rl);
+            memcpy(r->d, t == 0 ? t1 : (t == 1 ? t2 : n), sizeof(V3));
+        }
+        ++np_;
     }
-    return nc;
+    *npatch = np_;
+    return nr;
 }
 
-/* world-frame velocity of a contact point for group velocities vg */
-static void point_vel(const Work *w, const Contact *C, const V6 *vg, V3 out) {
-    V3 om = {vg[C->g][0], vg[C->g][1], vg[C->g][2]}, vl = {vg[C->g][3], vg[C->g][4], vg[C->g][5]}, wxr, loc;
-    cross3(om, C->r, wxr);
-    for (int k = 0; k < 3; ++k) loc[k] = vl[k] + wxr[k];
-    m3_v(w->Rw[C->g], loc, out);
+static void solve_contacts(const Env *e, Work *w, real h, real *qds, V6 v0s) {
+    const tg_model_desc *m = e->m;
+    int G = m->num_groups;
+    Row rows[3 * MAXC];
+    Patch patches[MAXC];
+    int npatch = 0;
+    int K = collect_rows(e, w, h, rows, patches, &npatch);
+    if (K == 0) return;
+    static __thread real W[3 * MAXC][3 * MAXC];
+    real vfree[3 * MAXC], lam[3 * MAXC];
+    V6 vg[MAXG];
+    group_vels(m, w, qds, v0s, vg);
+    for (int i = 0; i < K; ++i) vfree[i] = row_vel(w, &rows[i], vg);
+    for (int col = 0; col < K; ++col) {
+        V6 fi[MAXG];
+        memset(fi, 0, sizeof(V6) * G);
+        row_force(w, &rows[col], 1.0, fi);
+        real dqd[MAXD] = {0};
+        V6 dv0, dvg[MAXG];
+        impulse_response(e, w, fi, dqd, dv0);
+        group_vels(m, w, dqd, dv0, dvg);
+        for (int i = 0; i < K; ++i) W[i][col] = row_vel(w, &rows[i], dvg);
+    }
+    memset(lam, 0, sizeof(real) * K);
+#define ROWV(i) ({ real v_ = vfree[i]; for (int j_ = 0; j_ < K; ++j_) v_ += W[i][j_] * lam[j_]; v_; })
+    for (int it = 0; it < e->sp->contact_iterations; ++it) {
+        for (int p = 0; p < npatch; ++p) {
+            Patch *P = &patches[p];
+            real N = 0;
+            for (int i = P->n0; i < P->n0 + P->nn; ++i) {
+                real l = lam[i] + (rows[i].target - ROWV(i)) / W[i][i];
+                lam[i] = l > 0 ? l : 0;
+                N += lam[i];
+            }
+            int f = P->f0;
+            lam[f] -= ROWV(f) / W[f][f];
+            lam[f + 1] -= ROWV(f + 1) / W[f + 1][f + 1];
+            real lt = sqrt(lam[f] * lam[f] + lam[f + 1] * lam[f + 1]), lim = P->mu * N;
+            if (lt > lim) {
+                real sc = lt > 0 ? lim / lt : 0;
+                lam[f] *= sc;
+                lam[f + 1] *= sc;
+            }
+            real lt3 = lam[f + 2] - ROWV(f + 2) / W[f + 2][f + 2], lim3 = P->mu * N * P->reff;
+            lam[f + 2] = lt3 > lim3 ? lim3 : (lt3 < -lim3 ? -lim3 : lt3);
+        }
+    }
+#undef ROWV
+    V6 fi[MAXG];
+    memset(fi, 0, sizeof(V6) * G);
+    for (int i = 0; i < K; ++i) row_force(w, &rows[i], lam[i], fi);
+    real dqd[MAXD] = {0};
+    V6 dv0;
+    impulse_response(e, w, fi, dqd, dv0);
+    for (int g = 1; g < G; ++g) qds[w->gdof[g]] += dqd[w->gdof[g]];
+    for (int k = 0; k < 6; ++k) v0s[k] += dv0[k];
 }
 
 /* One env, one control step (all substeps).  root[13], dof[2D] updated in place. */
@@ -639,75 +747,12 @@ void oracle_physics_step_env(const tg_model_desc *m, const tg_sim_params *sp, fl
         memcpy(qds, qd, sizeof(real) * D);
         for (int g = 1; g < G; ++g) qds[w.gdof[g]] = qd[w.gdof[g]] + h * qdd[w.gdof[g]];
         for (int k = 0; k < 6; ++k) v0s[k] = v0[k] + h * a0[k];
-        /* contacts */
-        Contact cs[MAXC];
-        int nc = collect_contacts(&e, &w, h, cs);
-        if (nc > 0) {
-            int K = 3 * nc;
-            static __thread real W[3 * MAXC][3 * MAXC];
-            real vfree[3 * MAXC], lam[3 * MAXC];
-            V6 vg[MAXG];
-            group_vels(m, &w, qds, v0s, vg);
-            for (int c = 0; c < nc; ++c) {
-                V3 pv;
-                point_vel(&w, &cs[c], vg, pv);
-                for (int k = 0; k < 3; ++k) vfree[3 * c + k] = dot3(pv, cs[c].dir[k]);
-            }
-            for (int col = 0; col < K; ++col) {
-                const Contact *C = &cs[col / 3];
-                V6 fi[MAXG];
-                memset(fi, 0, sizeof(V6) * G);
-                V3 dl, rxd;
-                m3T_v(w.Rw[C->g], C->dir[col % 3], dl);
-                cross3(C->r, dl, rxd);
-                for (int k = 0; k < 3; ++k) { fi[C->g][k] = rxd[k]; fi[C->g][3 + k] = dl[k]; }
-                real dqd[MAXD] = {0};
-                V6 dv0, dvg[MAXG];
-                impulse_response(&e, &w, fi, dqd, dv0);
-                group_vels(m, &w, dqd, dv0, dvg);
-                for (int c = 0; c < nc; ++c) {
-                    V3 pv;
-                    point_vel(&w, &cs[c], dvg, pv);
-                    for (int k = 0; k < 3; ++k) W[3 * c + k][col] = dot3(pv, cs[c].dir[k]);
-                }
-            }
-            memset(lam, 0, sizeof(real) * K);
-            for (int it = 0; it < sp->contact_iterations; ++it) {
-                for (int c = 0; c < nc; ++c) {
-                    int i = 3 * c;
-                    real vn = vfree[i];
-                    for (int j = 0; j < K; ++j) vn += W[i][j] * lam[j];
-                    real ln = lam[i] + (cs[c].target - vn) / W[i][i];
-                    lam[i] = ln > 0 ? ln : 0;
-                    for (int t = 1; t < 3; ++t) {
-                        real vt = vfree[i + t];
-                        for (int j = 0; j < K; ++j) vt += W[i + t][j] * lam[j];
-                        lam[i + t] -= vt / W[i + t][i + t];
-                    }
-                    real lt = sqrt(lam[i + 1] * lam[i + 1] + lam[i + 2] * lam[i + 2]), lim = cs[c].mu * lam[i];
-                    if (lt > lim) {
-                        real sc = lt > 0 ? lim / lt : 0;
-                        lam[i + 1] *= sc;
-                        lam[i + 2] *= sc;
-                    }
-                }
-            }
-            V6 fi[MAXG];
-            memset(fi, 0, sizeof(V6) * G);
-            for (int c = 0; c < nc; ++c) {
-                V3 dw = {0, 0, 0}, dl, rxd;
-                for (int k = 0; k < 3; ++k)
-                    for (int j = 0; j < 3; ++j) dw[j] += lam[3 * c + k] * cs[c].dir[k][j];
-                m3T_v(w.Rw[cs[c].g], dw, dl);
-                cross3(cs[c].r, dl, rxd);
-                for (int k = 0; k < 3; ++k) { fi[cs[c].g][k] += rxd[k]; fi[cs[c].g][3 + k] += dl[k]; }
-            }
-            real dqd[MAXD] = {0};
-            V6 dv0;
-            impulse_response(&e, &w, fi, dqd, dv0);
-            for (int g = 1; g < G; ++g) qds[w.gdof[g]] += dqd[w.gdof[g]];
-            for (int k = 0; k < 6; ++k) v0s[k] += dv0[k];
+        {   /* classical (world-fixed) linear acceleration: spatial + w x v */
+            V3 wv = {v0[0], v0[1], v0[2]}, vv = {v0[3], v0[4], v0[5]}, wxv;
+            cross3(wv, vv, wxv);
+            for (int k = 0; k < 3; ++k) v0s[3 + k] += h * wxv[k];
         }
+        solve_contacts(&e, &w, h, qds, v0s);
         /* velocity limits, integrate */
         for (int g = 1; g < G; ++g) {
             int d = w.gdof[g];
@@ -737,6 +782,13 @@ void oracle_physics_step_env(const tg_model_desc *m, const tg_sim_params *sp, fl
             qn = sqrt(quat[0] * quat[0] + quat[1] * quat[1] + quat[2] * quat[2] + quat[3] * quat[3]);
             for (int k = 0; k < 4; ++k) quat[k] /= qn;
             quat_to_m3(quat, R);
+            /* re-express the world-fixed velocity in the rotated body frame: v <- Rot(dq)^T v */
+            M3 Rd;
+            quat_to_m3(dq, Rd);
+            V3 wv = {v0[0], v0[1], v0[2]}, vv = {v0[3], v0[4], v0[5]};
+            m3T_v(Rd, wv, wv);
+            m3T_v(Rd, vv, vv);
+            for (int k = 0; k < 3; ++k) { v0[k] = wv[k]; v0[3 + k] = vv[k]; }
         }
     }
     /* write back: root pose, com velocity (world), angular velocity (world) */

@@ -157,7 +157,7 @@ def default_dof_props(m: Model, num_envs: int) -> np.ndarray:
         p[TG_PROP_UPPER, d] = j.upper if j.has_limits else 3.4e38
         p[TG_PROP_EFFORT, d] = j.effort
         p[TG_PROP_VELOCITY, d] = j.velocity
-    return np.ascontiguousarray(np.broadcast_to(p[:, None, :], (TG_NUM_PROPS, num_envs, D)))
+    return np.repeat(p[:, None, :], num_envs, axis=1)
 
 
 def sim_params_from_cfg(cfg_sim: dict, asset_opts: dict | None = None, num_envs: int = 1,
