@@ -1,0 +1,168 @@
+"""Env-steps/sec of the full VecTask.step hot path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--task Gogoro] [--num-envs 4096]
+
+One process per GPU (torchrun for N>1, RANK/LOCAL_RANK/WORLD_SIZE from the
+env); every rank owns its own env batch (weak scaling, no collective on the
+hot path).  A "step" is one ``env.step(actions)`` call: pre-physics kernel,
+``sim.substeps`` articulation substeps, post-physics kernel (observations,
+reward, masked resets, timeouts) -- inputs resident in HBM, synthetic
+actions U(-1,1) from torch.Generator(seed 1234 + rank).  Rank 0 prints one
+JSON line; ``value`` = envs x steps x ranks / max-over-ranks wall time.
+
+Roofline: the dominant kernel is the articulation step kernel; its average
+launch time is measured with HIP events on the sim stream over the timed
+region, and its algorithmic bytes per env-step (state + inputs the kernel
+must read/write) give the achieved HBM rate against the
+8 TB/s MI355X peak.  cpu_baseline: the CPU oracle env (oracle/, fp64 physics +
+task restatement, OpenMP) on a bounded sample of the same workload, rank 0 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0
+
+
+def kernel_bytes_per_env(task_name: str, env) -> int:
+    """Algorithmic HBM bytes one articulation step reads + writes per env
+    (DESIGN.md §Roofline): root state r/w, dof_state r/w, active-dof targets and
+    properties, locked-dof lock windows, per-env composite cache, shape friction."""
+    m = env.sim.model
+    D, G, S = m.num_dof, m.num_groups, len(m.shapes)
+    na = len(m.active_dofs)
+    nl = len(m.locked_dofs)
+    kc = 10 * G + 12 * (G - 1) + 12 * S
+    read = 13 * 4 + na * 2 * 4 + na * 2 * 4 + na * 8 * 4 + nl * 2 * 4 + kc * 4 + S * 4 + 1
+    write = 13 * 4 + D * 2 * 4
+    return read + write
+
+
+def cpu_baseline(task_name: str, num_envs: int, threads: int):
+    from tests.gpu_harness import NumpyDraws, OracleGogoro, parity_cfg
+    cfg = parity_cfg(num_envs)
+    env = OracleGogoro(cfg, NumpyDraws(0), threads=threads)
+    rs = np.random.default_rng(1234)
+    steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 10.0 and steps < 400:
+        env.step(rs.uniform(-1, 1, num_envs).astype(np.float32))
+        steps += 1
+    dt = time.perf_counter() - t0
+    return {"value": num_envs * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{task_name} {num_envs} envs x {steps} steps (oracle/ fp64 physics + C task restatement, "
+                      f"OpenMP {threads} threads) = {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--task", default="Gogoro")
+    ap.add_argument("--num-envs", type=int, default=4096)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group(backend="nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = f"cuda:{local}"
+
+    import thormang_isaacgym_amd as tia
+    from thormang_isaacgym_amd.cfg import load_task_cfg
+    cfg = load_task_cfg(args.task, num_envs=args.num_envs, sim_device=dev)
+    env = tia.make(seed=42 + rank, task=args.task, num_envs=args.num_envs, sim_device=dev, rl_device=dev, cfg=cfg)
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    N = args.num_envs
+    acts = env.num_actions
+
+    def step():
+        a = torch.rand(N, acts, device=dev, generator=gen) * 2 - 1
+        return env.step(a)
+
+    for _ in range(args.warmup):
+        step()
+    # kernel timing: events around every simulate() on the sim stream
+    ev = []
+    orig_sim = env.simulate
+
+    def timed_sim():
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        orig_sim()
+        e.record()
+        ev.append((s, e))
+
+    env.simulate = timed_sim
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    env.simulate = orig_sim
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank != 0:
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+    value = N * args.steps * world / elapsed
+    bpe = kernel_bytes_per_env(args.task, env)
+    achieved = bpe * N / (kern_ms * 1e-3) / 1e9
+    sim_cfg = cfg["sim"]
+    out = {
+        "metric": "env-steps/sec (num_envs x step Hz)",
+        "value": value,
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (actions U(-1,1), seed 1234+rank; model compiled from the reference URDF)",
+        "config": {"workload": f"{args.task} {N} envs/GPU, flat ground, dt {sim_cfg['dt']} s x "
+                               f"{sim_cfg.get('substeps', 2)} substeps ({1.0 / sim_cfg['dt']:.1f} Hz control)",
+                   "num_envs_per_gpu": N, "parallelism": f"env-dp{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "tg::step_kernel (+compose) per simulate()", "kernel_ms": kern_ms,
+                     "bytes_per_env_step": bpe},
+    }
+    if not args.no_cpu_baseline and world == 1:
+        try:
+            out["cpu_baseline"] = cpu_baseline(args.task, N, threads=min(16, os.cpu_count() or 1))
+        except Exception as exc:  # baseline is reported, never the measured value
+            out["cpu_baseline"] = {"value": None, "error": repr(exc)}
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -103,6 +103,24 @@ typedef struct tg_gogoro_buffers {
     uint8_t *env_dirty;      /* [N] set when per-env props changed (sim recomposes) */
 } tg_gogoro_buffers;
 
+/* Gogoro.pre_physics_step (gogoro_new.py:347-369) + VecTask action clamp
+ * (vec_task.py:327).  actions [N] (the [N,1] action tensor), pre_draws [N] or NULL. */
+int tg_gogoro_pre_physics(tg_sim *sim, const tg_gogoro_params *p, const tg_gogoro_buffers *b,
+                          const float *actions, const float *pre_draws, uint64_t counter);
+
+/* Gogoro.post_physics_step + compute_obs_rwd + reset_idx (masked) + the
+ * VecTask.step tail (gogoro_new.py:373-601, vec_task.py:345-353).  Draw
+ * arrays as documented above, each NULL for in-kernel Philox draws. */
+int tg_gogoro_post_physics(tg_sim *sim, const tg_gogoro_params *p, const tg_gogoro_buffers *b,
+                           const float *reset_draws, const float *obs_draws, const float *speed_draws,
+                           const float *yaw_draws, uint64_t counter);
+
+/* Gogoro.reset_idx(env_ids) outside post_physics_step (gogoro_new.py:150,505-591;
+ * VecTask.reset_done, vec_task.py:391-406): ids [n] int32 device, reset_draws
+ * [N,11] (rows of the listed envs used) or NULL. */
+int tg_gogoro_reset_idx(tg_sim *sim, const tg_gogoro_params *p, const tg_gogoro_buffers *b, const int32_t *ids,
+                        int32_t n, const float *reset_draws, uint64_t counter);
+
 #ifdef __cplusplus
 }
 #endif

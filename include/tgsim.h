@@ -151,6 +151,11 @@ int tg_sim_create(const tg_model_desc *model, const tg_sim_params *params, int32
 int tg_sim_destroy(tg_sim *sim);
 int tg_set_stream(tg_sim *sim, void *hip_stream);
 int tg_state_ptrs(tg_sim *sim, tg_state_view *view);
+/* Adopt caller-owned device buffers (e.g. torch tensors) for any non-NULL
+ * pointer of `view` (sizes as in tg_state_view); the sim's current contents
+ * are copied into them first, so the caller's tensors become the live,
+ * zero-copy state (the gymtorch.wrap_tensor contract).  Caller keeps them alive. */
+int tg_bind_state(tg_sim *sim, const tg_state_view *view);
 int tg_refresh(tg_sim *sim);
 int tg_set_dof_position_targets(tg_sim *sim, const float *pos);
 int tg_set_dof_velocity_targets(tg_sim *sim, const float *vel);

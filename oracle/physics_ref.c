@@ -579,9 +579,16 @@ static int collect_rows(const Env *e, Work *w, real h, Row *rows, Patch *patches
             pts[0][2] -= m->shape_params[4 * s];
             np = 1;
         } else if (m->shape_kind[s] == TG_SHAPE_BOX) {
-            for (int k = 0; k < 8; ++k) {
-                V3 l = {(k & 1 ? 1 : -1) * m->shape_params[4 * s], (k & 2 ? 1 : -1) * m->shape_params[4 * s + 1],
-                        (k & 4 ? 1 : -1) * m->shape_params[4 * s + 2]}, wv;
+            /* the 4 corners of the face whose outward normal points most downward */
+            real zx = fabs(R[6]), zy = fabs(R[7]), zz = fabs(R[8]);
+            int ax = (zz >= zx && zz >= zy) ? 2 : (zy >= zx ? 1 : 0);
+            real sgn = R[6 + ax] > 0 ? -1.0 : 1.0;
+            int a1 = ax == 0 ? 1 : 0, a2 = ax == 2 ? 1 : 2;
+            for (int k = 0; k < 4; ++k) {
+                V3 l = {0, 0, 0}, wv;
+                l[ax] = sgn * m->shape_params[4 * s + ax];
+                l[a1] = (k & 1 ? 1 : -1) * m->shape_params[4 * s + a1];
+                l[a2] = (k & 2 ? 1 : -1) * m->shape_params[4 * s + a2];
                 m3_v(R, l, wv);
                 for (int j = 0; j < 3; ++j) pts[np][j] = c[j] + wv[j];
                 ++np;

@@ -1,0 +1,138 @@
+"""GPU-vs-oracle harness for the Gogoro task path (test infrastructure).
+
+``OracleGogoro`` is the CPU restatement of the whole env step: the task
+oracle (oracle/gogoro_task.c) around the fp64 physics oracle
+(oracle/physics_ref.c), driven exactly like the product ``Gogoro`` class.
+Both sides take their random draws from identically seeded ``NumpyDraws``
+sources in the reference's call order, so any difference is numerics."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from tests.oracle_lib import lib, physics_step, ptr
+from thormang_isaacgym_amd import abi
+from thormang_isaacgym_amd.cfg import load_task_cfg
+from thormang_isaacgym_amd.model.urdf import Model
+from thormang_isaacgym_amd.tasks.gogoro_cfg import ASSET_OPTIONS, env_origins, gogoro_params, initial_dof_props, \
+    thormang_pose
+from thormang_isaacgym_amd.tasks.gogoro_draws import post_draws, reset_draws
+
+
+class NumpyDraws:
+    """DrawSource over a seeded numpy generator (U[0,1) and N(0,1), float32)."""
+
+    def __init__(self, seed):
+        self.rs = np.random.default_rng(seed)
+
+    def uniform(self, n):
+        return self.rs.random(n, dtype=np.float32)
+
+    def normal(self, n):
+        return self.rs.standard_normal(n, dtype=np.float32)
+
+
+def parity_cfg(num_envs, max_steps=1000, freq=300):
+    cfg = load_task_cfg("Gogoro", num_envs=num_envs)
+    cfg["env"]["max_steps"] = max_steps
+    cfg["noises"]["speed_freq_update"] = freq
+    cfg["noises"]["yaw_freq_update"] = freq
+    cfg["task"]["randomization_params"] = {"frequency": 10 ** 9}   # DR off: both sides share one model
+    return cfg
+
+
+def load_gogoro_model():
+    import os
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(here, "thormang_isaacgym_amd", "model", "compiled", "gogoro.json")) as f:
+        return Model.from_json(f.read())
+
+
+class OracleGogoro:
+    def __init__(self, cfg, draws, env_spacing=1.0, threads=8):
+        self.cfg = cfg
+        self.src = draws
+        self.threads = threads
+        self.model = m = load_gogoro_model()
+        self.n = n = cfg["env"]["numEnvs"]
+        self.D = D = m.num_dof
+        self.dni = m.dof_name_to_id()
+        self.desc = abi.ModelDesc(m)
+        self.sp = abi.sim_params_from_cfg(cfg["sim"], ASSET_OPTIONS, n, env_spacing)
+        self.p = gogoro_params(cfg, self.dni, n)
+        z = lambda *s, dt=np.float32: np.zeros(s, dt)
+        self.a = dict(obs_buf=z(n, 6), rew_buf=z(n), reset_buf=np.ones(n, np.int64), progress_buf=z(n, dt=np.int64),
+                      timeout_buf=z(n, dt=np.uint8), action_history=z(n, 5), curent_command=z(n), yaw_command=z(n),
+                      curent_speed=z(n), steer_offsets=z(n), imu_offsets=z(n), speed_offset=z(n),
+                      config_vector=z(n, 5), buffer_obs=z(n, 1, 6), thormang_pose=thormang_pose(cfg, self.dni),
+                      root_reset=z(n, 13), root=z(n, 13), dof_state=z(n * D, 2), pos_target=z(n, D),
+                      vel_target=z(n, D), dof_props=initial_dof_props(m, cfg, n), env_dirty=z(n, dt=np.uint8))
+        org = env_origins(n, env_spacing)
+        a = self.a
+        a["root"][:, 0:2] = org[:, 0:2]
+        a["root"][:, 2] = 1.0
+        a["root"][:, 6] = 1.0
+        a["root_reset"][:] = a["root"]
+        a["root_reset"][:, 7:13] = 0
+        self.b = abi.tg_gogoro_buffers(**{k: v.ctypes.data for k, v in a.items()})
+        lo, hi = cfg["noises"]["speed_range"]
+        a["curent_speed"][:] = np.float32(lo) + draws.uniform(n) * np.float32(hi - lo)
+        rd = reset_draws(draws, np.arange(n), n)
+        lib().oracle_gogoro_reset_env.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+        for e in range(n):
+            lib().oracle_gogoro_reset_env(C.byref(self.p), C.byref(self.b), e, ptr(np.ascontiguousarray(rd[e])))
+        a["obs_buf"][:] = 0
+        a["buffer_obs"][:] = 0
+
+    def step(self, actions):
+        a, n = self.a, self.n
+        pre = self.src.normal(n)
+        lib().oracle_gogoro_pre_physics(C.byref(self.p), C.byref(self.b), ptr(np.ascontiguousarray(actions, np.float32)),
+                                        ptr(pre))
+        physics_step(self.desc, self.sp, a["root"], a["dof_state"], a["dof_props"], a["pos_target"], a["vel_target"],
+                     threads=self.threads)
+        ids = np.nonzero(a["reset_buf"])[0]
+        rd, od, sd, yd = post_draws(self.src, ids, a["progress_buf"].copy(), self.p.speed_freq_update,
+                                    self.p.yaw_freq_update)
+        lib().oracle_gogoro_post_physics(C.byref(self.p), C.byref(self.b), ptr(rd), ptr(od), ptr(sd), ptr(yd))
+        return a["obs_buf"], a["rew_buf"], a["reset_buf"], a["timeout_buf"]
+
+
+def make_gpu_gogoro(cfg, draws, env_spacing=1.0):
+    from thormang_isaacgym_amd.tasks.gogoro import Gogoro
+
+    class ReplayGogoro(Gogoro):
+        draw_source = draws
+
+    ReplayGogoro.env_spacing = env_spacing
+    return ReplayGogoro(cfg, "cuda:0", "cuda:0", -1, True, False, False)
+
+
+def balance_policy(obs):
+    """A hand-tuned steering controller that keeps the scooter up (turn into
+    the lean), so long parity runs are not dominated by fall timing."""
+    roll, droll = obs[:, 0], obs[:, 1]
+    return np.clip(4.0 * roll + 0.8 * droll, -1.0, 1.0)[:, None].astype(np.float32)
+
+
+def gogoro_env_vs_oracle(num_envs=64, steps=20, seed=0, policy=None, max_steps=1000):
+    import torch
+    cfg = parity_cfg(num_envs, max_steps=max_steps)
+    env = make_gpu_gogoro(cfg, NumpyDraws(seed))
+    orc = OracleGogoro(parity_cfg(num_envs, max_steps=max_steps), NumpyDraws(seed))
+    err = {"obs": 0.0, "rew": 0.0, "reset_equal": True, "timeout_equal": True, "root": 0.0, "steps": steps}
+    obs_np = orc.a["obs_buf"].copy()
+    for t in range(steps):
+        act = policy(obs_np) if policy is not None else np.zeros((num_envs, 1), np.float32)
+        obs_d, rew, reset, extras = env.step(torch.from_numpy(act).to("cuda:0"))
+        o_obs, o_rew, o_reset, o_to = orc.step(act[:, 0])
+        g_obs = obs_d["obs"].cpu().numpy()
+        err["obs"] = max(err["obs"], float(np.abs(g_obs - o_obs).max()))
+        err["rew"] = max(err["rew"], float(np.abs(rew.cpu().numpy() - o_rew).max()))
+        err["root"] = max(err["root"], float(np.abs(env.root_tensor.cpu().numpy() - orc.a["root"]).max()))
+        err["reset_equal"] &= bool(np.array_equal(reset.cpu().numpy(), o_reset))
+        err["timeout_equal"] &= bool(np.array_equal(extras["time_outs"].cpu().numpy().astype(np.uint8), o_to))
+        obs_np = o_obs.copy()
+    err["resets_seen"] = int(orc.a["progress_buf"].min())
+    return err

@@ -1,0 +1,311 @@
+// gogoro_task.hip -- fused Gogoro task kernels (one env per lane).
+//
+// Replaces the reference's per-step TorchScript / Python task code
+// (isaacgymenvs/tasks/gogoro_new.py):
+//   pre_kernel  : pre_physics_step :347-369 (+ VecTask action clamp, vec_task.py:327)
+//   post_kernel : post_physics_step :373-390, compute_obs_rwd :424-462,
+//                 compute_gogoro_observations :692-723, compute_gogoro_reward :645-684,
+//                 reset_idx/randomize/generate_spawn_r/set_env_dof_prop :474-601
+//                 (masked: no nonzero(), no host sync), VecTask timeout/obs clamp
+//                 (vec_task.py:345-353).
+// Arithmetic follows the reference's fp32 operation order (this TU is built
+// with -ffp-contract=off) so results match oracle/gogoro_task.c and the
+// golden fixtures to fp32 rounding of the transcendental functions.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "tg_kernels.h"
+
+namespace tg {
+
+#define F_PI 3.14159265358979323846f
+#define F_2PI 6.28318530717958647692f
+
+__device__ __forceinline__ float t_rem(float a, float b) {
+    float m = fmodf(a, b);
+    if (m != 0.0f && ((b < 0.0f) != (m < 0.0f))) m += b;
+    return m;
+}
+__device__ __forceinline__ float t_clamp(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+__device__ __forceinline__ float u_aff(float lo, float hi, float u) { return lo + u * (hi - lo); }
+__device__ __forceinline__ float n_aff(const float *mc, float r) { return mc[0] + r * mc[1]; }
+
+__device__ __forceinline__ void observation(const float *root, float desired_yaw, float cmd, float *obs) {
+    const float x = root[3], y = root[4], z = root[5], w = root[6];
+    float roll = t_rem(atan2f(2.0f * (w * x + y * z), w * w - x * x - y * y + z * z), F_2PI);
+    float yaw = t_rem(atan2f(2.0f * (w * z + x * y), w * w + x * x - y * y - z * z), F_2PI);
+    const float s = 2.0f * (w * w) - 1.0f;
+    // quat_rotate_inverse(q, v) = v*s - cross(q,v)*w*2 + q*dot(q,v)*2
+    const float *v = root + 7;
+    float d = x * v[0] + y * v[1] + z * v[2];
+    float lin_x = v[0] * s - (y * v[2] - z * v[1]) * w * 2.0f + x * d * 2.0f;
+    const float *o = root + 10;
+    float da = x * o[0] + y * o[1] + z * o[2];
+    float ang_x = o[0] * s - (y * o[2] - z * o[1]) * w * 2.0f + x * da * 2.0f;
+    float ang_z = o[2] * s - (x * o[1] - y * o[0]) * w * 2.0f + z * da * 2.0f;
+    if (roll > F_PI) roll = roll - F_2PI;
+    if (roll < -F_PI) roll = roll + F_2PI;
+    if (yaw > F_PI) yaw = yaw - F_2PI;
+    if (yaw < -F_PI) yaw = yaw + F_2PI;
+    obs[0] = roll;
+    obs[1] = ang_x;
+    obs[2] = ang_z;
+    obs[3] = lin_x;
+    obs[4] = t_rem(desired_yaw - yaw + F_PI, F_2PI) - F_PI;
+    obs[5] = cmd;
+}
+
+__global__ __launch_bounds__(256) void pre_kernel(tg_gogoro_params p, tg_gogoro_buffers b, const float *actions,
+                                                  const float *pre_draws, uint32_t c_lo, uint32_t c_hi) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= p.num_envs) return;
+    const int D = p.num_dof;
+    float a = t_clamp(actions[e], -p.clip_actions, p.clip_actions);
+    float *ah = b.action_history + 5 * e;
+    float h0 = ah[1], h1 = ah[2], h2 = ah[3], h3 = ah[4];
+    ah[0] = h0; ah[1] = h1; ah[2] = h2; ah[3] = h3; ah[4] = a;
+    float da = t_clamp(a * p.max_steering_change, -p.max_steering_change, p.max_steering_change);
+    float c = t_clamp(b.curent_command[e] + da, -p.max_steering, p.max_steering);
+    b.curent_command[e] = c;
+    float r;
+    if (pre_draws) r = pre_draws[e];
+    else {
+        U4 x = philox(U4{(uint32_t)e, c_lo, c_hi, 0x50524531u}, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+        r = gauss(x.x, x.y);
+    }
+    float noise = p.steering_action_noise[0] + r * p.steering_action_noise[1];
+    b.pos_target[(size_t)e * D + p.dof_steer] = c + b.steer_offsets[e] + noise;
+    b.vel_target[(size_t)e * D + p.dof_rear] = b.curent_speed[e];
+}
+
+__device__ void philox_reset_draws(int e, uint32_t c_lo, uint32_t c_hi, uint32_t k0, uint32_t k1, float *r);
+
+__device__ void reset_env(const tg_gogoro_params &p, const tg_gogoro_buffers &b, int e, const float *r) {
+    const int D = p.num_dof;
+    b.curent_speed[e] = u_aff(p.speed_range[0], p.speed_range[1], r[0]);
+    b.speed_offset[e] = u_aff(p.speed_sensor_offset[0], p.speed_sensor_offset[1], r[2]);
+    const float target = (r[3] * 2.0f - 1.0f) * F_PI;
+    const float rot = target + u_aff(-1.57f, 1.57f, r[4]);
+    const float hh = rot / 2.0f;
+    float *root = b.root + 13 * (size_t)e;
+    const float *tpl = b.root_reset + 13 * (size_t)e;
+    root[0] = tpl[0];
+    root[1] = tpl[1];
+    root[2] = p.spawn_z;
+    root[3] = 0.0f;
+    root[4] = 0.0f;
+    root[5] = sinf(hh);
+    root[6] = cosf(hh);
+#pragma unroll
+    for (int k = 7; k < 13; ++k) root[k] = 0.0f;
+    float *dof = b.dof_state + 2 * (size_t)e * D;
+    for (int d = 0; d < D; ++d) {
+        dof[2 * d] = b.thormang_pose[d];
+        dof[2 * d + 1] = 0.0f;
+    }
+    float *cv = b.config_vector + 5 * (size_t)e;
+    cv[0] = n_aff(p.seat_offset_x_range, r[5]);
+    cv[1] = n_aff(p.seat_offset_y_range, r[6]);
+    cv[2] = n_aff(p.seat_offset_z_range, r[7]);
+    cv[3] = n_aff(p.seat_offset_xr_range, r[8]);
+    cv[4] = n_aff(p.steering_offset, r[9]);
+    const size_t ND = (size_t)p.num_envs * D;
+    float *prop = b.dof_props + (size_t)e * D;
+    const int seat[3] = {p.dof_base_x, p.dof_base_y, p.dof_base_z};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        prop[TG_PROP_DRIVE_MODE * ND + seat[k]] = 0.0f;
+        prop[TG_PROP_LOWER * ND + seat[k]] = cv[k];
+        prop[TG_PROP_UPPER * ND + seat[k]] = cv[k] + 0.0001f;
+    }
+    b.imu_offsets[e] = cv[3];
+    b.steer_offsets[e] = cv[4];
+    const int st = p.dof_steer;
+    prop[TG_PROP_DRIVE_MODE * ND + st] = 1.0f;
+    prop[TG_PROP_STIFFNESS * ND + st] = p.steer_stiffness;
+    prop[TG_PROP_DAMPING * ND + st] = u_aff(p.steering_damping_range[0], p.steering_damping_range[1], r[10]);
+    prop[TG_PROP_EFFORT * ND + st] = p.steer_effort;
+    prop[TG_PROP_VELOCITY * ND + st] = p.steer_velocity;
+    b.env_dirty[e] = 1;
+    b.progress_buf[e] = 0;
+    b.reset_buf[e] = 0;
+    b.curent_command[e] = 0.0f;
+    b.yaw_command[e] = target;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) b.action_history[5 * (size_t)e + k] = 0.0f;
+}
+
+__global__ __launch_bounds__(256) void post_kernel(tg_gogoro_params p, tg_gogoro_buffers b, const float *reset_draws,
+                                                   const float *obs_draws, const float *speed_draws,
+                                                   const float *yaw_draws, uint32_t c_lo, uint32_t c_hi) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= p.num_envs) return;
+    const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
+    int64_t prog = b.progress_buf[e] + 1;
+    b.progress_buf[e] = prog;
+    if (b.reset_buf[e] != 0) {
+        float r[TG_GOGORO_RESET_DRAWS];
+        if (reset_draws) {
+#pragma unroll
+            for (int k = 0; k < TG_GOGORO_RESET_DRAWS; ++k) r[k] = reset_draws[(size_t)e * TG_GOGORO_RESET_DRAWS + k];
+        } else {
+            philox_reset_draws(e, c_lo, c_hi, k0, k1, r);
+        }
+        reset_env(p, b, e, r);
+        prog = 0;
+    }
+    float o[6];
+    observation(b.root + 13 * (size_t)e, b.yaw_command[e], b.curent_command[e], o);
+    float *bo = b.buffer_obs + 6 * (size_t)e;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) bo[k] = o[k];
+    // compute_gogoro_reward
+    const float max_tilt = 0.30f;
+    float tilt_err = t_clamp(o[0] / max_tilt, -1.0f, 1.0f);
+    float yaw_err = t_clamp(o[4] / F_PI, -1.0f, 1.0f);
+    float dtilt_err = t_clamp(o[1] / 0.3f, -1.0f, 1.0f);
+    float y30 = yaw_err * 30.0f;
+    float r1 = 1.0f / (1.0f + y30 * y30);
+    float r2 = 1.0f - tilt_err * tilt_err;
+    float r4 = 1.0f - dtilt_err * dtilt_err;
+    const float *ah = b.action_history + 5 * (size_t)e;
+    float ce = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) ce += 1.0f - ah[k] * ah[k];
+    float rew = r1 * 5.0f + r2 * 0.2f + r4 * 0.3f + ce * 0.5f;
+    const bool felt = fabsf(o[0]) >= max_tilt;
+    const bool finished = prog >= p.max_episode_length - 1;
+    const int64_t reset = (finished || felt) ? 1 : 0;
+    b.rew_buf[e] = felt ? -100.0f : rew;
+    b.reset_buf[e] = reset;
+    // sensor noise (compute_obs_rwd :449-462)
+    float nd[5];
+    if (obs_draws) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) nd[k] = obs_draws[(size_t)e * 5 + k];
+    } else {
+        U4 x0 = philox(U4{(uint32_t)e, c_lo, c_hi, 0x4F425330u}, k0, k1);
+        U4 x1 = philox(U4{(uint32_t)e, c_lo, c_hi, 0x4F425331u}, k0, k1);
+        U4 x2 = philox(U4{(uint32_t)e, c_lo, c_hi, 0x4F425332u}, k0, k1);
+        nd[0] = gauss(x0.x, x0.y); nd[1] = gauss(x0.z, x0.w); nd[2] = gauss(x1.x, x1.y);
+        nd[3] = gauss(x1.z, x1.w); nd[4] = gauss(x2.x, x2.y);
+    }
+    float rr[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) rr[k] = o[k];
+    rr[0] += n_aff(p.imu_filter_noise, nd[0]) + b.imu_offsets[e];
+    rr[1] += n_aff(p.imu_noise, nd[1]);
+    rr[2] += n_aff(p.imu_noise, nd[2]);
+    rr[3] = rintf(rr[4]);                     // quirk :457-458 (speed-sensor value discarded)
+    rr[4] += n_aff(p.imu_filter_noise, nd[4]);
+    float *ob = b.obs_buf + 6 * (size_t)e;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) ob[k] = t_clamp(rr[k], -p.clip_obs, p.clip_obs);
+    // command resampling (:384-389)
+    float su, yu;
+    if (speed_draws) { su = speed_draws[e]; yu = yaw_draws[e]; }
+    else {
+        U4 x = philox(U4{(uint32_t)e, c_lo, c_hi, 0x434D4430u}, k0, k1);
+        su = u01(x.x);
+        yu = u01(x.y);
+    }
+    if (prog == p.speed_freq_update) b.curent_speed[e] = u_aff(p.speed_range[0], p.speed_range[1], su);
+    float yc = b.yaw_command[e];
+    if (prog == p.yaw_freq_update) yc = u_aff(-F_PI, F_PI, yu);
+    if (yc > F_PI) yc = yc - F_2PI;
+    if (yc < -F_PI) yc = yc + F_2PI;
+    b.yaw_command[e] = yc;
+    b.timeout_buf[e] = (prog >= p.max_episode_length - 1) && (reset != 0);
+}
+
+__device__ void philox_reset_draws(int e, uint32_t c_lo, uint32_t c_hi, uint32_t k0, uint32_t k1, float *r);
+
+__global__ __launch_bounds__(256) void reset_idx_kernel(tg_gogoro_params p, tg_gogoro_buffers b, const int32_t *ids,
+                                                        int n, const float *reset_draws, uint32_t c_lo, uint32_t c_hi) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int e = ids[i];
+    if (e < 0 || e >= p.num_envs) return;
+    float r[TG_GOGORO_RESET_DRAWS];
+    if (reset_draws) {
+#pragma unroll
+        for (int k = 0; k < TG_GOGORO_RESET_DRAWS; ++k) r[k] = reset_draws[(size_t)e * TG_GOGORO_RESET_DRAWS + k];
+    } else {
+        philox_reset_draws(e, c_lo, c_hi, (uint32_t)p.seed, (uint32_t)(p.seed >> 32), r);
+    }
+    reset_env(p, b, e, r);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        b.obs_buf[6 * (size_t)e + k] = 0.0f;
+        b.buffer_obs[6 * (size_t)e + k] = 0.0f;
+    }
+}
+
+__device__ void philox_reset_draws(int e, uint32_t c_lo, uint32_t c_hi, uint32_t k0, uint32_t k1, float *r) {
+    U4 x0 = philox(U4{(uint32_t)e, c_lo, c_hi, 0x52535430u}, k0, k1);
+    U4 x1 = philox(U4{(uint32_t)e, c_lo, c_hi, 0x52535431u}, k0, k1);
+    U4 x2 = philox(U4{(uint32_t)e, c_lo, c_hi, 0x52535432u}, k0, k1);
+    U4 x3 = philox(U4{(uint32_t)e, c_lo, c_hi, 0x52535433u}, k0, k1);
+    U4 x4 = philox(U4{(uint32_t)e, c_lo, c_hi, 0x52535434u}, k0, k1);
+    r[0] = u01(x0.x); r[1] = gauss(x0.y, x0.z); r[2] = u01(x0.w);
+    r[3] = u01(x1.x); r[4] = u01(x1.y); r[5] = gauss(x1.z, x1.w);
+    r[6] = gauss(x2.x, x2.y); r[7] = gauss(x2.z, x2.w);
+    r[8] = gauss(x3.x, x3.y); r[9] = gauss(x3.z, x3.w);
+    r[10] = u01(x4.x);
+}
+
+int launch_gogoro_reset_idx(const tg_gogoro_params &p, const tg_gogoro_buffers &b, const int32_t *ids, int n,
+                            const float *reset_draws, uint64_t counter, hipStream_t stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(reset_idx_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, p, b, ids, n, reset_draws,
+                       (uint32_t)counter, (uint32_t)(counter >> 32));
+    return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
+}
+
+int launch_gogoro_pre(const tg_gogoro_params &p, const tg_gogoro_buffers &b, const float *actions,
+                      const float *pre_draws, uint64_t counter, hipStream_t stream) {
+    dim3 grid((p.num_envs + 255) / 256), block(256);
+    hipLaunchKernelGGL(pre_kernel, grid, block, 0, stream, p, b, actions, pre_draws, (uint32_t)counter,
+                       (uint32_t)(counter >> 32));
+    return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
+}
+
+int launch_gogoro_post(const tg_gogoro_params &p, const tg_gogoro_buffers &b, const float *reset_draws,
+                       const float *obs_draws, const float *speed_draws, const float *yaw_draws, uint64_t counter,
+                       hipStream_t stream) {
+    dim3 grid((p.num_envs + 255) / 256), block(256);
+    hipLaunchKernelGGL(post_kernel, grid, block, 0, stream, p, b, reset_draws, obs_draws, speed_draws, yaw_draws,
+                       (uint32_t)counter, (uint32_t)(counter >> 32));
+    return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
+}
+
+// ---------------------------------------------------------------- indexed setters
+__global__ void scatter_rows_kernel(float *dst, const float *src, const int32_t *ids, int n, int row) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (size_t)n * row) return;
+    const int i = (int)(t / row), k = (int)(t % row);
+    const size_t o = (size_t)ids[i] * row + k;
+    dst[o] = src[o];
+}
+__global__ void mark_dirty_kernel(uint8_t *dirty, const int32_t *ids, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dirty[ids[i]] = 1;
+}
+
+int launch_scatter_rows(float *dst, const float *src, const int32_t *ids, int n, int row, hipStream_t stream) {
+    if (n <= 0) return 0;
+    size_t tot = (size_t)n * row;
+    hipLaunchKernelGGL(scatter_rows_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, dst, src, ids,
+                       n, row);
+    return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
+}
+int launch_scatter_field(float *dst, const float *src, const int32_t *ids, int n, int row, hipStream_t stream) {
+    return launch_scatter_rows(dst, src, ids, n, row, stream);
+}
+int launch_mark_dirty(uint8_t *dirty, const int32_t *ids, int n, hipStream_t stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(mark_dirty_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, dirty, ids, n);
+    return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
+}
+
+}  // namespace tg

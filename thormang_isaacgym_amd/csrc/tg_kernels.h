@@ -1,0 +1,75 @@
+// Internal kernel argument blocks and launchers shared by the C-ABI host code
+// (tgsim_api.cpp) and the kernel translation units.  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/tg_gogoro.h"
+#include "../../include/tgsim.h"
+
+namespace tg {
+
+struct StepArgs {
+    int N, D;
+    float h;
+    int substeps;
+    float gx, gy, gz;
+    float lin_damp, ang_damp, max_depen, rest, margin, ground_mu, baumgarte, lim_k, lim_c;
+    int iters, fix_base;
+    float *root;              // [N,13]
+    float *dof;               // [N*D,2]
+    const float *pos_tgt;     // [N,D]
+    const float *vel_tgt;     // [N,D]
+    const float *act;         // [N,D] or null
+    const float *props;       // [TG_NUM_PROPS,N,D]
+    const float *force;       // [N,G,6] or null
+    const float *shape_mu;    // [N,S]
+    const float *mass_scale;  // [N,L] or null
+    float *comp;              // [KC,N]
+    uint8_t *dirty;           // [N]
+};
+
+int launch_step(uint64_t hash, const StepArgs &a, hipStream_t stream);
+int launch_compose(uint64_t hash, const StepArgs &a, hipStream_t stream);
+int compiled_hashes(uint64_t *out, int cap);
+int model_kc(uint64_t hash);
+
+int launch_gogoro_pre(const tg_gogoro_params &p, const tg_gogoro_buffers &b, const float *actions,
+                      const float *pre_draws, uint64_t counter, hipStream_t stream);
+int launch_gogoro_post(const tg_gogoro_params &p, const tg_gogoro_buffers &b, const float *reset_draws,
+                       const float *obs_draws, const float *speed_draws, const float *yaw_draws, uint64_t counter,
+                       hipStream_t stream);
+
+int launch_gogoro_reset_idx(const tg_gogoro_params &p, const tg_gogoro_buffers &b, const int32_t *ids, int n,
+                            const float *reset_draws, uint64_t counter, hipStream_t stream);
+
+// indexed scatter: dst[ids[i]*row + k] = src[ids[i]*row + k]
+int launch_scatter_rows(float *dst, const float *src, const int32_t *ids, int n, int row, hipStream_t stream);
+// dst[f][ids[i]][k] (field f of a [F,N,row] array) = src[ids[i]*row + k]
+int launch_scatter_field(float *dst, const float *src, const int32_t *ids, int n, int row, hipStream_t stream);
+int launch_mark_dirty(uint8_t *dirty, const int32_t *ids, int n, hipStream_t stream);
+
+// ---------------------------------------------------------------- Philox4x32-10
+struct U4 {
+    uint32_t x, y, z, w;
+};
+__device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+        uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+        c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+__device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
+// Box-Muller from two 32-bit draws
+__device__ __forceinline__ float gauss(uint32_t a, uint32_t b) {
+    float u1 = ((float)(a >> 8) + 1.0f) * (1.0f / 16777217.0f);
+    float u2 = u01(b);
+    return sqrtf(-2.0f * __logf(u1)) * __cosf(6.28318530718f * u2);
+}
+
+}  // namespace tg

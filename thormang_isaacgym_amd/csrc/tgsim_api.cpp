@@ -1,0 +1,389 @@
+// tgsim_api.cpp -- host side of the C-ABI (include/tgsim.h, include/tg_gogoro.h).
+//
+// Owns the per-sim device buffers (struct-of-arrays where the kernels want
+// coalescing, the reference's AoS row layouts where the Python side expects
+// IsaacGym-compatible tensor views), validates every call and reports errors
+// through tg_last_error().  All work is stream-ordered on the sim's stream.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/tg_gogoro.h"
+#include "../../include/tgsim.h"
+#include "tg_kernels.h"
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+#define HIPCHK(x)                                                                                   \
+    do {                                                                                            \
+        hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess) return fail(TG_ERR_HIP, "%s failed: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+}  // namespace
+
+struct tg_sim {
+    int device = 0;
+    int N = 0, D = 0, G = 0, L = 0, S = 0, KC = 0;
+    uint64_t hash = 0;
+    tg_sim_params params{};
+    hipStream_t stream = nullptr;
+    float gravity[3] = {0, 0, -9.81f};
+    bool forces_pending = false;
+    // device buffers
+    float *root = nullptr, *dof = nullptr, *pos_tgt = nullptr, *vel_tgt = nullptr, *act = nullptr;
+    float *props = nullptr, *force = nullptr, *mass_scale = nullptr, *shape_mu = nullptr, *comp = nullptr;
+    float *env_origin = nullptr;
+    uint8_t *dirty = nullptr;
+    std::vector<void *> allocs;
+
+    template <class T> int alloc(T **p, size_t count) {
+        void *q = nullptr;
+        if (count == 0) count = 1;
+        hipError_t e = hipMalloc(&q, count * sizeof(T));
+        if (e != hipSuccess) return fail(TG_ERR_HIP, "hipMalloc(%zu bytes): %s", count * sizeof(T), hipGetErrorString(e));
+        e = hipMemset(q, 0, count * sizeof(T));
+        if (e != hipSuccess) return fail(TG_ERR_HIP, "hipMemset: %s", hipGetErrorString(e));
+        allocs.push_back(q);
+        *p = (T *)q;
+        return 0;
+    }
+    ~tg_sim() {
+        for (void *p : allocs) (void)hipFree(p);
+    }
+};
+
+namespace {
+int check_sim(tg_sim *s) { return s ? 0 : fail(TG_ERR_ARG, "null tg_sim"); }
+int check_ids(tg_sim *s, const int32_t *ids, int32_t n) {
+    if (n < 0 || n > s->N) return fail(TG_ERR_ARG, "index count %d out of range [0, %d]", n, s->N);
+    if (n > 0 && !ids) return fail(TG_ERR_ARG, "null index pointer with n=%d", n);
+    return 0;
+}
+tg::StepArgs step_args(tg_sim *s) {
+    tg::StepArgs a{};
+    const tg_sim_params &p = s->params;
+    a.N = s->N;
+    a.D = s->D;
+    a.h = p.dt / (float)p.substeps;
+    a.substeps = p.substeps;
+    a.gx = s->gravity[0]; a.gy = s->gravity[1]; a.gz = s->gravity[2];
+    a.lin_damp = p.linear_damping;
+    a.ang_damp = p.angular_damping;
+    a.max_depen = p.max_depenetration_velocity;
+    a.rest = p.rest_offset;
+    a.margin = p.contact_margin;
+    a.ground_mu = p.ground_friction;
+    a.baumgarte = p.baumgarte;
+    a.lim_k = p.limit_stiffness;
+    a.lim_c = p.limit_damping;
+    a.iters = p.contact_iterations;
+    a.fix_base = p.fix_base;
+    a.root = s->root;
+    a.dof = s->dof;
+    a.pos_tgt = s->pos_tgt;
+    a.vel_tgt = s->vel_tgt;
+    a.act = s->act;
+    a.props = s->props;
+    a.force = s->forces_pending ? s->force : nullptr;
+    a.shape_mu = s->shape_mu;
+    a.mass_scale = s->mass_scale;
+    a.comp = s->comp;
+    a.dirty = s->dirty;
+    return a;
+}
+}  // namespace
+
+extern "C" {
+
+const char *tg_last_error(void) { return g_err.c_str(); }
+
+uint64_t tg_compiled_model_hashes(uint64_t *out, int32_t cap) { return (uint64_t)tg::compiled_hashes(out, cap); }
+
+int tg_sim_create(const tg_model_desc *m, const tg_sim_params *params, int32_t num_envs, int32_t device,
+                  tg_sim **out) {
+    if (!m || !params || !out) return fail(TG_ERR_ARG, "tg_sim_create: null argument");
+    *out = nullptr;
+    if (num_envs <= 0) return fail(TG_ERR_ARG, "num_envs must be positive (got %d)", num_envs);
+    if (params->substeps <= 0 || !(params->dt > 0.f)) return fail(TG_ERR_ARG, "dt and substeps must be positive");
+    if (params->contact_iterations < 0) return fail(TG_ERR_ARG, "contact_iterations must be >= 0");
+    int kc = tg::model_kc(m->model_hash);
+    if (kc < 0)
+        return fail(TG_ERR_MODEL,
+                    "model hash 0x%016llx has no compiled specialisation in libtgsim.so "
+                    "(rebuild with the model's JSON under thormang_isaacgym_amd/model/compiled/)",
+                    (unsigned long long)m->model_hash);
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(TG_ERR_ARG, "device %d not present (%d visible)", device, ndev);
+    HIPCHK(hipSetDevice(device));
+    tg_sim *s = new tg_sim();
+    s->device = device;
+    s->N = num_envs;
+    s->D = m->num_dofs;
+    s->G = m->num_groups;
+    s->L = m->num_links;
+    s->S = m->num_shapes;
+    s->KC = kc;
+    s->hash = m->model_hash;
+    s->params = *params;
+    memcpy(s->gravity, params->gravity, sizeof s->gravity);
+    const size_t N = num_envs;
+    int rc = 0;
+    rc |= s->alloc(&s->root, N * 13);
+    rc |= s->alloc(&s->dof, N * s->D * 2);
+    rc |= s->alloc(&s->pos_tgt, N * s->D);
+    rc |= s->alloc(&s->vel_tgt, N * s->D);
+    rc |= s->alloc(&s->act, N * s->D);
+    rc |= s->alloc(&s->props, (size_t)TG_NUM_PROPS * N * s->D);
+    rc |= s->alloc(&s->force, N * s->G * 6);
+    rc |= s->alloc(&s->mass_scale, N * s->L);
+    rc |= s->alloc(&s->shape_mu, N * (s->S > 0 ? s->S : 1));
+    rc |= s->alloc(&s->comp, (size_t)kc * N);
+    rc |= s->alloc(&s->env_origin, N * 3);
+    rc |= s->alloc(&s->dirty, N);
+    if (rc) {
+        std::string keep = g_err;
+        delete s;
+        g_err = keep;
+        return TG_ERR_HIP;
+    }
+    // host-side initial values: identity root pose at the env origin grid,
+    // unit mass scale, per-shape friction from the model, defaults for props
+    std::vector<float> h_root(N * 13, 0.f), h_org(N * 3, 0.f), h_ms(N * s->L, 1.f);
+    std::vector<float> h_mu(N * (s->S > 0 ? s->S : 1), 1.f);
+    std::vector<uint8_t> h_dirty(N, 1);
+    const int per_row = params->envs_per_row > 0 ? params->envs_per_row : 1;
+    for (size_t e = 0; e < N; ++e) {
+        h_org[3 * e + 0] = 2.f * params->env_spacing * (float)(e % per_row);
+        h_org[3 * e + 1] = 2.f * params->env_spacing * (float)(e / per_row);
+        h_root[13 * e + 0] = h_org[3 * e + 0];
+        h_root[13 * e + 1] = h_org[3 * e + 1];
+        h_root[13 * e + 6] = 1.f;
+        for (int k = 0; k < s->S; ++k) h_mu[e * s->S + k] = m->shape_friction[k];
+    }
+    std::vector<float> h_props((size_t)TG_NUM_PROPS * N * s->D, 0.f);
+    for (size_t i = 0; i < N * s->D; ++i) {
+        h_props[(size_t)TG_PROP_LOWER * N * s->D + i] = -3.4e38f;
+        h_props[(size_t)TG_PROP_UPPER * N * s->D + i] = 3.4e38f;
+    }
+    HIPCHK(hipMemcpy(s->root, h_root.data(), h_root.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(s->env_origin, h_org.data(), h_org.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(s->mass_scale, h_ms.data(), h_ms.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(s->shape_mu, h_mu.data(), h_mu.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(s->dirty, h_dirty.data(), N, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(s->props, h_props.data(), h_props.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipDeviceSynchronize());
+    *out = s;
+    return TG_OK;
+}
+
+int tg_sim_destroy(tg_sim *s) {
+    if (!s) return TG_OK;
+    (void)hipSetDevice(s->device);
+    (void)hipDeviceSynchronize();
+    delete s;
+    return TG_OK;
+}
+
+int tg_set_stream(tg_sim *s, void *stream) {
+    if (int rc = check_sim(s)) return rc;
+    s->stream = (hipStream_t)stream;
+    return TG_OK;
+}
+
+int tg_state_ptrs(tg_sim *s, tg_state_view *v) {
+    if (int rc = check_sim(s)) return rc;
+    if (!v) return fail(TG_ERR_ARG, "null view");
+    v->root_state = s->root;
+    v->dof_state = s->dof;
+    v->dof_pos_target = s->pos_tgt;
+    v->dof_vel_target = s->vel_tgt;
+    v->dof_actuation = s->act;
+    v->dof_props = s->props;
+    v->body_force = s->force;
+    v->env_origin = s->env_origin;
+    v->env_dirty = s->dirty;
+    v->num_envs = s->N;
+    v->num_dofs = s->D;
+    v->num_groups = s->G;
+    v->num_links = s->L;
+    return TG_OK;
+}
+
+int tg_refresh(tg_sim *s) { return check_sim(s); }
+
+int tg_bind_state(tg_sim *s, const tg_state_view *v) {
+    if (int rc = check_sim(s)) return rc;
+    if (!v) return fail(TG_ERR_ARG, "null view");
+    const size_t N = s->N, D = s->D;
+    struct B {
+        void *src;
+        void **dst;
+        size_t bytes;
+    } binds[] = {
+        {v->root_state, (void **)&s->root, N * 13 * 4},
+        {v->dof_state, (void **)&s->dof, N * D * 2 * 4},
+        {v->dof_pos_target, (void **)&s->pos_tgt, N * D * 4},
+        {v->dof_vel_target, (void **)&s->vel_tgt, N * D * 4},
+        {v->dof_actuation, (void **)&s->act, N * D * 4},
+        {v->dof_props, (void **)&s->props, (size_t)TG_NUM_PROPS * N * D * 4},
+        {v->body_force, (void **)&s->force, N * s->G * 6 * 4},
+        {v->env_origin, (void **)&s->env_origin, N * 3 * 4},
+        {v->env_dirty, (void **)&s->dirty, N},
+    };
+    for (auto &b : binds) {
+        if (!b.src || b.src == *b.dst) continue;
+        HIPCHK(hipMemcpyAsync(b.src, *b.dst, b.bytes, hipMemcpyDeviceToDevice, s->stream));
+        *b.dst = b.src;
+    }
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return TG_OK;
+}
+
+static int copy_full(tg_sim *s, float *dst, const float *src, size_t count) {
+    if (!src) return fail(TG_ERR_ARG, "null source tensor");
+    if (src == dst) return TG_OK;
+    HIPCHK(hipMemcpyAsync(dst, src, count * sizeof(float), hipMemcpyDeviceToDevice, s->stream));
+    return TG_OK;
+}
+
+int tg_set_dof_position_targets(tg_sim *s, const float *pos) {
+    if (int rc = check_sim(s)) return rc;
+    return copy_full(s, s->pos_tgt, pos, (size_t)s->N * s->D);
+}
+int tg_set_dof_velocity_targets(tg_sim *s, const float *vel) {
+    if (int rc = check_sim(s)) return rc;
+    return copy_full(s, s->vel_tgt, vel, (size_t)s->N * s->D);
+}
+int tg_set_dof_actuation_forces(tg_sim *s, const float *eff) {
+    if (int rc = check_sim(s)) return rc;
+    return copy_full(s, s->act, eff, (size_t)s->N * s->D);
+}
+
+int tg_set_actor_root_state_indexed(tg_sim *s, const float *root, const int32_t *ids, int32_t n) {
+    if (int rc = check_sim(s)) return rc;
+    if (int rc = check_ids(s, ids, n)) return rc;
+    if (!root) return fail(TG_ERR_ARG, "null root state");
+    if (root == s->root) return TG_OK;
+    if (int rc = tg::launch_scatter_rows(s->root, root, ids, n, 13, s->stream)) return fail(rc, "scatter failed");
+    return TG_OK;
+}
+
+int tg_set_dof_state_indexed(tg_sim *s, const float *dof, const int32_t *ids, int32_t n) {
+    if (int rc = check_sim(s)) return rc;
+    if (int rc = check_ids(s, ids, n)) return rc;
+    if (!dof) return fail(TG_ERR_ARG, "null dof state");
+    if (dof == s->dof) return TG_OK;
+    if (int rc = tg::launch_scatter_rows(s->dof, dof, ids, n, 2 * s->D, s->stream)) return fail(rc, "scatter failed");
+    return TG_OK;
+}
+
+int tg_set_dof_properties_indexed(tg_sim *s, int32_t field, const float *vals, const int32_t *ids, int32_t n) {
+    if (int rc = check_sim(s)) return rc;
+    if (int rc = check_ids(s, ids, n)) return rc;
+    if (field < 0 || field >= TG_NUM_PROPS) return fail(TG_ERR_ARG, "unknown dof property field %d", field);
+    if (!vals) return fail(TG_ERR_ARG, "null property values");
+    float *dst = s->props + (size_t)field * s->N * s->D;
+    if (vals != dst)
+        if (int rc = tg::launch_scatter_field(dst, vals, ids, n, s->D, s->stream)) return fail(rc, "scatter failed");
+    if (int rc = tg::launch_mark_dirty(s->dirty, ids, n, s->stream)) return fail(rc, "mark dirty failed");
+    return TG_OK;
+}
+
+int tg_set_body_mass_scale_indexed(tg_sim *s, const float *scale, const int32_t *ids, int32_t n) {
+    if (int rc = check_sim(s)) return rc;
+    if (int rc = check_ids(s, ids, n)) return rc;
+    if (!scale) return fail(TG_ERR_ARG, "null mass scale");
+    if (int rc = tg::launch_scatter_rows(s->mass_scale, scale, ids, n, s->L, s->stream)) return fail(rc, "scatter failed");
+    if (int rc = tg::launch_mark_dirty(s->dirty, ids, n, s->stream)) return fail(rc, "mark dirty failed");
+    return TG_OK;
+}
+
+int tg_set_shape_friction_indexed(tg_sim *s, const float *mu, const int32_t *ids, int32_t n) {
+    if (int rc = check_sim(s)) return rc;
+    if (int rc = check_ids(s, ids, n)) return rc;
+    if (!mu) return fail(TG_ERR_ARG, "null friction");
+    if (s->S == 0) return TG_OK;
+    if (int rc = tg::launch_scatter_rows(s->shape_mu, mu, ids, n, s->S, s->stream)) return fail(rc, "scatter failed");
+    return TG_OK;
+}
+
+int tg_set_gravity(tg_sim *s, const float *g3) {
+    if (int rc = check_sim(s)) return rc;
+    if (!g3) return fail(TG_ERR_ARG, "null gravity");
+    memcpy(s->gravity, g3, sizeof s->gravity);
+    return TG_OK;
+}
+
+int tg_apply_body_forces(tg_sim *s, const float *wrench) {
+    if (int rc = check_sim(s)) return rc;
+    if (!wrench) return fail(TG_ERR_ARG, "null wrench tensor");
+    if (int rc = copy_full(s, s->force, wrench, (size_t)s->N * s->G * 6)) return rc;
+    s->forces_pending = true;
+    return TG_OK;
+}
+
+int tg_simulate(tg_sim *s) {
+    if (int rc = check_sim(s)) return rc;
+    tg::StepArgs a = step_args(s);
+    int rc = tg::launch_step(s->hash, a, s->stream);
+    s->forces_pending = false;   // apply_rigid_body_force_tensors acts for one simulate call
+    if (rc) return fail(rc, "step launch failed: %s", hipGetErrorString(hipGetLastError()));
+    return TG_OK;
+}
+
+int tg_sync(tg_sim *s) {
+    if (int rc = check_sim(s)) return rc;
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return TG_OK;
+}
+
+int tg_gogoro_pre_physics(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_buffers *b, const float *actions,
+                          const float *pre_draws, uint64_t counter) {
+    if (int rc = check_sim(s)) return rc;
+    if (!p || !b || !actions) return fail(TG_ERR_ARG, "tg_gogoro_pre_physics: null argument");
+    if (p->num_envs != s->N || p->num_dof != s->D) return fail(TG_ERR_ARG, "gogoro params do not match the sim");
+    if (int rc = tg::launch_gogoro_pre(*p, *b, actions, pre_draws, counter, s->stream)) return fail(rc, "launch failed");
+    return TG_OK;
+}
+
+int tg_gogoro_post_physics(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_buffers *b, const float *reset_draws,
+                           const float *obs_draws, const float *speed_draws, const float *yaw_draws, uint64_t counter) {
+    if (int rc = check_sim(s)) return rc;
+    if (!p || !b) return fail(TG_ERR_ARG, "tg_gogoro_post_physics: null argument");
+    if (p->num_envs != s->N || p->num_dof != s->D) return fail(TG_ERR_ARG, "gogoro params do not match the sim");
+    if ((speed_draws == nullptr) != (yaw_draws == nullptr))
+        return fail(TG_ERR_ARG, "speed_draws and yaw_draws must both be given or both be NULL");
+    if (int rc = tg::launch_gogoro_post(*p, *b, reset_draws, obs_draws, speed_draws, yaw_draws, counter, s->stream))
+        return fail(rc, "launch failed");
+    return TG_OK;
+}
+
+int tg_gogoro_reset_idx(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_buffers *b, const int32_t *ids,
+                        int32_t n, const float *reset_draws, uint64_t counter) {
+    if (int rc = check_sim(s)) return rc;
+    if (int rc = check_ids(s, ids, n)) return rc;
+    if (!p || !b) return fail(TG_ERR_ARG, "tg_gogoro_reset_idx: null argument");
+    if (p->num_envs != s->N || p->num_dof != s->D) return fail(TG_ERR_ARG, "gogoro params do not match the sim");
+    if (int rc = tg::launch_gogoro_reset_idx(*p, *b, ids, n, reset_draws, counter, s->stream))
+        return fail(rc, "launch failed");
+    return TG_OK;
+}
+
+}  // extern "C"

@@ -70,7 +70,8 @@ def build_thormang():
 def main():
     out = os.path.join(HERE, "compiled")
     os.makedirs(out, exist_ok=True)
-    for m in (build_gogoro(), build_thormang()):
+    from thormang_isaacgym_amd.model.kat_models import all_models
+    for m in [build_gogoro(), build_thormang()] + all_models():
         with open(os.path.join(out, f"{m.name}.json"), "w") as f:
             f.write(m.to_json())
         print(m.name, "links", m.num_bodies, "dofs", m.num_dof, "groups", m.num_groups, "active", len(m.active_dofs),

@@ -1,0 +1,155 @@
+"""Python face of one libtgsim simulation: the part of ``gymapi.Gym`` the
+reference tasks use (create_sim/load_asset/create_actor, the tensor API,
+simulate), with torch tensors as zero-copy state views.
+
+Reference calls mirrored (isaacgymenvs/tasks/...):
+  acquire_actor_root_state_tensor / acquire_dof_state_tensor + wrap_tensor
+      -> Sim.root_state [N,13], Sim.dof_state [N*D,2]      (gogoro_new.py:125-130)
+  refresh_*_tensor -> Sim.refresh() (no-op, state is live)  (gogoro_new.py:141-142)
+  set_dof_position/velocity_target_tensor -> Sim.set_dof_*_targets (gogoro_new.py:364,369)
+  set_actor_root_state_tensor_indexed / set_dof_state_tensor_indexed  (gogoro_new.py:547,552)
+  set_actor_dof_properties (per env)   -> Sim.set_dof_properties_indexed (gogoro_new.py:294,601)
+  simulate / fetch_results             -> Sim.simulate / Sim.sync (vec_task.py:335,339)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+
+import numpy as np
+import torch
+
+from . import abi
+from ._lib import check, lib
+from .model.urdf import Model
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+COMPILED = os.path.join(HERE, "model", "compiled")
+
+
+def load_model(name: str) -> Model:
+    with open(os.path.join(COMPILED, f"{name}.json")) as f:
+        return Model.from_json(f.read())
+
+
+def _ptr(t: torch.Tensor | None):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+class Sim:
+    def __init__(self, model: Model, params: abi.tg_sim_params, num_envs: int, device: str = "cuda:0"):
+        if not device.startswith("cuda"):
+            raise RuntimeError(f"libtgsim runs on an MI355X ('cuda:N' device), got {device!r}; "
+                               "there is no CPU physics path outside the test oracle")
+        self.device = torch.device(device)
+        self.model = model
+        self.num_envs = N = int(num_envs)
+        self.desc = abi.ModelDesc(model)
+        self.params = params
+        self.D, self.G, self.L, self.S = model.num_dof, model.num_groups, model.num_bodies, len(model.shapes)
+        torch.cuda.set_device(self.device)
+        h = C.c_void_p()
+        check(lib().tg_sim_create(C.byref(self.desc.desc), C.byref(params), N, self.device.index or 0, C.byref(h)),
+              "tg_sim_create")
+        self._h = h
+        self.stream = torch.cuda.current_stream(self.device)
+        check(lib().tg_set_stream(self._h, C.c_void_p(self.stream.cuda_stream)), "tg_set_stream")
+        f32 = dict(dtype=torch.float32, device=self.device)
+        D, G = self.D, self.G
+        self.root_state = torch.zeros(N, 13, **f32)
+        self.dof_state = torch.zeros(N * D, 2, **f32)
+        self.dof_pos_target = torch.zeros(N, D, **f32)
+        self.dof_vel_target = torch.zeros(N, D, **f32)
+        self.dof_actuation = torch.zeros(N, D, **f32)
+        self.dof_props = torch.zeros(abi.TG_NUM_PROPS, N, D, **f32)
+        self.body_force = torch.zeros(N, G, 6, **f32)
+        self.env_origin = torch.zeros(N, 3, **f32)
+        self.env_dirty = torch.zeros(N, dtype=torch.uint8, device=self.device)
+        v = abi.tg_state_view()
+        for k in ("root_state", "dof_state", "dof_pos_target", "dof_vel_target", "dof_actuation", "dof_props",
+                  "body_force", "env_origin", "env_dirty"):
+            setattr(v, k, getattr(self, k).data_ptr())
+        check(lib().tg_bind_state(self._h, C.byref(v)), "tg_bind_state")
+        self.all_ids = torch.arange(N, dtype=torch.int32, device=self.device)
+
+    @property
+    def handle(self):
+        return self._h
+
+    # ---------------------------------------------------------------- tensor API
+    def refresh(self):
+        check(lib().tg_refresh(self._h), "refresh")
+
+    def set_dof_position_targets(self, t: torch.Tensor):
+        check(lib().tg_set_dof_position_targets(self._h, _ptr(self._dev(t))), "set_dof_position_target_tensor")
+
+    def set_dof_velocity_targets(self, t: torch.Tensor):
+        check(lib().tg_set_dof_velocity_targets(self._h, _ptr(self._dev(t))), "set_dof_velocity_target_tensor")
+
+    def set_dof_actuation_forces(self, t: torch.Tensor):
+        check(lib().tg_set_dof_actuation_forces(self._h, _ptr(self._dev(t))), "set_dof_actuation_force_tensor")
+
+    def set_actor_root_state_indexed(self, root: torch.Tensor, ids: torch.Tensor):
+        ids = self._ids(ids)
+        check(lib().tg_set_actor_root_state_indexed(self._h, _ptr(self._dev(root)), _ptr(ids), ids.numel()),
+              "set_actor_root_state_tensor_indexed")
+        return True
+
+    def set_dof_state_indexed(self, dof: torch.Tensor, ids: torch.Tensor):
+        ids = self._ids(ids)
+        check(lib().tg_set_dof_state_indexed(self._h, _ptr(self._dev(dof)), _ptr(ids), ids.numel()),
+              "set_dof_state_tensor_indexed")
+        return True
+
+    def set_dof_properties_indexed(self, field: int, vals: torch.Tensor, ids: torch.Tensor):
+        ids = self._ids(ids)
+        check(lib().tg_set_dof_properties_indexed(self._h, int(field), _ptr(self._dev(vals)), _ptr(ids),
+                                                  ids.numel()), "set_actor_dof_properties")
+
+    def set_body_mass_scale_indexed(self, scale: torch.Tensor, ids: torch.Tensor):
+        ids = self._ids(ids)
+        check(lib().tg_set_body_mass_scale_indexed(self._h, _ptr(self._dev(scale)), _ptr(ids), ids.numel()),
+              "mass scale")
+
+    def set_shape_friction_indexed(self, mu: torch.Tensor, ids: torch.Tensor):
+        ids = self._ids(ids)
+        check(lib().tg_set_shape_friction_indexed(self._h, _ptr(self._dev(mu)), _ptr(ids), ids.numel()), "friction")
+
+    def set_gravity(self, g):
+        arr = (C.c_float * 3)(*[float(x) for x in g])
+        check(lib().tg_set_gravity(self._h, arr), "set_gravity")
+
+    def apply_body_forces(self, wrench: torch.Tensor):
+        check(lib().tg_apply_body_forces(self._h, _ptr(self._dev(wrench))), "apply_rigid_body_force_tensors")
+
+    def simulate(self):
+        check(lib().tg_simulate(self._h), "simulate")
+
+    def sync(self):
+        check(lib().tg_sync(self._h), "sync")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().tg_sim_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------------- helpers
+    def _dev(self, t: torch.Tensor) -> torch.Tensor:
+        if t.device != self.device or t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError(f"expected a contiguous float32 tensor on {self.device}, got {t.dtype} on {t.device}")
+        return t
+
+    def _ids(self, ids: torch.Tensor) -> torch.Tensor:
+        ids = ids.to(device=self.device, dtype=torch.int32).contiguous()
+        return ids
+
+    def props_view(self, field: int) -> torch.Tensor:
+        """[N,D] live view of one per-env DOF property field (tgsim.h TG_PROP_*)."""
+        return self.dof_props[field]

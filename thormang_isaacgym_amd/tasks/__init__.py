@@ -1,0 +1,7 @@
+"""Task registry (mirror of isaacgymenvs/tasks/__init__.py:54-77, restricted to
+the tasks this build provides)."""
+from .gogoro import Gogoro
+
+isaacgym_task_map = {
+    "Gogoro": Gogoro,
+}

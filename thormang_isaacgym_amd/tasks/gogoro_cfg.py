@@ -56,6 +56,46 @@ def thormang_pose(cfg: dict, dof_name_to_id: dict) -> np.ndarray:
     return pose
 
 
+#: AssetOptions of gogoro_new.py:202-211 (+ the plane friction of :188; IsaacGym's
+#: default angular_damping 0.5) as tgsim sim-parameter inputs
+ASSET_OPTIONS = {"fix_base_link": False, "linear_damping": 0.01, "angular_damping": 0.5, "armature": 0.0001,
+                 "ground_friction": 0.99}
+
+
+def initial_dof_props(model, cfg: dict, num_envs: int) -> np.ndarray:
+    """[TG_NUM_PROPS, N, D] DOF properties exactly as ``_create_envs`` sets them
+    (gogoro_new.py:246-275,294): no drives and zero gains everywhere, the
+    joints_pos lock windows, rear wheel velocity drive (damping 1000, effort
+    170), steering position drive (100/100, effort 10, velocity 10), asset armature."""
+    from ..abi import (TG_PROP_ARMATURE, TG_PROP_DAMPING, TG_PROP_DRIVE_MODE, TG_PROP_EFFORT, TG_PROP_LOWER,
+                       TG_PROP_STIFFNESS, TG_PROP_UPPER, TG_PROP_VELOCITY, default_dof_props)
+    dni = model.dof_name_to_id()
+    props = default_dof_props(model, num_envs)
+    props[TG_PROP_DRIVE_MODE] = 0
+    props[TG_PROP_DAMPING] = 0
+    props[TG_PROP_STIFFNESS] = 0
+    props[TG_PROP_EFFORT] = 0
+    lock_window(cfg, dni, props[TG_PROP_LOWER], props[TG_PROP_UPPER])
+    rw, st = dni["rear_wheel_joint"], dni["steering_joint"]
+    props[TG_PROP_DRIVE_MODE, :, rw] = 2
+    props[TG_PROP_DAMPING, :, rw] = 1000.0
+    props[TG_PROP_EFFORT, :, rw] = 170.0
+    props[TG_PROP_DRIVE_MODE, :, st] = 1
+    props[TG_PROP_STIFFNESS, :, st] = 100.0
+    props[TG_PROP_DAMPING, :, st] = 100.0
+    props[TG_PROP_EFFORT, :, st] = 10.0
+    props[TG_PROP_VELOCITY, :, st] = 10.0
+    props[TG_PROP_ARMATURE] = ASSET_OPTIONS["armature"]
+    return props
+
+
+def env_origins(num_envs: int, spacing: float) -> np.ndarray:
+    """create_env grid origins (tgsim_api.cpp tg_sim_create): row-major, 2*spacing pitch."""
+    per_row = max(1, int(math.sqrt(num_envs)))
+    e = np.arange(num_envs)
+    return np.stack([2 * spacing * (e % per_row), 2 * spacing * (e // per_row), np.zeros(num_envs)], 1).astype(np.float32)
+
+
 def lock_window(cfg: dict, dof_name_to_id: dict, lower: np.ndarray, upper: np.ndarray) -> None:
     """Apply the joints_pos lock windows [v, v+1e-4] to [.., D] limit arrays in place (:257-261)."""
     for name, val in cfg["joints_pos"].items():
