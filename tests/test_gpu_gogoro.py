@@ -46,6 +46,7 @@ def test_gpu_task_kernels_replay_reference_steps():
             self.frame_count += 1
 
     cfg = gogoro_cfg(n, int(f["max_steps"]), int(f["freq"]))
+    cfg["sim"]["use_gpu_pipeline"] = True     # fixture cfg was recorded for the reference's CPU pipeline
     env = Replay(cfg, "cuda:0", "cuda:0", -1, True, False, False)
     assert src.i == int(f["init_n_draws_init"])
     np.testing.assert_allclose(env.root_tensor.cpu().numpy(), f["init_root"], atol=1e-6)

@@ -40,7 +40,9 @@ def side_by_side(model, steps, n=16, seed=0, setup=None, **simkw):
         gr = g.root_state.cpu().numpy()
         gd = g.dof_state.cpu().numpy()
         scale = max(1.0, float(np.abs(root).max()))
-        worst = max(worst, float(np.abs(gr - root).max()) / scale, float(np.abs(gd - dof).max()) / scale)
+        worst = max(worst, float(np.abs(gr - root).max()) / scale)
+        if dof.size:
+            worst = max(worst, float(np.abs(gd - dof).max()) / scale)
     return worst, g, root, dof
 
 
