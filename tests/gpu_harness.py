@@ -136,3 +136,107 @@ def gogoro_env_vs_oracle(num_envs=64, steps=20, seed=0, policy=None, max_steps=1
         obs_np = o_obs.copy()
     err["resets_seen"] = int(orc.a["progress_buf"].min())
     return err
+
+
+# ----------------------------------------------------------------------------- ThormangWalk
+class OracleWalk:
+    """CPU restatement of the ThormangWalk env step (oracle/walk_task.c around
+    oracle/physics_ref.c), driven like thormang_isaacgym_amd.tasks.thormang_walk."""
+
+    def __init__(self, cfg, draws, threads=8):
+        import math
+        from thormang_isaacgym_amd.sim import load_model
+        from thormang_isaacgym_amd.tasks.thormang_walk import walk_asset_options, walk_dof_props, walk_params
+        self.cfg, self.src, self.threads = cfg, draws, threads
+        self.model = m = load_model("thormang")
+        env = cfg["env"]
+        self.n = n = env["numEnvs"]
+        self.D = D = m.num_dof
+        self.desc = abi.ModelDesc(m)
+        spacing = float(env.get("envSpacing", 1.0))
+        self.sp = abi.sim_params_from_cfg(cfg["sim"], walk_asset_options(cfg), n, spacing)
+        props, kp, default = walk_dof_props(m, cfg, n)
+        dt = float(cfg["sim"]["dt"])
+        self.p = walk_params(cfg, m, n, m.num_groups, dt, int(math.ceil(env.get("episodeLength_s", 20) / dt)),
+                             float(env.get("clipActions", math.inf)), float(env.get("clipObservations", math.inf)),
+                             kp, default, 42)
+        z = lambda *s, dt=np.float32: np.zeros(s, dt)
+        self.a = dict(obs_buf=z(n, 13 + 3 * D), rew_buf=z(n), reset_buf=np.ones(n, np.int64),
+                      progress_buf=z(n, dt=np.int64), timeout_buf=z(n, dt=np.uint8), actions=z(n, D),
+                      last_actions=z(n, D), commands=z(n, 3), root_reset=z(n, 13), root=z(n, 13),
+                      dof_state=z(n * D, 2), pos_target=z(n, D), body_force=z(n, m.num_groups, 6),
+                      env_dirty=z(n, dt=np.uint8))
+        self.props = props
+        org = env_origins(n, spacing)
+        a = self.a
+        a["root"][:, 0:2] = org[:, 0:2]
+        a["root"][:, 2] = float(env.get("spawnHeight", 0.79))
+        a["root"][:, 6] = 1.0
+        a["root_reset"][:] = a["root"]
+        self.b = abi.tg_walk_buffers(**{k: v.ctypes.data for k, v in a.items()})
+        self.push = self.p.push_force > 0
+        if not self.push:
+            self.b.body_force = None
+        for e in range(n):
+            r = np.ascontiguousarray(draws.uniform(4 + 2 * D))
+            lib().oracle_walk_reset_env(C.byref(self.p), C.byref(self.b), e, ptr(r))
+        # the GPU reset_idx kernel also observes (prog 0): mirror it through a no-reset post pass
+        self._observe_only()
+
+    def _observe_only(self):
+        a = self.a
+        saved = a["progress_buf"].copy()
+        a["progress_buf"][:] = -1
+        a["reset_buf"][:] = 0
+        zeros = np.zeros((self.n, 3), np.float32)
+        lib().oracle_walk_post_physics(C.byref(self.p), C.byref(self.b), None, ptr(zeros))
+        a["progress_buf"][:] = saved
+
+    def step(self, actions):
+        a, n, D = self.a, self.n, self.D
+        lib().oracle_walk_pre_physics(C.byref(self.p), C.byref(self.b), ptr(np.ascontiguousarray(actions, np.float32)))
+        force = a["body_force"] if self.push else None
+        physics_step(self.desc, self.sp, a["root"], a["dof_state"], self.props, a["pos_target"],
+                     np.zeros((n, D), np.float32), force=force, threads=self.threads)
+        ids = np.nonzero(a["reset_buf"])[0]
+        rd = np.zeros((n, 4 + 2 * D), np.float32)
+        for i in ids:
+            rd[i] = self.src.uniform(4 + 2 * D)
+        pd = self.src.uniform(3 * n).reshape(n, 3)
+        lib().oracle_walk_post_physics(C.byref(self.p), C.byref(self.b), ptr(rd), ptr(np.ascontiguousarray(pd)))
+        return a["obs_buf"], a["rew_buf"], a["reset_buf"], a["timeout_buf"]
+
+
+def walk_cfg(num_envs, task="ThormangWalk"):
+    cfg = load_task_cfg(task, num_envs=num_envs)
+    cfg["task"]["randomize"] = False
+    return cfg
+
+
+def make_gpu_walk(cfg, draws):
+    from thormang_isaacgym_amd.tasks.thormang_walk import ThormangWalk
+
+    class ReplayWalk(ThormangWalk):
+        draw_source = draws
+
+    return ReplayWalk(cfg, "cuda:0", "cuda:0", -1, True, False, False)
+
+
+def walk_env_vs_oracle(num_envs=32, steps=30, seed=0, task="ThormangWalk"):
+    import torch
+    env = make_gpu_walk(walk_cfg(num_envs, task), NumpyDraws(seed))
+    orc = OracleWalk(walk_cfg(num_envs, task), NumpyDraws(seed))
+    rs = np.random.default_rng(seed + 100)
+    err = {"obs": 0.0, "rew": 0.0, "reset_equal": True, "timeout_equal": True, "root": 0.0, "steps": steps}
+    err["obs0"] = float(np.abs(env.obs_buf.cpu().numpy() - orc.a["obs_buf"]).max())
+    for t in range(steps):
+        act = rs.uniform(-0.3, 0.3, (num_envs, orc.D)).astype(np.float32)
+        obs_d, rew, reset, extras = env.step(torch.from_numpy(act).to("cuda:0"))
+        o_obs, o_rew, o_reset, o_to = orc.step(act)
+        err["obs"] = max(err["obs"], float(np.abs(obs_d["obs"].cpu().numpy() - o_obs).max()))
+        err["rew"] = max(err["rew"], float(np.abs(rew.cpu().numpy() - o_rew).max()))
+        err["root"] = max(err["root"], float(np.abs(env.root_tensor.cpu().numpy() - orc.a["root"]).max()))
+        err["reset_equal"] &= bool(np.array_equal(reset.cpu().numpy(), o_reset))
+        err["timeout_equal"] &= bool(np.array_equal(extras["time_outs"].cpu().numpy().astype(np.uint8), o_to))
+    err["min_height"] = float(orc.a["root"][:, 2].min())
+    return err

@@ -20,7 +20,7 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
-        srcs = [os.path.join(REPO, "oracle", f) for f in ("gogoro_task.c", "physics_ref.c")]
+        srcs = [os.path.join(REPO, "oracle", f) for f in ("gogoro_task.c", "physics_ref.c", "walk_task.c")]
         if not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in srcs):
             subprocess.run(["make", "-C", os.path.join(REPO, "oracle")], check=True, capture_output=True)
         _lib = C.CDLL(LIB)
@@ -29,6 +29,9 @@ def lib():
         _lib.oracle_gogoro_reward.argtypes = [C.c_int, vp, vp, vp, C.c_int64, vp, vp]
         _lib.oracle_gogoro_pre_physics.argtypes = [vp, vp, vp, vp]
         _lib.oracle_gogoro_post_physics.argtypes = [vp, vp, vp, vp, vp, vp]
+        _lib.oracle_walk_pre_physics.argtypes = [vp, vp, vp]
+        _lib.oracle_walk_post_physics.argtypes = [vp, vp, vp, vp]
+        _lib.oracle_walk_reset_env.argtypes = [vp, vp, C.c_int, vp]
         _lib.oracle_physics_step.argtypes = [vp, vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_int]
     return _lib
 

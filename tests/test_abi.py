@@ -15,7 +15,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared_symbols():
     out = set()
-    for h in ("tgsim.h", "tg_gogoro.h"):
+    for h in ("tgsim.h", "tg_gogoro.h", "tg_walk.h"):
         text = open(os.path.join(REPO, "include", h)).read()
         out |= set(re.findall(r"^(?:int|const char \*|uint64_t)\s*(tg_\w+)\(", text, re.M))
     return out
@@ -68,11 +68,12 @@ def test_struct_layouts_match_c():
 #include <stdio.h>
 #include <stddef.h>
 #include "tg_gogoro.h"
+#include "tg_walk.h"
 int main(void){
  printf("%zu %zu %zu %zu %zu\n", sizeof(tg_model_desc), sizeof(tg_sim_params), sizeof(tg_state_view),
         sizeof(tg_gogoro_params), sizeof(tg_gogoro_buffers));
- printf("%zu %zu %zu\n", offsetof(tg_gogoro_params, max_episode_length), offsetof(tg_gogoro_params, seed),
-        offsetof(tg_model_desc, model_hash));
+ printf("%zu %zu %zu %zu %zu\n", offsetof(tg_gogoro_params, max_episode_length), offsetof(tg_gogoro_params, seed),
+        offsetof(tg_model_desc, model_hash), sizeof(tg_walk_params), sizeof(tg_walk_buffers));
  return 0;}
 '''
     tmp = os.path.join(REPO, "oracle", "_build")
@@ -85,5 +86,5 @@ int main(void){
     sizes = [C.sizeof(t) for t in (abi.tg_model_desc, abi.tg_sim_params, abi.tg_state_view, abi.tg_gogoro_params,
                                    abi.tg_gogoro_buffers)]
     offs = [abi.tg_gogoro_params.max_episode_length.offset, abi.tg_gogoro_params.seed.offset,
-            abi.tg_model_desc.model_hash.offset]
+            abi.tg_model_desc.model_hash.offset, C.sizeof(abi.tg_walk_params), C.sizeof(abi.tg_walk_buffers)]
     assert [int(x) for x in out] == sizes + offs

@@ -44,6 +44,11 @@ SIGNATURES = {
                                _VP, _VP, C.c_uint64],
     "tg_gogoro_reset_idx": [_VP, C.POINTER(abi.tg_gogoro_params), C.POINTER(abi.tg_gogoro_buffers), _VP,
                             C.c_int32, _VP, C.c_uint64],
+    "tg_walk_pre_physics": [_VP, C.POINTER(abi.tg_walk_params), C.POINTER(abi.tg_walk_buffers), _VP],
+    "tg_walk_post_physics": [_VP, C.POINTER(abi.tg_walk_params), C.POINTER(abi.tg_walk_buffers), _VP, _VP,
+                             C.c_uint64],
+    "tg_walk_reset_idx": [_VP, C.POINTER(abi.tg_walk_params), C.POINTER(abi.tg_walk_buffers), _VP, C.c_int32,
+                          _VP, C.c_uint64],
 }
 
 

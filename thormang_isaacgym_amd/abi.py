@@ -85,6 +85,32 @@ class tg_gogoro_buffers(C.Structure):
         "dof_props", "env_dirty")]
 
 
+TG_WALK_MAX_DOF = 40
+F40 = C.c_float * TG_WALK_MAX_DOF
+
+
+class tg_walk_params(C.Structure):
+    _fields_ = [
+        ("num_envs", C.c_int32), ("num_dof", C.c_int32), ("num_obs", C.c_int32), ("num_groups", C.c_int32),
+        ("action_scale", C.c_float), ("clip_actions", C.c_float), ("clip_obs", C.c_float),
+        ("lin_vel_scale", C.c_float), ("ang_vel_scale", C.c_float), ("dof_pos_scale", C.c_float),
+        ("dof_vel_scale", C.c_float), ("cmd_vx", F2), ("cmd_vy", F2), ("cmd_wz", F2),
+        ("rew_lin_vel_xy", C.c_float), ("rew_ang_vel_z", C.c_float), ("rew_upright", C.c_float),
+        ("rew_alive", C.c_float), ("rew_action_rate", C.c_float), ("rew_dof_vel", C.c_float),
+        ("rew_torque", C.c_float), ("rew_termination", C.c_float), ("rew_height", C.c_float),
+        ("target_height", C.c_float), ("termination_height", C.c_float), ("termination_up", C.c_float),
+        ("spawn_height", C.c_float), ("joint_noise", C.c_float), ("push_force", C.c_float),
+        ("push_interval", C.c_int32), ("max_episode_length", C.c_int64), ("dt", C.c_float),
+        ("default_pos", F40), ("stiffness", F40), ("seed", C.c_uint64),
+    ]
+
+
+class tg_walk_buffers(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in (
+        "obs_buf", "rew_buf", "reset_buf", "progress_buf", "timeout_buf", "actions", "last_actions", "commands",
+        "root_reset", "root", "dof_state", "pos_target", "body_force", "env_dirty")]
+
+
 def model_arrays(m: Model) -> Dict[str, np.ndarray]:
     """Flatten a grouped Model into the tg_model_desc arrays (numpy, C-contiguous)."""
     L, D, G, S = m.num_bodies, m.num_dof, m.num_groups, len(m.shapes)

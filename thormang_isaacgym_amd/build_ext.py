@@ -24,6 +24,7 @@ UNITS = {
     "articulation.hip": ["-O3", "-ffast-math", "-munsafe-fp-atomics"],
     # task math must follow the reference's fp32 operation order
     "gogoro_task.hip": ["-O3", "-ffp-contract=off"],
+    "walk_task.hip": ["-O3", "-ffp-contract=off"],
     "tgsim_api.cpp": ["-O2", "-x", "hip"],
 }
 

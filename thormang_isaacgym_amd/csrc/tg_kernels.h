@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "../../include/tg_gogoro.h"
+#include "../../include/tg_walk.h"
 #include "../../include/tgsim.h"
 
 namespace tg {
@@ -42,6 +43,12 @@ int launch_gogoro_post(const tg_gogoro_params &p, const tg_gogoro_buffers &b, co
 
 int launch_gogoro_reset_idx(const tg_gogoro_params &p, const tg_gogoro_buffers &b, const int32_t *ids, int n,
                             const float *reset_draws, uint64_t counter, hipStream_t stream);
+
+int launch_walk_pre(const tg_walk_params &p, const tg_walk_buffers &b, const float *actions, hipStream_t s);
+int launch_walk_post(const tg_walk_params &p, const tg_walk_buffers &b, const float *rd, const float *pd,
+                     uint64_t counter, hipStream_t s);
+int launch_walk_reset_idx(const tg_walk_params &p, const tg_walk_buffers &b, const int32_t *ids, int n,
+                          const float *rd, uint64_t counter, hipStream_t s);
 
 // indexed scatter: dst[ids[i]*row + k] = src[ids[i]*row + k]
 int launch_scatter_rows(float *dst, const float *src, const int32_t *ids, int n, int row, hipStream_t stream);

@@ -386,4 +386,39 @@ int tg_gogoro_reset_idx(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_bu
     return TG_OK;
 }
 
+static int check_walk(tg_sim *s, const tg_walk_params *p, const tg_walk_buffers *b) {
+    if (int rc = check_sim(s)) return rc;
+    if (!p || !b) return fail(TG_ERR_ARG, "walk: null argument");
+    if (p->num_envs != s->N || p->num_dof != s->D || p->num_groups != s->G)
+        return fail(TG_ERR_ARG, "walk params do not match the sim (N %d/%d, D %d/%d, G %d/%d)", p->num_envs, s->N,
+                    p->num_dof, s->D, p->num_groups, s->G);
+    if (p->num_dof > TG_WALK_MAX_DOF) return fail(TG_ERR_ARG, "walk: num_dof %d > %d", p->num_dof, TG_WALK_MAX_DOF);
+    if (p->num_obs != TG_WALK_NUM_OBS_BASE + 3 * p->num_dof) return fail(TG_ERR_ARG, "walk: num_obs mismatch");
+    return 0;
+}
+
+int tg_walk_pre_physics(tg_sim *s, const tg_walk_params *p, const tg_walk_buffers *b, const float *actions) {
+    if (int rc = check_walk(s, p, b)) return rc;
+    if (!actions) return fail(TG_ERR_ARG, "walk: null actions");
+    if (int rc = tg::launch_walk_pre(*p, *b, actions, s->stream)) return fail(rc, "launch failed");
+    return TG_OK;
+}
+
+int tg_walk_post_physics(tg_sim *s, const tg_walk_params *p, const tg_walk_buffers *b, const float *reset_draws,
+                         const float *push_draws, uint64_t counter) {
+    if (int rc = check_walk(s, p, b)) return rc;
+    if (int rc = tg::launch_walk_post(*p, *b, reset_draws, push_draws, counter, s->stream))
+        return fail(rc, "launch failed");
+    return TG_OK;
+}
+
+int tg_walk_reset_idx(tg_sim *s, const tg_walk_params *p, const tg_walk_buffers *b, const int32_t *ids, int32_t n,
+                      const float *reset_draws, uint64_t counter) {
+    if (int rc = check_walk(s, p, b)) return rc;
+    if (int rc = check_ids(s, ids, n)) return rc;
+    if (int rc = tg::launch_walk_reset_idx(*p, *b, ids, n, reset_draws, counter, s->stream))
+        return fail(rc, "launch failed");
+    return TG_OK;
+}
+
 }  // extern "C"

@@ -1,0 +1,194 @@
+// walk_task.hip -- fused ThormangWalk task kernels (include/tg_walk.h), one env
+// per lane.  The reference has no walking task; the
+// semantics are this build's design and are checked against oracle/walk_task.c.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "../../include/tg_walk.h"
+#include "tg_kernels.h"
+
+namespace tg {
+
+#define W_PI 3.14159265358979323846f
+
+__device__ __forceinline__ float clampw(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+__global__ __launch_bounds__(256) void walk_pre_kernel(tg_walk_params p, tg_walk_buffers b, const float *actions) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int D = p.num_dof;
+    if (t >= (size_t)p.num_envs * D) return;
+    const int d = (int)(t % D);
+    float a = clampw(actions[t], -p.clip_actions, p.clip_actions);
+    b.actions[t] = a;
+    b.pos_target[t] = p.default_pos[d] + p.action_scale * a;
+}
+
+__device__ void walk_reset_draws(const tg_walk_params &p, int e, uint32_t c_lo, uint32_t c_hi, float *r) {
+    const int n = 4 + 2 * p.num_dof;
+    for (int k = 0; k < n; k += 4) {
+        U4 x = philox(U4{(uint32_t)e, c_lo, c_hi, 0x57524530u + (uint32_t)(k >> 2)}, (uint32_t)p.seed,
+                      (uint32_t)(p.seed >> 32));
+        r[k] = u01(x.x);
+        if (k + 1 < n) r[k + 1] = u01(x.y);
+        if (k + 2 < n) r[k + 2] = u01(x.z);
+        if (k + 3 < n) r[k + 3] = u01(x.w);
+    }
+}
+
+__device__ void walk_reset_env(const tg_walk_params &p, const tg_walk_buffers &b, int e, const float *r) {
+    const int D = p.num_dof;
+    b.commands[3 * (size_t)e + 0] = p.cmd_vx[0] + r[0] * (p.cmd_vx[1] - p.cmd_vx[0]);
+    b.commands[3 * (size_t)e + 1] = p.cmd_vy[0] + r[1] * (p.cmd_vy[1] - p.cmd_vy[0]);
+    b.commands[3 * (size_t)e + 2] = p.cmd_wz[0] + r[2] * (p.cmd_wz[1] - p.cmd_wz[0]);
+    const float yaw = (r[3] * 2.0f - 1.0f) * W_PI;
+    float *root = b.root + 13 * (size_t)e;
+    const float *tpl = b.root_reset + 13 * (size_t)e;
+    root[0] = tpl[0];
+    root[1] = tpl[1];
+    root[2] = p.spawn_height;
+    root[3] = 0.0f;
+    root[4] = 0.0f;
+    root[5] = sinf(0.5f * yaw);
+    root[6] = cosf(0.5f * yaw);
+#pragma unroll
+    for (int k = 7; k < 13; ++k) root[k] = 0.0f;
+    for (int d = 0; d < D; ++d) {
+        const size_t i = (size_t)e * D + d;
+        b.dof_state[2 * i] = p.default_pos[d] + (r[4 + d] * 2.0f - 1.0f) * p.joint_noise;
+        b.dof_state[2 * i + 1] = 0.1f * (r[4 + D + d] * 2.0f - 1.0f);
+        b.last_actions[i] = 0.0f;
+        b.actions[i] = 0.0f;
+    }
+    b.progress_buf[e] = 0;
+    b.reset_buf[e] = 0;
+}
+
+__device__ void walk_observe(const tg_walk_params &p, const tg_walk_buffers &b, int e, int64_t prog) {
+    const int D = p.num_dof;
+    const float *r = b.root + 13 * (size_t)e;
+    const float x = r[3], y = r[4], z = r[5], w = r[6];
+    const float R[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w),
+                        2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w),
+                        2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)};
+    float vb[3], wb[3], gb[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        vb[i] = R[i] * r[7] + R[3 + i] * r[8] + R[6 + i] * r[9];
+        wb[i] = R[i] * r[10] + R[3 + i] * r[11] + R[6 + i] * r[12];
+        gb[i] = -R[6 + i];
+    }
+    float *o = b.obs_buf + (size_t)p.num_obs * e;
+    const float *cmd = b.commands + 3 * (size_t)e;
+    const float co = p.clip_obs;
+    o[0] = clampw(r[2], -co, co);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        o[1 + i] = clampw(vb[i] * p.lin_vel_scale, -co, co);
+        o[4 + i] = clampw(wb[i] * p.ang_vel_scale, -co, co);
+        o[7 + i] = clampw(gb[i], -co, co);
+    }
+    o[10] = clampw(cmd[0] * p.lin_vel_scale, -co, co);
+    o[11] = clampw(cmd[1] * p.lin_vel_scale, -co, co);
+    o[12] = clampw(cmd[2] * p.ang_vel_scale, -co, co);
+    float rate = 0.0f, vel2 = 0.0f, tq = 0.0f;
+    const float *ds = b.dof_state + 2 * (size_t)e * D;
+    for (int d = 0; d < D; ++d) {
+        const size_t i = (size_t)e * D + d;
+        const float q = ds[2 * d], qd = ds[2 * d + 1];
+        const float a = b.actions[i], la = b.last_actions[i];
+        o[13 + d] = clampw((q - p.default_pos[d]) * p.dof_pos_scale, -co, co);
+        o[13 + D + d] = clampw(qd * p.dof_vel_scale, -co, co);
+        o[13 + 2 * D + d] = clampw(a, -co, co);
+        rate += (a - la) * (a - la);
+        vel2 += qd * qd;
+        const float t = p.stiffness[d] * (b.pos_target[i] - q);
+        tq += t * t;
+        b.last_actions[i] = a;
+    }
+    const float lin_err = (cmd[0] - vb[0]) * (cmd[0] - vb[0]) + (cmd[1] - vb[1]) * (cmd[1] - vb[1]);
+    const float ang_err = (cmd[2] - wb[2]) * (cmd[2] - wb[2]);
+    const float dz = r[2] - p.target_height;
+    float rew = p.rew_lin_vel_xy * expf(-lin_err / 0.25f) + p.rew_ang_vel_z * expf(-ang_err / 0.25f) +
+                p.rew_upright * (-gb[2]) + p.rew_alive + p.rew_height * expf(-dz * dz / 0.01f) +
+                p.rew_action_rate * rate + p.rew_dof_vel * vel2 + p.rew_torque * tq;
+    const bool fall = (r[2] < p.termination_height) || (-gb[2] < p.termination_up);
+    if (fall) rew += p.rew_termination;
+    const bool reset = fall || prog >= p.max_episode_length - 1;
+    b.rew_buf[e] = rew;
+    b.reset_buf[e] = reset ? 1 : 0;
+    b.timeout_buf[e] = (prog >= p.max_episode_length - 1) && reset;
+}
+
+__global__ __launch_bounds__(64) void walk_post_kernel(tg_walk_params p, tg_walk_buffers b, const float *reset_draws,
+                                                       const float *push_draws, uint32_t c_lo, uint32_t c_hi) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= p.num_envs) return;
+    const int D = p.num_dof;
+    int64_t prog = b.progress_buf[e] + 1;
+    b.progress_buf[e] = prog;
+    if (b.reset_buf[e] != 0) {
+        float r[4 + 2 * TG_WALK_MAX_DOF];
+        if (reset_draws) {
+            for (int k = 0; k < 4 + 2 * D; ++k) r[k] = reset_draws[(size_t)(4 + 2 * D) * e + k];
+        } else {
+            walk_reset_draws(p, e, c_lo, c_hi, r);
+        }
+        walk_reset_env(p, b, e, r);
+        prog = 0;
+    }
+    walk_observe(p, b, e, prog);
+    if (b.body_force) {
+        float *f = b.body_force + (size_t)6 * p.num_groups * e;
+        const bool push = p.push_force > 0.0f && p.push_interval > 0 && prog > 0 && (prog % p.push_interval) == 0;
+        float u[3];
+        if (push_draws) {
+            u[0] = push_draws[3 * (size_t)e]; u[1] = push_draws[3 * (size_t)e + 1]; u[2] = push_draws[3 * (size_t)e + 2];
+        } else {
+            U4 x = philox(U4{(uint32_t)e, c_lo, c_hi, 0x50555348u}, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+            u[0] = u01(x.x); u[1] = u01(x.y); u[2] = u01(x.z);
+        }
+        f[0] = push ? p.push_force * (u[0] * 2.0f - 1.0f) : 0.0f;
+        f[1] = push ? p.push_force * (u[1] * 2.0f - 1.0f) : 0.0f;
+        f[2] = push ? 0.25f * p.push_force * (u[2] * 2.0f - 1.0f) : 0.0f;
+        f[3] = 0.0f; f[4] = 0.0f; f[5] = 0.0f;
+    }
+}
+
+__global__ __launch_bounds__(64) void walk_reset_idx_kernel(tg_walk_params p, tg_walk_buffers b, const int32_t *ids,
+                                                            int n, const float *reset_draws, uint32_t c_lo,
+                                                            uint32_t c_hi) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int e = ids[i];
+    if (e < 0 || e >= p.num_envs) return;
+    const int D = p.num_dof;
+    float r[4 + 2 * TG_WALK_MAX_DOF];
+    if (reset_draws) {
+        for (int k = 0; k < 4 + 2 * D; ++k) r[k] = reset_draws[(size_t)(4 + 2 * D) * e + k];
+    } else {
+        walk_reset_draws(p, e, c_lo, c_hi, r);
+    }
+    walk_reset_env(p, b, e, r);
+    walk_observe(p, b, e, 0);
+}
+
+int launch_walk_pre(const tg_walk_params &p, const tg_walk_buffers &b, const float *actions, hipStream_t s) {
+    const size_t tot = (size_t)p.num_envs * p.num_dof;
+    hipLaunchKernelGGL(walk_pre_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, p, b, actions);
+    return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
+}
+int launch_walk_post(const tg_walk_params &p, const tg_walk_buffers &b, const float *rd, const float *pd,
+                     uint64_t counter, hipStream_t s) {
+    hipLaunchKernelGGL(walk_post_kernel, dim3((p.num_envs + 63) / 64), dim3(64), 0, s, p, b, rd, pd,
+                       (uint32_t)counter, (uint32_t)(counter >> 32));
+    return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
+}
+int launch_walk_reset_idx(const tg_walk_params &p, const tg_walk_buffers &b, const int32_t *ids, int n,
+                          const float *rd, uint64_t counter, hipStream_t s) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(walk_reset_idx_kernel, dim3((n + 63) / 64), dim3(64), 0, s, p, b, ids, n, rd,
+                       (uint32_t)counter, (uint32_t)(counter >> 32));
+    return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
+}
+
+}  // namespace tg

@@ -131,6 +131,47 @@ class Model:
                 return i
         raise KeyError(name)
 
+    def forward_kinematics(self, q: Dict[str, float]) -> List[tuple]:
+        """World (R, p) of every link with the root at the origin and joint
+        positions ``q`` by dof name (missing names = 0)."""
+        out = []
+        for link in self.links:
+            if link.parent < 0:
+                out.append((np.eye(3), np.zeros(3)))
+                continue
+            j = self.joints[link.joint]
+            R = np.asarray(j.origin_rot, np.float64)
+            t = np.asarray(j.origin_pos, np.float64)
+            th = float(q.get(j.name, 0.0)) if j.jtype != JOINT_FIXED else 0.0
+            a = np.asarray(j.axis, np.float64)
+            if j.jtype == JOINT_REVOLUTE:
+                K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+                R = R @ (np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K)
+            elif j.jtype == JOINT_PRISMATIC:
+                t = t + R @ a * th
+            Rp, pp = out[link.parent]
+            out.append((Rp @ R, pp + Rp @ t))
+        return out
+
+    def lowest_point(self, q: Dict[str, float]) -> float:
+        """Lowest z over all collision shapes (box corners / sphere / torus bottoms) at pose q."""
+        fk = self.forward_kinematics(q)
+        zmin = math.inf
+        for s in self.shapes:
+            R, p = fk[self.link_index(s.link)]
+            Rs = R @ np.asarray(s.rot)
+            c = p + R @ np.asarray(s.pos)
+            if s.kind == "box":
+                for sx in (-1, 1):
+                    for sy in (-1, 1):
+                        for sz in (-1, 1):
+                            zmin = min(zmin, (c + Rs @ (np.array([sx, sy, sz]) * np.asarray(s.params)))[2])
+            elif s.kind == "sphere":
+                zmin = min(zmin, c[2] - s.params[0])
+            else:
+                zmin = min(zmin, c[2] - s.params[0] * np.sqrt(max(0.0, 1 - Rs[2, 2] ** 2)) - s.params[1])
+        return zmin
+
     def to_json(self) -> str:
         return json.dumps(asdict(self), indent=1)
 
