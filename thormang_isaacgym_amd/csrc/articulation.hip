@@ -376,7 +376,7 @@ template <class M> __global__ __launch_bounds__(64) void step_kernel(StepArgs a)
                 Rs = mul(w.Rw[g], Rsl);
                 V3 cl = v3(CP(CL::shape(s) + 9), CP(CL::shape(s) + 10), CP(CL::shape(s) + 11));
                 V3 cw = w.pw[g] + mul(w.Rw[g], cl);
-                V3 pts[M::shape_nrows[s] > 0 ? 4 : 1];
+                V3 pts[4];
                 if (M::shape_kind[s] == TG_SHAPE_TORUS) {
                     V3 ax = v3(Rs.a[2], Rs.a[5], Rs.a[8]);
                     V3 dd = v3(-ax.z * ax.x, -ax.z * ax.y, 1.f - ax.z * ax.z);
@@ -577,14 +577,41 @@ template <class M> __global__ __launch_bounds__(64) void step_kernel(StepArgs a)
     }
 }
 
+}  // namespace tg
+
+#include "step_lds.h"
+
+namespace tg {
+
 // ---------------------------------------------------------------- dispatch
-#define TG_LAUNCH(MODEL)                                                                      \
-    if (hash == MODEL::hash) {                                                                \
-        dim3 grid((a.N + 63) / 64), block(64);                                                \
-        hipLaunchKernelGGL(compose_kernel<MODEL>, grid, block, 0, stream, a);                 \
-        hipLaunchKernelGGL(step_kernel<MODEL>, grid, block, 0, stream, a);                    \
-        return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;                              \
+// Small trees: fully unrolled register-resident step_kernel, 64 envs/block.
+// Large trees (M::use_lds): LDS-resident step_lds_kernel, LDS_EPB envs/block
+// (Thormang: 16 envs x 2370 floats = 148 KB of the 160 KB LDS per CU).
+constexpr int LDS_EPB = 16;
+
+template <class M> int launch_model(const StepArgs &a, hipStream_t stream) {
+    const dim3 cgrid((a.N + 63) / 64), cblock(64);
+    hipLaunchKernelGGL(compose_kernel<M>, cgrid, cblock, 0, stream, a);
+    if constexpr (M::use_lds) {
+        constexpr size_t bytes = (size_t)LdsLayout<M>::TOTAL * LDS_EPB * sizeof(float);
+        static_assert(bytes <= 160 * 1024, "LDS budget");
+        static bool attr = false;
+        if (!attr) {
+            if (hipFuncSetAttribute((const void *)step_lds_kernel<M, LDS_EPB>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess)
+                return TG_ERR_HIP;
+            attr = true;
+        }
+        hipLaunchKernelGGL((step_lds_kernel<M, LDS_EPB>), dim3((a.N + LDS_EPB - 1) / LDS_EPB), dim3(LDS_EPB), bytes,
+                           stream, a);
+    } else {
+        hipLaunchKernelGGL(step_kernel<M>, cgrid, cblock, 0, stream, a);
     }
+    return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
+}
+
+#define TG_LAUNCH(MODEL) \
+    if (hash == MODEL::hash) return launch_model<MODEL>(a, stream);
 
 int launch_step(uint64_t hash, const StepArgs &a, hipStream_t stream) {
     TG_FOR_EACH_MODEL(TG_LAUNCH)
