@@ -1,0 +1,37 @@
+"""Per-section cycle breakdown of the LDS articulation kernel (developer tool).
+
+Needs the profiling build:
+    TG_EXTRA_FLAGS=-DTG_SECTION_PROF TG_LIB_NAME=libtgsim_prof.so python thormang_isaacgym_amd/build_ext.py
+    TG_LIB_PATH=thormang_isaacgym_amd/libtgsim_prof.so python scripts/section_prof.py
+"""
+import ctypes as C
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import thormang_isaacgym_amd as tia  # noqa: E402
+from thormang_isaacgym_amd import _lib  # noqa: E402
+
+NAMES = ["load", "pass1", "pass2", "pass3", "contact setup", "delassus", "pgs", "apply", "integrate", "store"]
+
+
+def main():
+    task = sys.argv[1] if len(sys.argv) > 1 else "ThormangWalk"
+    env = tia.make(seed=0, task=task, num_envs=4096, sim_device="cuda:0", rl_device="cuda:0")
+    L = _lib.lib()
+    L.tg_prof_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    g = torch.Generator(device="cuda:0").manual_seed(0)
+    for _ in range(20):
+        env.step(torch.rand(4096, env.num_actions, device="cuda:0", generator=g) * 2 - 1)
+    torch.cuda.synchronize()
+    buf = (C.c_ulonglong * 16)()
+    L.tg_prof_read(buf, 16)
+    tot = sum(buf[:len(NAMES)])
+    for n, v in zip(NAMES, buf):
+        print(f"{n:14s} {v / tot * 100:6.2f} %  {v:14d}")
+
+
+if __name__ == "__main__":
+    main()

@@ -10,7 +10,7 @@ import os
 from . import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libtgsim.so")
+LIB_PATH = os.environ.get("TG_LIB_PATH") or os.path.join(HERE, "libtgsim.so")
 
 _lib = None
 

@@ -15,7 +15,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 BUILD = os.path.join(REPO, "build", "tgsim")
-LIB = os.path.join(HERE, "libtgsim.so")
+LIB = os.path.join(HERE, os.environ.get("TG_LIB_NAME", "libtgsim.so"))
+# developer builds (e.g. TG_EXTRA_FLAGS=-DTG_SECTION_PROF TG_LIB_NAME=libtgsim_prof.so) get their own objects
+EXTRA = os.environ.get("TG_EXTRA_FLAGS", "").split()
+if EXTRA:
+    BUILD = BUILD + "_" + "_".join(f.strip("-").replace("=", "_") for f in EXTRA)
 ARCH = os.environ.get("TG_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
@@ -48,7 +52,7 @@ def build(verbose: bool = False, jobs: int = 4) -> str:
         if os.path.exists(o) and os.path.getmtime(o) >= max(os.path.getmtime(s), dep_mtime):
             continue
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
-               "-Wno-unused-variable", *flags, "-c", s, "-o", o]
+               "-Wno-unused-variable", *flags, *EXTRA, "-c", s, "-o", o]
         if verbose:
             print(" ".join(cmd))
         procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))

@@ -579,31 +579,31 @@ template <class M> __global__ __launch_bounds__(64) void step_kernel(StepArgs a)
 
 }  // namespace tg
 
-#include "step_lds.h"
+#include "step_par.h"
 
 namespace tg {
 
 // ---------------------------------------------------------------- dispatch
 // Small trees: fully unrolled register-resident step_kernel, 64 envs/block.
-// Large trees (M::use_lds): LDS-resident step_lds_kernel, LDS_EPB envs/block
-// (Thormang: 16 envs x 2370 floats = 148 KB of the 160 KB LDS per CU).
+// Large trees (M::use_lds): tree-parallel LDS-resident step_par_kernel,
+// LDS_EPB envs x M::LPE lanes per block (Thormang: 16 envs, 151 KB of LDS).
 constexpr int LDS_EPB = 16;
 
 template <class M> int launch_model(const StepArgs &a, hipStream_t stream) {
     const dim3 cgrid((a.N + 63) / 64), cblock(64);
     hipLaunchKernelGGL(compose_kernel<M>, cgrid, cblock, 0, stream, a);
     if constexpr (M::use_lds) {
-        constexpr size_t bytes = (size_t)LdsLayout<M>::TOTAL * LDS_EPB * sizeof(float);
+        constexpr size_t bytes = ParLayout<M>::template bytes<LDS_EPB>();
         static_assert(bytes <= 160 * 1024, "LDS budget");
         static bool attr = false;
         if (!attr) {
-            if (hipFuncSetAttribute((const void *)step_lds_kernel<M, LDS_EPB>,
+            if (hipFuncSetAttribute((const void *)step_par_kernel<M, LDS_EPB>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess)
                 return TG_ERR_HIP;
             attr = true;
         }
-        hipLaunchKernelGGL((step_lds_kernel<M, LDS_EPB>), dim3((a.N + LDS_EPB - 1) / LDS_EPB), dim3(LDS_EPB), bytes,
-                           stream, a);
+        hipLaunchKernelGGL((step_par_kernel<M, LDS_EPB>), dim3((a.N + LDS_EPB - 1) / LDS_EPB), dim3(LDS_EPB * M::LPE),
+                           bytes, stream, a);
     } else {
         hipLaunchKernelGGL(step_kernel<M>, cgrid, cblock, 0, stream, a);
     }
@@ -629,6 +629,14 @@ int launch_compose(uint64_t hash, const StepArgs &a, hipStream_t stream) {
     TG_FOR_EACH_MODEL(TG_COMPOSE)
     return TG_ERR_MODEL;
 }
+
+#ifdef TG_SECTION_PROF
+extern "C" int tg_prof_read(unsigned long long *out, int n) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tg_prof_acc), sizeof(unsigned long long) * (n < 16 ? n : 16)) != hipSuccess)
+        return -1;
+    return 0;
+}
+#endif
 
 #define TG_HASH(MODEL) if (n < cap) out[n] = MODEL::hash; ++n;
 #define TG_KC(MODEL) if (hash == MODEL::hash) return MODEL::KC;

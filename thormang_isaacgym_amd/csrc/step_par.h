@@ -1,0 +1,677 @@
+// step_par.h -- tree-parallel, LDS-resident articulation step for large joint
+// trees (included by articulation.hip after the shared helpers; same algorithm
+// and operation order per group as step_kernel<M> and oracle/physics_ref.c).
+//
+// Layout: EPB envs per workgroup, LPE lanes per env (LPE consecutive lanes of
+// one wavefront).  Each env's articulated state (per group: X, v, I^A, p^A, U,
+// D^-1, u, q, qd, qds, gravity-in-frame) lives in LDS at
+// lds[env * ES + group * GF + field]; ES is odd so the same field of the 8
+// envs of a wavefront falls in distinct banks.  At 16 envs x 2370 floats the
+// Thormang block uses 148 KB of the 160 KB LDS of a CU; 4096 envs = 256
+// workgroups = one per CU.
+//
+// Parallelism inside an env: model/codegen.py list-schedules the non-root
+// groups onto the LPE lanes (M::sched[step][lane], parents at earlier steps).
+//   pass 1 (kinematics, velocities, bias)      -- schedule forward
+//   pass 2 (articulated inertias)               -- schedule backward; a group
+//          gathers its children's contributions (each child leaves
+//          X^T I^a X and X^T p^a in its own I^A / p^A slots), so lanes never
+//          accumulate into the same address
+//   pass 3 (accelerations), impulse application -- forward / backward again
+//   Delassus columns                            -- one column per lane, the
+//          impulse's up-walk kept in registers (path-restricted: only the
+//          ancestors of the contact group and the root->contact-group paths)
+//   PGS                                         -- lane 0 of the env
+// The root (group 0) quantities that every lane needs (pose, base velocity,
+// root LDL factor) are computed redundantly in all lanes of the env.
+#pragma once
+
+namespace tg {
+
+#ifdef TG_SECTION_PROF
+// developer build only: per-section cycle counts summed over thread 0 of every block
+__device__ unsigned long long tg_prof_acc[16];
+#define TG_PROF_INIT unsigned long long tg_t0 = clock64();
+#define TG_PROF(k)                                                              \
+    {                                                                           \
+        const unsigned long long t1 = clock64();                               \
+        if (threadIdx.x == 0) atomicAdd(&tg_prof_acc[k], t1 - tg_t0);           \
+        tg_t0 = t1;                                                             \
+    }
+#else
+#define TG_PROF_INIT
+#define TG_PROF(k)
+#endif
+
+// one env's LDS state
+struct LE {
+    float *b;
+    __device__ __forceinline__ float &operator()(int i) const { return b[i]; }
+};
+
+// per-group field offsets (GF floats per group)
+enum : int {
+    F_E = 0, F_R = 9, F_V = 12, F_IA = 18, F_PA = 39, F_U = 45, F_DINV = 51, F_UU = 52, F_Q = 53, F_QD = 54,
+    F_QDS = 55, F_GL = 56, GF = 59
+};
+
+__device__ __forceinline__ V3 ldv3(const LE &s, int o) { return v3(s(o), s(o + 1), s(o + 2)); }
+__device__ __forceinline__ void stv3(const LE &s, int o, V3 v) { s(o) = v.x; s(o + 1) = v.y; s(o + 2) = v.z; }
+__device__ __forceinline__ SV ldsv(const LE &s, int o) { return SV{ldv3(s, o), ldv3(s, o + 3)}; }
+__device__ __forceinline__ void stsv(const LE &s, int o, const SV &v) { stv3(s, o, v.w); stv3(s, o + 3, v.v); }
+__device__ __forceinline__ M3 ldm3(const LE &s, int o) {
+    M3 m;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) m.a[k] = s(o + k);
+    return m;
+}
+__device__ __forceinline__ void stm3(const LE &s, int o, const M3 &m) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) s(o + k) = m.a[k];
+}
+__device__ __forceinline__ SI ldsi(const LE &s, int o) {
+    SI I;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) { I.A[k] = s(o + k); I.C[k] = s(o + 15 + k); }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) I.B[k] = s(o + 6 + k);
+    return I;
+}
+__device__ __forceinline__ void stsi(const LE &s, int o, const SI &I) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) { s(o + k) = I.A[k]; s(o + 15 + k) = I.C[k]; }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) s(o + 6 + k) = I.B[k];
+}
+__device__ __forceinline__ Xf ldx(const LE &s, int g) { return Xf{ldm3(s, g * GF + F_E), ldv3(s, g * GF + F_R)}; }
+
+// per-group model table in LDS (ints; axis as float bits), built once per block
+enum : int { GI_PARENT = 0, GI_DOF = 1, GI_JT = 2, GI_AX = 3, GI_NCH = 6, GI_CH = 7 };
+
+template <class M> struct ParLayout {
+    static constexpr int K = M::NROWS;
+    static constexpr int GIW = GI_CH + M::MAXC;
+    // per-env floats
+    static constexpr int W = M::NG * GF;             // K*K Delassus
+    static constexpr int ROW = W + K * K;            // K * 8: r(3) d(3) target on
+    static constexpr int VFREE = ROW + K * 8;
+    static constexpr int LAM = VFREE + K;
+    static constexpr int SHP = LAM + K;              // per shape: mu, reff
+    static constexpr int CGP = SHP + 2 * M::NSA;     // per contact group: world R (9), p (3)
+    static constexpr int CGV = CGP + 12 * M::NCG;    // per contact group: free velocity (6)
+    static constexpr int TOTAL = CGV + 6 * M::NCG;
+    static constexpr int ES = TOTAL | 1;             // env stride
+    // per-block ints after the env area
+    static constexpr int T_GI = 0;
+    static constexpr int T_SCHED = M::NG * GIW;
+    static constexpr int T_CPATH = T_SCHED + M::NSTEP * M::LPE;   // [NCG][MAXD]
+    static constexpr int T_TOTAL = T_CPATH + M::NCG * M::MAXD;
+    template <int EPB> static constexpr size_t bytes() { return ((size_t)EPB * ES + T_TOTAL) * 4; }
+};
+
+struct GInfo {
+    int parent, dof, jt;
+    V3 ax;
+    __device__ __forceinline__ SV S() const { return jt == TG_JOINT_REVOLUTE ? SV{ax, v3(0, 0, 0)} : SV{v3(0, 0, 0), ax}; }
+};
+
+template <class M> __device__ __forceinline__ GInfo ginfo(const int *gi, int g) {
+    const int *p = gi + g * ParLayout<M>::GIW;
+    return GInfo{p[GI_PARENT], p[GI_DOF], p[GI_JT], v3(__int_as_float(p[GI_AX]), __int_as_float(p[GI_AX + 1]),
+                                                        __int_as_float(p[GI_AX + 2]))};
+}
+
+// world pose of group g by walking up to the root: R_g = R_0 E_a1^T ... E_g^T
+__device__ __forceinline__ void world_pose(const LE &s, const int *gi, int giw, int g, const M3 &R0, V3 p0, M3 &Rg,
+                                           V3 &pg) {
+    M3 Mr = eye3();
+    V3 t = v3(0, 0, 0);
+    while (g > 0) {
+        const M3 Et = transpose(ldm3(s, g * GF + F_E));
+        t = ldv3(s, g * GF + F_R) + mul(Et, t);
+        Mr = mul(Et, Mr);
+        g = gi[g * giw + GI_PARENT];
+    }
+    Rg = mul(R0, Mr);
+    pg = p0 + mul(R0, t);
+}
+
+#define TG_SYNC() __syncthreads()
+
+template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a) {
+    constexpr int LPE = M::LPE;
+    using CL = CompLayout<M>;
+    using PL = ParLayout<M>;
+    constexpr int K = PL::K;
+    constexpr int GIW = PL::GIW;
+    extern __shared__ float lds_raw[];
+    int *tab = reinterpret_cast<int *>(lds_raw + EPB * PL::ES);
+    const int *gi = tab + PL::T_GI;
+    const int *sched = tab + PL::T_SCHED;
+    const int *cpath = tab + PL::T_CPATH;
+    const int tid = threadIdx.x;
+    const int le = tid / LPE, sub = tid % LPE;
+    const int e = min(blockIdx.x * EPB + le, a.N - 1);   // tail lanes redo the last env, never store
+    const bool owner = blockIdx.x * EPB + le < a.N;
+    TG_PROF_INIT
+
+    for (int i = tid; i < M::NG; i += EPB * LPE) {
+        int *p = tab + PL::T_GI + i * GIW;
+        p[GI_PARENT] = M::parent[i];
+        p[GI_DOF] = M::gdof[i];
+        p[GI_JT] = M::jtype[i];
+        p[GI_AX] = __float_as_int(M::axis[i][0]);
+        p[GI_AX + 1] = __float_as_int(M::axis[i][1]);
+        p[GI_AX + 2] = __float_as_int(M::axis[i][2]);
+        p[GI_NCH] = M::nchild[i];
+        for (int c = 0; c < M::MAXC; ++c) p[GI_CH + c] = M::child[i][c];
+    }
+    for (int i = tid; i < M::NSTEP * LPE; i += EPB * LPE) tab[PL::T_SCHED + i] = M::sched[i / LPE][i % LPE];
+    for (int i = tid; i < M::NCG * M::MAXD; i += EPB * LPE) tab[PL::T_CPATH + i] = M::cpath[i / M::MAXD][i % M::MAXD];
+
+    const LE s{lds_raw + le * PL::ES};
+    const size_t N = a.N;
+    const int D = a.D;
+    const float h = a.h;
+    const bool fix_base = a.fix_base != 0;
+    const float *comp = a.comp;
+    auto CP = [&](int k) { return comp[(size_t)k * N + e]; };
+    auto PR = [&](int f, int d) { return a.props[((size_t)f * N + e) * D + d]; };
+    const bool lead = sub == 0;
+
+    float *root = a.root + (size_t)e * 13;
+    float *dofs = a.dof + (size_t)e * D * 2;
+    TG_SYNC();
+    for (int g = 1 + sub; g < M::NG; g += LPE) {
+        const int d = gi[g * GIW + GI_DOF];
+        s(g * GF + F_Q) = dofs[2 * d];
+        s(g * GF + F_QD) = dofs[2 * d + 1];
+    }
+    V3 pos = v3(root[0], root[1], root[2]);
+    float qx = root[3], qy = root[4], qz = root[5], qw = root[6];
+    {
+        const float in = rsqrtf(qx * qx + qy * qy + qz * qz + qw * qw);
+        qx *= in; qy *= in; qz *= in; qw *= in;
+    }
+    M3 R = quat_to_m3(qx, qy, qz, qw);
+    const V3 c0 = v3(M::root_com[0], M::root_com[1], M::root_com[2]);
+    const V3 ww = v3(root[10], root[11], root[12]);
+    const V3 vo = v3(root[7], root[8], root[9]) - cross(ww, mul(R, c0));
+    SV v0 = fix_base ? sv0() : SV{mulT(R, ww), mulT(R, vo)};
+    const V3 grav = v3(a.gx, a.gy, a.gz);
+
+    // rigid inertia + bias force of group g (pass 1 body), v and gl already known
+    auto body_bias = [&](int g, const SV &vg, V3 gl) {
+        const int o = g * GF;
+        const float m = CP(CL::inertia(g));
+        const V3 cg = v3(CP(CL::inertia(g) + 1), CP(CL::inertia(g) + 2), CP(CL::inertia(g) + 3));
+        float Ic[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) Ic[k] = CP(CL::inertia(g) + 4 + k);
+        const SI I = rb_inertia(m, cg, Ic);
+        stsi(s, o + F_IA, I);
+        const SV b = crf(vg, mul(I, vg));
+        V3 F = m * gl;
+        F = F - (a.lin_damp * m) * (vg.v + cross(vg.w, cg));
+        V3 n = cross(cg, F) - a.ang_damp * symmul(Ic, vg.w);
+        if (a.force) {
+            const float *fw = a.force + ((size_t)e * M::NG + g) * 6;
+            M3 Rw;
+            V3 pw;
+            world_pose(s, gi, GIW, g, R, pos, Rw, pw);
+            const V3 fl = mulT(Rw, v3(fw[0], fw[1], fw[2])), tl = mulT(Rw, v3(fw[3], fw[4], fw[5]));
+            F = F + fl;
+            n = n + tl + cross(cg, fl);
+        }
+        stsv(s, o + F_PA, SV{b.w - n, b.v - F});
+    };
+    TG_SYNC();
+    TG_PROF(0)
+
+    for (int sub_i = 0; sub_i < a.substeps; ++sub_i) {
+        // ---- pass 1: root, then the schedule forward
+        if (lead) {
+            const V3 gl = mulT(R, grav);
+            stsv(s, F_V, v0);
+            stv3(s, F_GL, gl);
+            body_bias(0, v0, gl);
+        }
+        TG_SYNC();
+#pragma unroll 1
+        for (int t = 0; t < M::NSTEP; ++t) {
+            const int g = sched[t * LPE + sub];
+            if (g > 0) {
+                const int o = g * GF;
+                const GInfo G = ginfo<M>(gi, g);
+                M3 Rpc;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) Rpc.a[k] = CP(CL::xtree(g) + k);
+                V3 tr = v3(CP(CL::xtree(g) + 9), CP(CL::xtree(g) + 10), CP(CL::xtree(g) + 11));
+                const float qg = s(o + F_Q);
+                if (G.jt == TG_JOINT_REVOLUTE) Rpc = mul(Rpc, rot_axis(G.ax.x, G.ax.y, G.ax.z, qg));
+                else tr = tr + qg * mul(Rpc, G.ax);
+                const Xf X{transpose(Rpc), tr};
+                stm3(s, o + F_E, X.E);
+                stv3(s, o + F_R, tr);
+                const SV vg = xmotion(X, ldsv(s, G.parent * GF + F_V)) + s(o + F_QD) * G.S();
+                const V3 gl = mul(X.E, ldv3(s, G.parent * GF + F_GL));
+                stsv(s, o + F_V, vg);
+                stv3(s, o + F_GL, gl);
+                body_bias(g, vg, gl);
+            }
+            TG_SYNC();
+        }
+        TG_PROF(1)
+        // ---- pass 2: schedule backward, children contributions gathered
+#pragma unroll 1
+        for (int t = M::NSTEP - 1; t >= 0; --t) {
+            const int g = sched[t * LPE + sub];
+            if (g > 0) {
+                const int o = g * GF;
+                const GInfo G = ginfo<M>(gi, g);
+                const int d = G.dof;
+                const SV S = G.S();
+                SI IA = ldsi(s, o + F_IA);
+                SV pA = ldsv(s, o + F_PA);
+                const int nch = gi[g * GIW + GI_NCH];
+                for (int c = 0; c < nch; ++c) {
+                    const int ch = gi[g * GIW + GI_CH + c];
+                    si_add(IA, ldsi(s, ch * GF + F_IA));
+                    pA = pA + ldsv(s, ch * GF + F_PA);
+                }
+                const SV U = mul(IA, S);
+                const float q = s(o + F_Q), qd = s(o + F_QD);
+                const float D0 = dot(S, U) + PR(TG_PROP_ARMATURE, d);
+                float Dimp = 0.f, tau = 0.f;
+                const int mode = (int)rintf(PR(TG_PROP_DRIVE_MODE, d));
+                const float kp = PR(TG_PROP_STIFFNESS, d), kd = PR(TG_PROP_DAMPING, d);
+                const float eff = PR(TG_PROP_EFFORT, d);
+                if (mode == TG_DOF_MODE_POS || mode == TG_DOF_MODE_VEL) {
+                    const float te = kp * (a.pos_tgt[(size_t)e * D + d] - q - h * qd) + kd * (a.vel_tgt[(size_t)e * D + d] - qd);
+                    if (fabsf(te) <= eff) { tau += te; Dimp += h * kd + h * h * kp; }
+                    else tau += te > 0.f ? eff : -eff;
+                } else if (mode == TG_DOF_MODE_EFFORT && a.act) {
+                    tau += fminf(fmaxf(a.act[(size_t)e * D + d], -eff), eff);
+                }
+                const float lo = PR(TG_PROP_LOWER, d), hi = PR(TG_PROP_UPPER, d);
+                const float qp = q + h * qd;
+                const float kl = a.lim_k * D0 / (h * h), cl = a.lim_c * D0 / h;
+                if (qp < lo && lo > -1e30f) { tau += kl * (lo - qp) - cl * qd; Dimp += h * cl + h * h * kl; }
+                else if (qp > hi && hi < 1e30f) { tau += kl * (hi - qp) - cl * qd; Dimp += h * cl + h * h * kl; }
+                const float Dinv = 1.0f / (D0 + Dimp);
+                const float u = tau - dot(S, pA);
+                stsv(s, o + F_U, U);
+                s(o + F_DINV) = Dinv;
+                s(o + F_UU) = u;
+                SI Ia = IA;
+                si_sub_outer(Ia, U, Dinv);
+                const SV cb = crm(ldsv(s, o + F_V), qd * S);
+                const SV pa = pA + mul(Ia, cb) + (u * Dinv) * U;
+                const Xf X = ldx(s, g);
+                stsi(s, o + F_IA, si_to_parent(Ia, X));     // contribution to the parent
+                stsv(s, o + F_PA, xTforce(X, pa));
+            }
+            TG_SYNC();
+        }
+        // root: every lane factors the root articulated inertia itself
+        LDL6 rootf{};
+        SV a0 = sv0();
+        {
+            SI IA0 = ldsi(s, F_IA);
+            SV pA0 = ldsv(s, F_PA);
+            for (int c = 0; c < M::nchild[0]; ++c) {
+                si_add(IA0, ldsi(s, M::child[0][c] * GF + F_IA));
+                pA0 = pA0 + ldsv(s, M::child[0][c] * GF + F_PA);
+            }
+            if (!fix_base) {
+                rootf = ldl6(IA0);
+                a0 = ldl6_solve(rootf, -1.0f * pA0);
+            }
+        }
+        TG_SYNC();
+        TG_PROF(2)
+        // ---- pass 3: free accelerations (through the F_PA slots) and velocities
+        if (lead) stsv(s, F_PA, a0);
+        TG_SYNC();
+#pragma unroll 1
+        for (int t = 0; t < M::NSTEP; ++t) {
+            const int g = sched[t * LPE + sub];
+            if (g > 0) {
+                const int o = g * GF;
+                const GInfo G = ginfo<M>(gi, g);
+                const SV S = G.S();
+                const float qd = s(o + F_QD);
+                const SV cb = crm(ldsv(s, o + F_V), qd * S);
+                const SV ap = xmotion(ldx(s, g), ldsv(s, G.parent * GF + F_PA)) + cb;
+                const float qdd = (s(o + F_UU) - dot(ldsv(s, o + F_U), ap)) * s(o + F_DINV);
+                stsv(s, o + F_PA, ap + qdd * S);
+                s(o + F_QDS) = qd + h * qdd;
+            }
+            TG_SYNC();
+        }
+        SV v0s = v0 + h * a0;
+        v0s.v = v0s.v + h * cross(v0.w, v0.v);
+        if (fix_base) v0s = sv0();
+        TG_PROF(3)
+
+        // ---- contacts
+        if constexpr (M::NS > 0) {
+            // contact-group world poses and free velocities (one lane per contact group)
+            for (int c = sub; c < M::NCG; c += LPE) {
+                M3 Rc;
+                V3 pc;
+                world_pose(s, gi, GIW, M::cgroup[c], R, pos, Rc, pc);
+                stm3(s, PL::CGP + 12 * c, Rc);
+                stv3(s, PL::CGP + 12 * c + 9, pc);
+                SV v = v0s;
+                for (int i = 0; i < M::cpath_len[c]; ++i) {
+                    const int hg = cpath[c * M::MAXD + i];
+                    v = xmotion(ldx(s, hg), v) + s(hg * GF + F_QDS) * ginfo<M>(gi, hg).S();
+                }
+                stsv(s, PL::CGV + 6 * c, v);
+            }
+            TG_SYNC();
+            // contact rows (one lane per shape)
+            for (int sh = sub; sh < M::NS; sh += LPE) {
+                const int cgi = M::shape_cg[sh];
+                const int rb = row_base<M>(sh);
+                const M3 Rwg = ldm3(s, PL::CGP + 12 * cgi);
+                const V3 pwg = ldv3(s, PL::CGP + 12 * cgi + 9);
+                M3 Rsl;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) Rsl.a[k] = CP(CL::shape(sh) + k);
+                const M3 Rs = mul(Rwg, Rsl);
+                const V3 cl = v3(CP(CL::shape(sh) + 9), CP(CL::shape(sh) + 10), CP(CL::shape(sh) + 11));
+                const V3 cw = pwg + mul(Rwg, cl);
+                V3 pts[4];
+                const int nr = M::shape_nrows[sh];
+                const int kind = M::shape_kind[sh];
+                if (kind == TG_SHAPE_TORUS) {
+                    const V3 ax = v3(Rs.a[2], Rs.a[5], Rs.a[8]);
+                    V3 dd = v3(-ax.z * ax.x, -ax.z * ax.y, 1.f - ax.z * ax.z);
+                    float nd = sqrtf(dot(dd, dd));
+                    if (nd < 1e-6f) { dd = v3(1, 0, 0); nd = 1.f; }
+                    pts[0] = cw - (M::shape_params[sh][0] / nd) * dd - v3(0, 0, M::shape_params[sh][1]);
+                } else if (kind == TG_SHAPE_SPHERE) {
+                    pts[0] = cw - v3(0, 0, M::shape_params[sh][0]);
+                } else {
+                    const float hx = M::shape_params[sh][0], hy = M::shape_params[sh][1], hz = M::shape_params[sh][2];
+                    const float zx = Rs.a[6], zy = Rs.a[7], zz = Rs.a[8];
+                    const float ax_ = fabsf(zx), ay_ = fabsf(zy), az_ = fabsf(zz);
+                    const V3 ex = v3(Rs.a[0], Rs.a[3], Rs.a[6]), ey = v3(Rs.a[1], Rs.a[4], Rs.a[7]),
+                             ez = v3(Rs.a[2], Rs.a[5], Rs.a[8]);
+                    V3 fn, u1, u2;
+                    if (az_ >= ax_ && az_ >= ay_) { fn = (zz > 0 ? -hz : hz) * ez; u1 = hx * ex; u2 = hy * ey; }
+                    else if (ay_ >= ax_) { fn = (zy > 0 ? -hy : hy) * ey; u1 = hx * ex; u2 = hz * ez; }
+                    else { fn = (zx > 0 ? -hx : hx) * ex; u1 = hy * ey; u2 = hz * ez; }
+                    pts[0] = cw + fn - u1 - u2;
+                    pts[1] = cw + fn + u1 - u2;
+                    pts[2] = cw + fn - u1 + u2;
+                    pts[3] = cw + fn + u1 + u2;
+                }
+                V3 cen = v3(0, 0, 0);
+                float nact = 0.f;
+                float onk[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (k >= nr) break;
+                    const int ro = PL::ROW + (rb + k) * 8;
+                    const float phi = pts[k].z;
+                    const float on = phi <= a.margin ? 1.f : 0.f;
+                    onk[k] = on;
+                    stv3(s, ro, mulT(Rwg, pts[k] - pwg));
+                    stv3(s, ro + 3, v3(0, 0, 1));
+                    s(ro + 6) = phi > a.rest ? -(phi - a.rest) / h : fminf(a.baumgarte * (a.rest - phi) / h, a.max_depen);
+                    s(ro + 7) = on;
+                    cen = cen + on * pts[k];
+                    nact += on;
+                }
+                cen = (nact > 0.f ? 1.f / nact : 0.f) * cen;
+                float re = 0.f;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (k >= nr) break;
+                    const float dx = pts[k].x - cen.x, dy = pts[k].y - cen.y;
+                    re += onk[k] * sqrtf(dx * dx + dy * dy);
+                }
+                s(PL::SHP + 2 * sh) = 0.5f * (a.shape_mu[(size_t)e * M::NS + sh] + a.ground_mu);
+                s(PL::SHP + 2 * sh + 1) = nact > 0.f ? re / nact : 0.f;
+                V3 t1 = v3(1, 0, 0);
+                if (kind == TG_SHAPE_TORUS) {
+                    const V3 ax = v3(Rs.a[2], Rs.a[5], Rs.a[8]);
+                    const V3 x = cross(ax, v3(0, 0, 1));
+                    const float nx = sqrtf(dot(x, x));
+                    if (nx > 1e-6f) t1 = (1.f / nx) * x;
+                }
+                const V3 t2 = cross(v3(0, 0, 1), t1);
+                const V3 rl = mulT(Rwg, cen - pwg);
+                const float fon = nact > 0.f ? 1.f : 0.f;
+                for (int t = 0; t < 3; ++t) {
+                    const int ro = PL::ROW + (rb + nr + t) * 8;
+                    stv3(s, ro, rl);
+                    stv3(s, ro + 3, t == 0 ? t1 : (t == 1 ? t2 : v3(0, 0, 1)));
+                    s(ro + 6) = 0.f;
+                    s(ro + 7) = fon;
+                }
+            }
+            TG_SYNC();
+            // row helpers (row i on contact group cg(i))
+            auto row_is_ang = [&](int i) {
+                const int sh = row_shape<M>(i);
+                return i == row_base<M>(sh) + M::shape_nrows[sh] + 2;
+            };
+            auto rvel = [&](int i, const SV &vg) {
+                const int ro = PL::ROW + i * 8;
+                const M3 Rwg = ldm3(s, PL::CGP + 12 * M::shape_cg[row_shape<M>(i)]);
+                const V3 o = row_is_ang(i) ? mul(Rwg, vg.w) : mul(Rwg, vg.v + cross(vg.w, ldv3(s, ro)));
+                return dot(o, ldv3(s, ro + 3));
+            };
+            auto rforce = [&](int i, float lam) {
+                const int ro = PL::ROW + i * 8;
+                const V3 dl = mulT(ldm3(s, PL::CGP + 12 * M::shape_cg[row_shape<M>(i)]), ldv3(s, ro + 3));
+                return row_is_ang(i) ? SV{lam * dl, v3(0, 0, 0)} : SV{lam * cross(ldv3(s, ro), dl), lam * dl};
+            };
+            for (int i = sub; i < K; i += LPE) {
+                s(PL::VFREE + i) = rvel(i, ldsv(s, PL::CGV + 6 * M::shape_cg[row_shape<M>(i)]));
+                s(PL::LAM + i) = 0.f;
+            }
+            TG_PROF(4)
+            // Delassus columns, one per lane: unit row impulse on contact group k,
+            // up-walk along k's path (du in registers), root solve, down-walk
+            // along every contact group's path
+#pragma unroll 1
+            for (int j = sub; j < K; j += LPE) {
+                const int ck = M::shape_cg[row_shape<M>(j)];
+                const int lk = M::cpath_len[ck];
+                const int *pk = cpath + ck * M::MAXD;
+                SV p = -1.0f * rforce(j, 1.0f);
+                float du[M::MAXD];
+#pragma unroll
+                for (int i = M::MAXD - 1; i >= 0; --i) {
+                    du[i] = 0.f;
+                    if (i < lk) {
+                        const int g = pk[i];
+                        const float u = -dot(ginfo<M>(gi, g).S(), p);
+                        du[i] = u;
+                        const SV pa = p + (u * s(g * GF + F_DINV)) * ldsv(s, g * GF + F_U);
+                        p = xTforce(ldx(s, g), pa);
+                    }
+                }
+                const SV aj = fix_base ? sv0() : ldl6_solve(rootf, -1.0f * p);
+                SV dvc[M::NCG];
+#pragma unroll
+                for (int c = 0; c < M::NCG; ++c) {
+                    SV av = aj;
+#pragma unroll
+                    for (int i = 0; i < M::MAXD; ++i) {
+                        if (i < M::cpath_len[c]) {
+                            const int hg = M::cpath[c][i];
+                            const SV ap = xmotion(ldx(s, hg), av);
+                            const float dui = (i < lk && pk[i] == hg) ? du[i] : 0.0f;
+                            const float x = (dui - dot(ldsv(s, hg * GF + F_U), ap)) * s(hg * GF + F_DINV);
+                            av = ap + x * ginfo<M>(gi, hg).S();
+                        }
+                    }
+                    dvc[c] = av;
+                }
+#pragma unroll
+                for (int i = 0; i < K; ++i) s(PL::W + i * K + j) = rvel(i, dvc[M::shape_cg[row_shape<M>(i)]]);
+            }
+            TG_SYNC();
+            TG_PROF(5)
+            // projected Gauss-Seidel with patch friction (lead lane)
+            if (lead) {
+#pragma unroll 1
+                for (int it = 0; it < a.iters; ++it) {
+                    for (int sh = 0; sh < M::NS; ++sh) {
+                        const int rb = row_base<M>(sh), nr = M::shape_nrows[sh];
+                        float Nsum = 0.f;
+                        for (int k = 0; k < nr; ++k) {
+                            const int i = rb + k;
+                            float vi = s(PL::VFREE + i);
+#pragma unroll
+                            for (int j = 0; j < K; ++j) vi += s(PL::W + i * K + j) * s(PL::LAM + j);
+                            const float l = s(PL::LAM + i) + (s(PL::ROW + i * 8 + 6) - vi) / s(PL::W + i * K + i);
+                            const float li = s(PL::ROW + i * 8 + 7) * fmaxf(l, 0.f);
+                            s(PL::LAM + i) = li;
+                            Nsum += li;
+                        }
+                        const int f = rb + nr;
+                        const float mu = s(PL::SHP + 2 * sh), reff = s(PL::SHP + 2 * sh + 1);
+                        for (int t = 0; t < 3; ++t) {
+                            const int i = f + t;
+                            float vi = s(PL::VFREE + i);
+#pragma unroll
+                            for (int j = 0; j < K; ++j) vi += s(PL::W + i * K + j) * s(PL::LAM + j);
+                            s(PL::LAM + i) = s(PL::LAM + i) - vi / s(PL::W + i * K + i);
+                            if (t == 1) {
+                                const float l0 = s(PL::LAM + f), l1 = s(PL::LAM + f + 1);
+                                const float lt = sqrtf(l0 * l0 + l1 * l1), lim = mu * Nsum;
+                                const float sc = lt > lim ? (lt > 0.f ? lim / lt : 0.f) : 1.f;
+                                s(PL::LAM + f) = l0 * sc;
+                                s(PL::LAM + f + 1) = l1 * sc;
+                            }
+                        }
+                        const float lim3 = mu * Nsum * reff;
+                        s(PL::LAM + f + 2) = fminf(fmaxf(s(PL::LAM + f + 2), -lim3), lim3);
+                    }
+                }
+                // impulses into the contact groups' F_PA slots (p = -f convention)
+                for (int c = 0; c < M::NCG; ++c) stsv(s, M::cgroup[c] * GF + F_PA, sv0());
+                for (int i = 0; i < K; ++i) {
+                    const int g = M::shape_group[row_shape<M>(i)];
+                    stsv(s, g * GF + F_PA, ldsv(s, g * GF + F_PA) + (-1.0f) * rforce(i, s(PL::LAM + i)));
+                }
+            } else {
+                // clear every other group's slot
+                for (int g = sub - 1; g < M::NG; g += LPE - 1) {
+                    bool is_cg = false;
+                    for (int c = 0; c < M::NCG; ++c) is_cg |= (M::cgroup[c] == g);
+                    if (g >= 0 && !is_cg) stsv(s, g * GF + F_PA, sv0());
+                }
+            }
+            TG_SYNC();
+            TG_PROF(6)
+            // impulse application: bottom-up gather, root solve, top-down
+#pragma unroll 1
+            for (int t = M::NSTEP - 1; t >= 0; --t) {
+                const int g = sched[t * LPE + sub];
+                if (g > 0) {
+                    const int o = g * GF;
+                    SV p = ldsv(s, o + F_PA);
+                    const int nch = gi[g * GIW + GI_NCH];
+                    for (int c = 0; c < nch; ++c) p = p + ldsv(s, gi[g * GIW + GI_CH + c] * GF + F_PA);
+                    const float u = -dot(ginfo<M>(gi, g).S(), p);
+                    s(o + F_UU) = u;
+                    const SV pa = p + (u * s(o + F_DINV)) * ldsv(s, o + F_U);
+                    stsv(s, o + F_PA, xTforce(ldx(s, g), pa));
+                }
+                TG_SYNC();
+            }
+            SV da0 = sv0();
+            {
+                SV p0 = ldsv(s, F_PA);
+                for (int c = 0; c < M::nchild[0]; ++c) p0 = p0 + ldsv(s, M::child[0][c] * GF + F_PA);
+                if (!fix_base) da0 = ldl6_solve(rootf, -1.0f * p0);
+            }
+            TG_SYNC();
+            if (lead) stsv(s, F_PA, da0);
+            TG_SYNC();
+#pragma unroll 1
+            for (int t = 0; t < M::NSTEP; ++t) {
+                const int g = sched[t * LPE + sub];
+                if (g > 0) {
+                    const int o = g * GF;
+                    const GInfo G = ginfo<M>(gi, g);
+                    const SV ap = xmotion(ldx(s, g), ldsv(s, G.parent * GF + F_PA));
+                    const float x = (s(o + F_UU) - dot(ldsv(s, o + F_U), ap)) * s(o + F_DINV);
+                    stsv(s, o + F_PA, ap + x * G.S());
+                    s(o + F_QDS) += x;
+                }
+                TG_SYNC();
+            }
+            if (!fix_base) v0s = v0s + da0;
+            TG_PROF(7)
+        }
+        // ---- velocity limits + integration
+        for (int g = 1 + sub; g < M::NG; g += LPE) {
+            const int o = g * GF;
+            const float vl = PR(TG_PROP_VELOCITY, gi[g * GIW + GI_DOF]);
+            float x = s(o + F_QDS);
+            if (vl > 0.f) x = fminf(fmaxf(x, -vl), vl);
+            s(o + F_QD) = x;
+            s(o + F_Q) += h * x;
+        }
+        if (!fix_base) {
+            v0 = v0s;
+            pos = pos + h * mul(R, v0.v);
+            const float wn = sqrtf(dot(v0.w, v0.w));
+            const float an = wn * h;
+            float dx = 0.f, dy = 0.f, dz = 0.f, dw = 1.f;
+            if (an > 1e-12f) {
+                float sa, ca;
+                __sincosf(0.5f * an, &sa, &ca);
+                const float kk = sa / wn;
+                dx = v0.w.x * kk; dy = v0.w.y * kk; dz = v0.w.z * kk; dw = ca;
+            }
+            const float nx = qw * dx + qx * dw + qy * dz - qz * dy;
+            const float ny = qw * dy - qx * dz + qy * dw + qz * dx;
+            const float nz = qw * dz + qx * dy - qy * dx + qz * dw;
+            const float nw = qw * dw - qx * dx - qy * dy - qz * dz;
+            const float in = rsqrtf(nx * nx + ny * ny + nz * nz + nw * nw);
+            qx = nx * in; qy = ny * in; qz = nz * in; qw = nw * in;
+            R = quat_to_m3(qx, qy, qz, qw);
+            const M3 Rd = quat_to_m3(dx, dy, dz, dw);
+            v0.w = mulT(Rd, v0.w);
+            v0.v = mulT(Rd, v0.v);
+        }
+        TG_SYNC();
+        TG_PROF(8)
+    }
+    if (owner) {
+        if (lead) {
+            const V3 wwo = mul(R, v0.w);
+            const V3 vco = mul(R, v0.v) + cross(wwo, mul(R, c0));
+            root[0] = pos.x; root[1] = pos.y; root[2] = pos.z;
+            root[3] = qx; root[4] = qy; root[5] = qz; root[6] = qw;
+            root[7] = vco.x; root[8] = vco.y; root[9] = vco.z;
+            root[10] = wwo.x; root[11] = wwo.y; root[12] = wwo.z;
+        }
+        for (int g = 1 + sub; g < M::NG; g += LPE) {
+            const int d = gi[g * GIW + GI_DOF];
+            dofs[2 * d] = s(g * GF + F_Q);
+            dofs[2 * d + 1] = s(g * GF + F_QD);
+        }
+        for (int d = sub; d < M::ND; d += LPE) {
+            if (M::dof_locked[d]) {
+                dofs[2 * d] = 0.5f * (PR(TG_PROP_LOWER, d) + PR(TG_PROP_UPPER, d));
+                dofs[2 * d + 1] = 0.f;
+            }
+        }
+    }
+    TG_PROF(9)
+}
+
+#undef TG_SYNC
+
+}  // namespace tg
