@@ -136,10 +136,20 @@ __device__ __forceinline__ void world_pose(const LE &s, const int *gi, int giw, 
     pg = p0 + mul(R0, t);
 }
 
-#define TG_SYNC() __syncthreads()
+// The LPE lanes of an env are consecutive lanes of one wavefront, whose LDS
+// operations execute in program order: an env-level "barrier" only has to stop
+// the compiler from moving LDS accesses across it (no s_barrier, and no
+// s_waitcnt on the prefetched global loads still in flight).
+#define TG_SYNC()                                          \
+    do {                                                   \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); \
+        __builtin_amdgcn_wave_barrier();                   \
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); \
+    } while (0)
 
 template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a) {
     constexpr int LPE = M::LPE;
+    static_assert(64 % LPE == 0, "an env's lanes must share a wavefront");
     using CL = CompLayout<M>;
     using PL = ParLayout<M>;
     constexpr int K = PL::K;
@@ -181,7 +191,7 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
 
     float *root = a.root + (size_t)e * 13;
     float *dofs = a.dof + (size_t)e * D * 2;
-    TG_SYNC();
+    __syncthreads();   // group tables (shared by both wavefronts)
     for (int g = 1 + sub; g < M::NG; g += LPE) {
         const int d = gi[g * GIW + GI_DOF];
         s(g * GF + F_Q) = dofs[2 * d];
@@ -201,13 +211,14 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
     const V3 grav = v3(a.gx, a.gy, a.gz);
 
     // rigid inertia + bias force of group g (pass 1 body), v and gl already known
-    auto body_bias = [&](int g, const SV &vg, V3 gl) {
+    // cin: the group's composite inertia (m, c, Ic) from the per-env cache
+    auto body_bias = [&](int g, const SV &vg, V3 gl, const float *cin) {
         const int o = g * GF;
-        const float m = CP(CL::inertia(g));
-        const V3 cg = v3(CP(CL::inertia(g) + 1), CP(CL::inertia(g) + 2), CP(CL::inertia(g) + 3));
+        const float m = cin[0];
+        const V3 cg = v3(cin[1], cin[2], cin[3]);
         float Ic[6];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) Ic[k] = CP(CL::inertia(g) + 4 + k);
+        for (int k = 0; k < 6; ++k) Ic[k] = cin[4 + k];
         const SI I = rb_inertia(m, cg, Ic);
         stsi(s, o + F_IA, I);
         const SV b = crf(vg, mul(I, vg));
@@ -225,6 +236,29 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
         }
         stsv(s, o + F_PA, SV{b.w - n, b.v - F});
     };
+    // per-group per-env inputs, prefetched one schedule step ahead
+    auto load_kin = [&](int g, float *x) {   // joint placement (12) + inertia (10)
+#pragma unroll
+        for (int k = 0; k < 12; ++k) x[k] = CP(CL::xtree(g) + k);
+#pragma unroll
+        for (int k = 0; k < 10; ++k) x[12 + k] = CP(CL::inertia(g) + k);
+    };
+    auto load_drv = [&](int g, float *x) {   // drive / limit inputs of the group's dof
+        const int d = gi[g * GIW + GI_DOF];
+        x[0] = PR(TG_PROP_ARMATURE, d);
+        x[1] = PR(TG_PROP_DRIVE_MODE, d);
+        x[2] = PR(TG_PROP_STIFFNESS, d);
+        x[3] = PR(TG_PROP_DAMPING, d);
+        x[4] = PR(TG_PROP_EFFORT, d);
+        x[5] = PR(TG_PROP_LOWER, d);
+        x[6] = PR(TG_PROP_UPPER, d);
+        x[7] = a.pos_tgt[(size_t)e * D + d];
+        x[8] = a.vel_tgt[(size_t)e * D + d];
+        x[9] = a.act ? a.act[(size_t)e * D + d] : 0.f;
+    };
+    float rin[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) rin[k] = CP(CL::inertia(0) + k);
     TG_SYNC();
     TG_PROF(0)
 
@@ -234,19 +268,27 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
             const V3 gl = mulT(R, grav);
             stsv(s, F_V, v0);
             stv3(s, F_GL, gl);
-            body_bias(0, v0, gl);
+            body_bias(0, v0, gl, rin);
         }
         TG_SYNC();
+        float nk[22];
+        int gn = sched[sub];
+        if (gn > 0) load_kin(gn, nk);
 #pragma unroll 1
         for (int t = 0; t < M::NSTEP; ++t) {
-            const int g = sched[t * LPE + sub];
+            const int g = gn;
+            float ck[22];
+#pragma unroll
+            for (int k = 0; k < 22; ++k) ck[k] = nk[k];
+            gn = t + 1 < M::NSTEP ? sched[(t + 1) * LPE + sub] : -1;
+            if (gn > 0) load_kin(gn, nk);
             if (g > 0) {
                 const int o = g * GF;
                 const GInfo G = ginfo<M>(gi, g);
                 M3 Rpc;
 #pragma unroll
-                for (int k = 0; k < 9; ++k) Rpc.a[k] = CP(CL::xtree(g) + k);
-                V3 tr = v3(CP(CL::xtree(g) + 9), CP(CL::xtree(g) + 10), CP(CL::xtree(g) + 11));
+                for (int k = 0; k < 9; ++k) Rpc.a[k] = ck[k];
+                V3 tr = v3(ck[9], ck[10], ck[11]);
                 const float qg = s(o + F_Q);
                 if (G.jt == TG_JOINT_REVOLUTE) Rpc = mul(Rpc, rot_axis(G.ax.x, G.ax.y, G.ax.z, qg));
                 else tr = tr + qg * mul(Rpc, G.ax);
@@ -257,19 +299,26 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
                 const V3 gl = mul(X.E, ldv3(s, G.parent * GF + F_GL));
                 stsv(s, o + F_V, vg);
                 stv3(s, o + F_GL, gl);
-                body_bias(g, vg, gl);
+                body_bias(g, vg, gl, ck + 12);
             }
             TG_SYNC();
         }
         TG_PROF(1)
         // ---- pass 2: schedule backward, children contributions gathered
+        float nd[10];
+        gn = sched[(M::NSTEP - 1) * LPE + sub];
+        if (gn > 0) load_drv(gn, nd);
 #pragma unroll 1
         for (int t = M::NSTEP - 1; t >= 0; --t) {
-            const int g = sched[t * LPE + sub];
+            const int g = gn;
+            float cd[10];
+#pragma unroll
+            for (int k = 0; k < 10; ++k) cd[k] = nd[k];
+            gn = t > 0 ? sched[(t - 1) * LPE + sub] : -1;
+            if (gn > 0) load_drv(gn, nd);
             if (g > 0) {
                 const int o = g * GF;
                 const GInfo G = ginfo<M>(gi, g);
-                const int d = G.dof;
                 const SV S = G.S();
                 SI IA = ldsi(s, o + F_IA);
                 SV pA = ldsv(s, o + F_PA);
@@ -281,19 +330,19 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
                 }
                 const SV U = mul(IA, S);
                 const float q = s(o + F_Q), qd = s(o + F_QD);
-                const float D0 = dot(S, U) + PR(TG_PROP_ARMATURE, d);
+                const float D0 = dot(S, U) + cd[0];
                 float Dimp = 0.f, tau = 0.f;
-                const int mode = (int)rintf(PR(TG_PROP_DRIVE_MODE, d));
-                const float kp = PR(TG_PROP_STIFFNESS, d), kd = PR(TG_PROP_DAMPING, d);
-                const float eff = PR(TG_PROP_EFFORT, d);
+                const int mode = (int)rintf(cd[1]);
+                const float kp = cd[2], kd = cd[3];
+                const float eff = cd[4];
                 if (mode == TG_DOF_MODE_POS || mode == TG_DOF_MODE_VEL) {
-                    const float te = kp * (a.pos_tgt[(size_t)e * D + d] - q - h * qd) + kd * (a.vel_tgt[(size_t)e * D + d] - qd);
+                    const float te = kp * (cd[7] - q - h * qd) + kd * (cd[8] - qd);
                     if (fabsf(te) <= eff) { tau += te; Dimp += h * kd + h * h * kp; }
                     else tau += te > 0.f ? eff : -eff;
                 } else if (mode == TG_DOF_MODE_EFFORT && a.act) {
-                    tau += fminf(fmaxf(a.act[(size_t)e * D + d], -eff), eff);
+                    tau += fminf(fmaxf(cd[9], -eff), eff);
                 }
-                const float lo = PR(TG_PROP_LOWER, d), hi = PR(TG_PROP_UPPER, d);
+                const float lo = cd[5], hi = cd[6];
                 const float qp = q + h * qd;
                 const float kl = a.lim_k * D0 / (h * h), cl = a.lim_c * D0 / h;
                 if (qp < lo && lo > -1e30f) { tau += kl * (lo - qp) - cl * qd; Dimp += h * cl + h * h * kl; }
