@@ -9,9 +9,13 @@ ARGS="${BENCH_ARGS:---steps 200 --warmup 30} --no-cpu-baseline"
 stop_if_fatal() { if [ "$1" -ge 124 ] || [ "$1" -eq 134 ] || [ "$1" -eq 139 ]; then echo "FATAL: $2 exited $1"; exit "$1"; fi; }
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof/trace -o run -- python3 bench.py $ARGS > gpurun_out/prof/trace.log 2>&1
 rc=$?; echo "trace rc=$rc"; tail -3 gpurun_out/prof/trace.log; stop_if_fatal $rc trace
-for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 600 rocprofv3 --pmc $c -T --output-format csv -d gpurun_out/prof/pmc_$c -o run -- python3 bench.py $ARGS > gpurun_out/prof/pmc_$c.log 2>&1
-  rc=$?; echo "pmc $c rc=$rc"; tail -2 gpurun_out/prof/pmc_$c.log; stop_if_fatal $rc pmc_$c
+# counter passes: ';'-separated sets, counters within a set share one pass
+PMC_SETS="${PMC_SETS:-FETCH_SIZE;WRITE_SIZE}"
+IFS=';' read -ra SETS <<< "$PMC_SETS"
+for set in "${SETS[@]}"; do
+  tag=$(echo $set | awk '{print $1}')
+  timeout -k 10 600 rocprofv3 --pmc $set -T --output-format csv -d gpurun_out/prof/pmc_$tag -o run -- python3 bench.py $ARGS > gpurun_out/prof/pmc_$tag.log 2>&1
+  rc=$?; echo "pmc $set rc=$rc"; tail -2 gpurun_out/prof/pmc_$tag.log; stop_if_fatal $rc pmc_$tag
 done
 find gpurun_out/prof -name "*.csv" | head -20
 exit 0

@@ -254,17 +254,27 @@ __device__ void philox_reset_draws(int e, uint32_t c_lo, uint32_t c_hi, uint32_t
     r[10] = u01(x4.x);
 }
 
+// one env per lane with a long dependent chain per lane: spread the envs over
+// as many CUs as possible (16-lane workgroups up to 1024 workgroups)
+static int env_threads(int n) {
+    int t = 16;
+    while (t < 256 && (n + t - 1) / t > 1024) t *= 2;
+    return t;
+}
+
 int launch_gogoro_reset_idx(const tg_gogoro_params &p, const tg_gogoro_buffers &b, const int32_t *ids, int n,
                             const float *reset_draws, uint64_t counter, hipStream_t stream) {
     if (n <= 0) return 0;
-    hipLaunchKernelGGL(reset_idx_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, p, b, ids, n, reset_draws,
+    const int t = env_threads(n);
+    hipLaunchKernelGGL(reset_idx_kernel, dim3((n + t - 1) / t), dim3(t), 0, stream, p, b, ids, n, reset_draws,
                        (uint32_t)counter, (uint32_t)(counter >> 32));
     return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
 }
 
 int launch_gogoro_pre(const tg_gogoro_params &p, const tg_gogoro_buffers &b, const float *actions,
                       const float *pre_draws, uint64_t counter, hipStream_t stream) {
-    dim3 grid((p.num_envs + 255) / 256), block(256);
+    const int t = env_threads(p.num_envs);
+    dim3 grid((p.num_envs + t - 1) / t), block(t);
     hipLaunchKernelGGL(pre_kernel, grid, block, 0, stream, p, b, actions, pre_draws, (uint32_t)counter,
                        (uint32_t)(counter >> 32));
     return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
@@ -273,7 +283,8 @@ int launch_gogoro_pre(const tg_gogoro_params &p, const tg_gogoro_buffers &b, con
 int launch_gogoro_post(const tg_gogoro_params &p, const tg_gogoro_buffers &b, const float *reset_draws,
                        const float *obs_draws, const float *speed_draws, const float *yaw_draws, uint64_t counter,
                        hipStream_t stream) {
-    dim3 grid((p.num_envs + 255) / 256), block(256);
+    const int t = env_threads(p.num_envs);
+    dim3 grid((p.num_envs + t - 1) / t), block(t);
     hipLaunchKernelGGL(post_kernel, grid, block, 0, stream, p, b, reset_draws, obs_draws, speed_draws, yaw_draws,
                        (uint32_t)counter, (uint32_t)(counter >> 32));
     return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;

@@ -1,6 +1,6 @@
-// step_par.h -- tree-parallel, LDS-resident articulation step for large joint
-// trees (included by articulation.hip after the shared helpers; same algorithm
-// and operation order per group as step_kernel<M> and oracle/physics_ref.c).
+// step_par.h -- tree-parallel, LDS-resident articulation step (included by
+// articulation.hip after the shared helpers; the algorithm of
+// oracle/physics_ref.c, operation for operation per group).
 //
 // Layout: EPB envs per workgroup, LPE lanes per env (LPE consecutive lanes of
 // one wavefront).  Each env's articulated state (per group: X, v, I^A, p^A, U,
@@ -568,6 +568,9 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
             }
             TG_SYNC();
             TG_PROF(5)
+            // impulse accumulators (F_PA slots) cleared by all lanes
+            for (int g = sub; g < M::NG; g += LPE) stsv(s, g * GF + F_PA, sv0());
+            TG_SYNC();
             // projected Gauss-Seidel with patch friction (lead lane)
             if (lead) {
 #pragma unroll 1
@@ -606,17 +609,9 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
                     }
                 }
                 // impulses into the contact groups' F_PA slots (p = -f convention)
-                for (int c = 0; c < M::NCG; ++c) stsv(s, M::cgroup[c] * GF + F_PA, sv0());
                 for (int i = 0; i < K; ++i) {
                     const int g = M::shape_group[row_shape<M>(i)];
                     stsv(s, g * GF + F_PA, ldsv(s, g * GF + F_PA) + (-1.0f) * rforce(i, s(PL::LAM + i)));
-                }
-            } else {
-                // clear every other group's slot
-                for (int g = sub - 1; g < M::NG; g += LPE - 1) {
-                    bool is_cg = false;
-                    for (int c = 0; c < M::NCG; ++c) is_cg |= (M::cgroup[c] == g);
-                    if (g >= 0 && !is_cg) stsv(s, g * GF + F_PA, sv0());
                 }
             }
             TG_SYNC();

@@ -1,5 +1,6 @@
-// walk_task.hip -- fused ThormangWalk task kernels (include/tg_walk.h), one env
-// per lane.  The reference has no walking task; the
+// walk_task.hip -- fused ThormangWalk task kernels (include/tg_walk.h): the
+// action kernel runs one lane per (env, dof); post-physics and reset run one
+// wavefront per env (lane = dof).  The reference has no walking task; the
 // semantics are this build's design and are checked against oracle/walk_task.c.
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -23,76 +24,65 @@ __global__ __launch_bounds__(256) void walk_pre_kernel(tg_walk_params p, tg_walk
     b.pos_target[t] = p.default_pos[d] + p.action_scale * a;
 }
 
-__device__ void walk_reset_draws(const tg_walk_params &p, int e, uint32_t c_lo, uint32_t c_hi, float *r) {
+// reset draw k of env e (replay array or in-kernel Philox, 4 draws per counter)
+__device__ __forceinline__ float walk_draw(const tg_walk_params &p, const float *reset_draws, int e, int k,
+                                           uint32_t c_lo, uint32_t c_hi) {
     const int n = 4 + 2 * p.num_dof;
-    for (int k = 0; k < n; k += 4) {
-        U4 x = philox(U4{(uint32_t)e, c_lo, c_hi, 0x57524530u + (uint32_t)(k >> 2)}, (uint32_t)p.seed,
-                      (uint32_t)(p.seed >> 32));
-        r[k] = u01(x.x);
-        if (k + 1 < n) r[k + 1] = u01(x.y);
-        if (k + 2 < n) r[k + 2] = u01(x.z);
-        if (k + 3 < n) r[k + 3] = u01(x.w);
-    }
+    if (reset_draws) return reset_draws[(size_t)n * e + k];
+    const U4 x = philox(U4{(uint32_t)e, c_lo, c_hi, 0x57524530u + (uint32_t)(k >> 2)}, (uint32_t)p.seed,
+                        (uint32_t)(p.seed >> 32));
+    const uint32_t c = (k & 3) == 0 ? x.x : (k & 3) == 1 ? x.y : (k & 3) == 2 ? x.z : x.w;
+    return u01(c);
 }
 
-__device__ void walk_reset_env(const tg_walk_params &p, const tg_walk_buffers &b, int e, const float *r) {
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+    return v;
+}
+
+// One wavefront per env: lane d handles dof d (reset, dof observations, the
+// per-dof reward sums); lane 0 the root, commands, reward and termination.
+__device__ void walk_env(const tg_walk_params &p, const tg_walk_buffers &b, int e, bool reset, int64_t prog,
+                         const float *reset_draws, uint32_t c_lo, uint32_t c_hi) {
+    const int lane = threadIdx.x;
     const int D = p.num_dof;
-    b.commands[3 * (size_t)e + 0] = p.cmd_vx[0] + r[0] * (p.cmd_vx[1] - p.cmd_vx[0]);
-    b.commands[3 * (size_t)e + 1] = p.cmd_vy[0] + r[1] * (p.cmd_vy[1] - p.cmd_vy[0]);
-    b.commands[3 * (size_t)e + 2] = p.cmd_wz[0] + r[2] * (p.cmd_wz[1] - p.cmd_wz[0]);
-    const float yaw = (r[3] * 2.0f - 1.0f) * W_PI;
     float *root = b.root + 13 * (size_t)e;
-    const float *tpl = b.root_reset + 13 * (size_t)e;
-    root[0] = tpl[0];
-    root[1] = tpl[1];
-    root[2] = p.spawn_height;
-    root[3] = 0.0f;
-    root[4] = 0.0f;
-    root[5] = sinf(0.5f * yaw);
-    root[6] = cosf(0.5f * yaw);
-#pragma unroll
-    for (int k = 7; k < 13; ++k) root[k] = 0.0f;
-    for (int d = 0; d < D; ++d) {
-        const size_t i = (size_t)e * D + d;
-        b.dof_state[2 * i] = p.default_pos[d] + (r[4 + d] * 2.0f - 1.0f) * p.joint_noise;
-        b.dof_state[2 * i + 1] = 0.1f * (r[4 + D + d] * 2.0f - 1.0f);
-        b.last_actions[i] = 0.0f;
-        b.actions[i] = 0.0f;
-    }
-    b.progress_buf[e] = 0;
-    b.reset_buf[e] = 0;
-}
-
-__device__ void walk_observe(const tg_walk_params &p, const tg_walk_buffers &b, int e, int64_t prog) {
-    const int D = p.num_dof;
-    const float *r = b.root + 13 * (size_t)e;
-    const float x = r[3], y = r[4], z = r[5], w = r[6];
-    const float R[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w),
-                        2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w),
-                        2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)};
-    float vb[3], wb[3], gb[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        vb[i] = R[i] * r[7] + R[3 + i] * r[8] + R[6 + i] * r[9];
-        wb[i] = R[i] * r[10] + R[3 + i] * r[11] + R[6 + i] * r[12];
-        gb[i] = -R[6 + i];
-    }
     float *o = b.obs_buf + (size_t)p.num_obs * e;
-    const float *cmd = b.commands + 3 * (size_t)e;
     const float co = p.clip_obs;
-    o[0] = clampw(r[2], -co, co);
+    if (reset) {
+        for (int d = lane; d < D; d += 64) {
+            const size_t i = (size_t)e * D + d;
+            b.dof_state[2 * i] = p.default_pos[d] + (walk_draw(p, reset_draws, e, 4 + d, c_lo, c_hi) * 2.0f - 1.0f) * p.joint_noise;
+            b.dof_state[2 * i + 1] = 0.1f * (walk_draw(p, reset_draws, e, 4 + D + d, c_lo, c_hi) * 2.0f - 1.0f);
+            b.last_actions[i] = 0.0f;
+            b.actions[i] = 0.0f;
+        }
+        if (lane == 0) {
+            float r[4];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        o[1 + i] = clampw(vb[i] * p.lin_vel_scale, -co, co);
-        o[4 + i] = clampw(wb[i] * p.ang_vel_scale, -co, co);
-        o[7 + i] = clampw(gb[i], -co, co);
+            for (int k = 0; k < 4; ++k) r[k] = walk_draw(p, reset_draws, e, k, c_lo, c_hi);
+            b.commands[3 * (size_t)e + 0] = p.cmd_vx[0] + r[0] * (p.cmd_vx[1] - p.cmd_vx[0]);
+            b.commands[3 * (size_t)e + 1] = p.cmd_vy[0] + r[1] * (p.cmd_vy[1] - p.cmd_vy[0]);
+            b.commands[3 * (size_t)e + 2] = p.cmd_wz[0] + r[2] * (p.cmd_wz[1] - p.cmd_wz[0]);
+            const float yaw = (r[3] * 2.0f - 1.0f) * W_PI;
+            const float *tpl = b.root_reset + 13 * (size_t)e;
+            root[0] = tpl[0];
+            root[1] = tpl[1];
+            root[2] = p.spawn_height;
+            root[3] = 0.0f;
+            root[4] = 0.0f;
+            root[5] = sinf(0.5f * yaw);
+            root[6] = cosf(0.5f * yaw);
+#pragma unroll
+            for (int k = 7; k < 13; ++k) root[k] = 0.0f;
+            b.progress_buf[e] = 0;
+        }
     }
-    o[10] = clampw(cmd[0] * p.lin_vel_scale, -co, co);
-    o[11] = clampw(cmd[1] * p.lin_vel_scale, -co, co);
-    o[12] = clampw(cmd[2] * p.ang_vel_scale, -co, co);
+    // dof observations and the per-dof reward terms
     float rate = 0.0f, vel2 = 0.0f, tq = 0.0f;
     const float *ds = b.dof_state + 2 * (size_t)e * D;
-    for (int d = 0; d < D; ++d) {
+    for (int d = lane; d < D; d += 64) {
         const size_t i = (size_t)e * D + d;
         const float q = ds[2 * d], qd = ds[2 * d + 1];
         const float a = b.actions[i], la = b.last_actions[i];
@@ -105,71 +95,76 @@ __device__ void walk_observe(const tg_walk_params &p, const tg_walk_buffers &b, 
         tq += t * t;
         b.last_actions[i] = a;
     }
+    rate = wave_sum(rate);
+    vel2 = wave_sum(vel2);
+    tq = wave_sum(tq);
+    if (lane != 0) return;
+    const float x = root[3], y = root[4], z = root[5], w = root[6];
+    const float R[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w),
+                        2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w),
+                        2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)};
+    float vb[3], wb[3], gb[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        vb[i] = R[i] * root[7] + R[3 + i] * root[8] + R[6 + i] * root[9];
+        wb[i] = R[i] * root[10] + R[3 + i] * root[11] + R[6 + i] * root[12];
+        gb[i] = -R[6 + i];
+    }
+    const float *cmd = b.commands + 3 * (size_t)e;
+    o[0] = clampw(root[2], -co, co);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        o[1 + i] = clampw(vb[i] * p.lin_vel_scale, -co, co);
+        o[4 + i] = clampw(wb[i] * p.ang_vel_scale, -co, co);
+        o[7 + i] = clampw(gb[i], -co, co);
+    }
+    o[10] = clampw(cmd[0] * p.lin_vel_scale, -co, co);
+    o[11] = clampw(cmd[1] * p.lin_vel_scale, -co, co);
+    o[12] = clampw(cmd[2] * p.ang_vel_scale, -co, co);
     const float lin_err = (cmd[0] - vb[0]) * (cmd[0] - vb[0]) + (cmd[1] - vb[1]) * (cmd[1] - vb[1]);
     const float ang_err = (cmd[2] - wb[2]) * (cmd[2] - wb[2]);
-    const float dz = r[2] - p.target_height;
+    const float dz = root[2] - p.target_height;
     float rew = p.rew_lin_vel_xy * expf(-lin_err / 0.25f) + p.rew_ang_vel_z * expf(-ang_err / 0.25f) +
                 p.rew_upright * (-gb[2]) + p.rew_alive + p.rew_height * expf(-dz * dz / 0.01f) +
                 p.rew_action_rate * rate + p.rew_dof_vel * vel2 + p.rew_torque * tq;
-    const bool fall = (r[2] < p.termination_height) || (-gb[2] < p.termination_up);
+    const bool fall = (root[2] < p.termination_height) || (-gb[2] < p.termination_up);
     if (fall) rew += p.rew_termination;
-    const bool reset = fall || prog >= p.max_episode_length - 1;
+    const bool rs = fall || prog >= p.max_episode_length - 1;
     b.rew_buf[e] = rew;
-    b.reset_buf[e] = reset ? 1 : 0;
-    b.timeout_buf[e] = (prog >= p.max_episode_length - 1) && reset;
+    b.reset_buf[e] = rs ? 1 : 0;
+    b.timeout_buf[e] = (prog >= p.max_episode_length - 1) && rs;
 }
 
 __global__ __launch_bounds__(64) void walk_post_kernel(tg_walk_params p, tg_walk_buffers b, const float *reset_draws,
                                                        const float *push_draws, uint32_t c_lo, uint32_t c_hi) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= p.num_envs) return;
-    const int D = p.num_dof;
+    const int e = blockIdx.x;
     int64_t prog = b.progress_buf[e] + 1;
-    b.progress_buf[e] = prog;
-    if (b.reset_buf[e] != 0) {
-        float r[4 + 2 * TG_WALK_MAX_DOF];
-        if (reset_draws) {
-            for (int k = 0; k < 4 + 2 * D; ++k) r[k] = reset_draws[(size_t)(4 + 2 * D) * e + k];
-        } else {
-            walk_reset_draws(p, e, c_lo, c_hi, r);
-        }
-        walk_reset_env(p, b, e, r);
-        prog = 0;
+    const bool reset = b.reset_buf[e] != 0;
+    if (threadIdx.x == 0) b.progress_buf[e] = prog;
+    if (reset) prog = 0;
+    walk_env(p, b, e, reset, prog, reset_draws, c_lo, c_hi);
+    if (threadIdx.x != 0 || !b.body_force) return;
+    float *f = b.body_force + (size_t)6 * p.num_groups * e;
+    const bool push = p.push_force > 0.0f && p.push_interval > 0 && prog > 0 && (prog % p.push_interval) == 0;
+    float u[3];
+    if (push_draws) {
+        u[0] = push_draws[3 * (size_t)e]; u[1] = push_draws[3 * (size_t)e + 1]; u[2] = push_draws[3 * (size_t)e + 2];
+    } else {
+        U4 x = philox(U4{(uint32_t)e, c_lo, c_hi, 0x50555348u}, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+        u[0] = u01(x.x); u[1] = u01(x.y); u[2] = u01(x.z);
     }
-    walk_observe(p, b, e, prog);
-    if (b.body_force) {
-        float *f = b.body_force + (size_t)6 * p.num_groups * e;
-        const bool push = p.push_force > 0.0f && p.push_interval > 0 && prog > 0 && (prog % p.push_interval) == 0;
-        float u[3];
-        if (push_draws) {
-            u[0] = push_draws[3 * (size_t)e]; u[1] = push_draws[3 * (size_t)e + 1]; u[2] = push_draws[3 * (size_t)e + 2];
-        } else {
-            U4 x = philox(U4{(uint32_t)e, c_lo, c_hi, 0x50555348u}, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
-            u[0] = u01(x.x); u[1] = u01(x.y); u[2] = u01(x.z);
-        }
-        f[0] = push ? p.push_force * (u[0] * 2.0f - 1.0f) : 0.0f;
-        f[1] = push ? p.push_force * (u[1] * 2.0f - 1.0f) : 0.0f;
-        f[2] = push ? 0.25f * p.push_force * (u[2] * 2.0f - 1.0f) : 0.0f;
-        f[3] = 0.0f; f[4] = 0.0f; f[5] = 0.0f;
-    }
+    f[0] = push ? p.push_force * (u[0] * 2.0f - 1.0f) : 0.0f;
+    f[1] = push ? p.push_force * (u[1] * 2.0f - 1.0f) : 0.0f;
+    f[2] = push ? 0.25f * p.push_force * (u[2] * 2.0f - 1.0f) : 0.0f;
+    f[3] = 0.0f; f[4] = 0.0f; f[5] = 0.0f;
 }
 
 __global__ __launch_bounds__(64) void walk_reset_idx_kernel(tg_walk_params p, tg_walk_buffers b, const int32_t *ids,
                                                             int n, const float *reset_draws, uint32_t c_lo,
                                                             uint32_t c_hi) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int e = ids[i];
+    const int e = ids[blockIdx.x];
     if (e < 0 || e >= p.num_envs) return;
-    const int D = p.num_dof;
-    float r[4 + 2 * TG_WALK_MAX_DOF];
-    if (reset_draws) {
-        for (int k = 0; k < 4 + 2 * D; ++k) r[k] = reset_draws[(size_t)(4 + 2 * D) * e + k];
-    } else {
-        walk_reset_draws(p, e, c_lo, c_hi, r);
-    }
-    walk_reset_env(p, b, e, r);
-    walk_observe(p, b, e, 0);
+    walk_env(p, b, e, true, 0, reset_draws, c_lo, c_hi);
 }
 
 int launch_walk_pre(const tg_walk_params &p, const tg_walk_buffers &b, const float *actions, hipStream_t s) {
@@ -179,14 +174,15 @@ int launch_walk_pre(const tg_walk_params &p, const tg_walk_buffers &b, const flo
 }
 int launch_walk_post(const tg_walk_params &p, const tg_walk_buffers &b, const float *rd, const float *pd,
                      uint64_t counter, hipStream_t s) {
-    hipLaunchKernelGGL(walk_post_kernel, dim3((p.num_envs + 63) / 64), dim3(64), 0, s, p, b, rd, pd,
+    if (p.num_dof > TG_WALK_MAX_DOF) return TG_ERR_ARG;
+    hipLaunchKernelGGL(walk_post_kernel, dim3(p.num_envs), dim3(64), 0, s, p, b, rd, pd,
                        (uint32_t)counter, (uint32_t)(counter >> 32));
     return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
 }
 int launch_walk_reset_idx(const tg_walk_params &p, const tg_walk_buffers &b, const int32_t *ids, int n,
                           const float *rd, uint64_t counter, hipStream_t s) {
     if (n <= 0) return 0;
-    hipLaunchKernelGGL(walk_reset_idx_kernel, dim3((n + 63) / 64), dim3(64), 0, s, p, b, ids, n, rd,
+    hipLaunchKernelGGL(walk_reset_idx_kernel, dim3(n), dim3(64), 0, s, p, b, ids, n, rd,
                        (uint32_t)counter, (uint32_t)(counter >> 32));
     return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
 }
