@@ -10,11 +10,15 @@ reward, masked resets, timeouts) -- inputs resident in HBM, synthetic
 actions U(-1,1) from torch.Generator(seed 1234 + rank).  Rank 0 prints one
 JSON line; ``value`` = envs x steps x ranks / max-over-ranks wall time.
 
-Roofline: the dominant kernel is the articulation step kernel; its average
-launch time is measured with HIP events on the sim stream over the timed
-region, and its algorithmic bytes per env-step (state + inputs the kernel
-must read/write) give the achieved HBM rate against the
-8 TB/s MI355X peak.  cpu_baseline: the CPU oracle env (oracle/, fp64 physics +
+Roofline: the dominant kernel is the articulation step kernel
+(tg::step_par_kernel, all substeps of one simulate() in one launch); the
+library brackets every launch with HIP events on the sim stream during the
+timed region (tg_set_kernel_timing), and its algorithmic bytes per env-step
+(state + inputs the kernel must read/write) give the achieved
+HBM rate against the 8 TB/s MI355X peak.  ``traffic`` is the PMC-measured HBM
+bytes per launch of the same kernel from a committed rocprofv3 summary
+(scripts/gpu_profile.sh + scripts/pmc_summary.py) when one exists for this
+workload, else null.  cpu_baseline: the CPU oracle env (oracle/, fp64 physics +
 task restatement, OpenMP) on a bounded sample of the same workload, rank 0 only.
 """
 from __future__ import annotations
@@ -46,6 +50,21 @@ def kernel_bytes_per_env(task_name: str, env) -> int:
     read = 13 * 4 + na * 2 * 4 + na * 2 * 4 + na * 8 * 4 + nl * 2 * 4 + kc * 4 + S * 4 + 1
     write = 13 * 4 + D * 2 * 4
     return read + write
+
+
+def committed_traffic(task_name: str, num_envs: int):
+    """PMC HBM bytes per step-kernel launch from the newest committed summary for
+    this workload (profiles/*/pmc_<task><envs>.json), or (None, None)."""
+    import glob
+    hits = sorted(glob.glob(os.path.join(REPO, "profiles", "*", f"pmc_{task_name.lower()}{num_envs}.json")))
+    if not hits:
+        return None, None
+    with open(hits[-1]) as f:
+        d = json.load(f)
+    for k, v in d.items():
+        if "step_par_kernel" in k and "hbm_bytes_per_dispatch" in v:
+            return v["hbm_bytes_per_dispatch"], os.path.relpath(hits[-1], REPO) + " (FETCH_SIZE x2 + WRITE_SIZE)"
+    return None, None
 
 
 def cpu_baseline(task_name: str, num_envs: int, threads: int):
@@ -105,18 +124,8 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    # kernel timing: events around every simulate() on the sim stream
-    ev = []
-    orig_sim = env.simulate
-
-    def timed_sim():
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        orig_sim()
-        e.record()
-        ev.append((s, e))
-
-    env.simulate = timed_sim
+    env.sim.read_kernel_timing()
+    env.sim.set_kernel_timing(True)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -127,8 +136,9 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
-    env.simulate = orig_sim
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    env.sim.set_kernel_timing(False)
+    tot_ms, launches = env.sim.read_kernel_timing()
+    kern_ms = tot_ms / max(launches, 1)
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -139,6 +149,7 @@ def main():
         return
     value = N * args.steps * world / elapsed
     bpe = kernel_bytes_per_env(args.task, env)
+    traffic, traffic_src = committed_traffic(args.task, N)
     achieved = bpe * N / (kern_ms * 1e-3) / 1e9
     sim_cfg = cfg["sim"]
     out = {
@@ -158,9 +169,10 @@ def main():
                                f"{sim_cfg.get('substeps', 2)} substeps ({1.0 / sim_cfg['dt']:.1f} Hz control)",
                    "num_envs_per_gpu": N, "parallelism": f"env-dp{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "tg::step_kernel (+compose) per simulate()", "kernel_ms": kern_ms,
-                     "bytes_per_env_step": bpe},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "tg::step_par_kernel (one launch per simulate)", "kernel_ms": kern_ms,
+                     "kernel_launches": launches, "bytes_per_env_step": bpe,
+                     "algorithmic_bytes_per_launch": bpe * N, "traffic_source": traffic_src},
     }
     if not args.no_cpu_baseline and world == 1:
         try:

@@ -164,7 +164,7 @@ namespace tg {
 // compose (dirty envs only), then the tree-parallel LDS-resident step,
 // M::EPB envs x M::LPE lanes per workgroup (Thormang: 16 envs, 151 KB of LDS).
 
-template <class M> int launch_model(const StepArgs &a, hipStream_t stream) {
+template <class M> int launch_model(const StepArgs &a, hipStream_t stream, hipEvent_t ev_begin, hipEvent_t ev_end) {
     const dim3 cgrid((a.N + 63) / 64), cblock(64);
     hipLaunchKernelGGL(compose_kernel<M>, cgrid, cblock, 0, stream, a);
     constexpr size_t bytes = ParLayout<M>::template bytes<M::EPB>();
@@ -176,15 +176,17 @@ template <class M> int launch_model(const StepArgs &a, hipStream_t stream) {
             return TG_ERR_HIP;
         attr = true;
     }
+    if (ev_begin && hipEventRecord(ev_begin, stream) != hipSuccess) return TG_ERR_HIP;
     hipLaunchKernelGGL((step_par_kernel<M, M::EPB>), dim3((a.N + M::EPB - 1) / M::EPB), dim3(M::EPB * M::LPE), bytes,
                        stream, a);
+    if (ev_end && hipEventRecord(ev_end, stream) != hipSuccess) return TG_ERR_HIP;
     return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
 }
 
 #define TG_LAUNCH(MODEL) \
-    if (hash == MODEL::hash) return launch_model<MODEL>(a, stream);
+    if (hash == MODEL::hash) return launch_model<MODEL>(a, stream, ev_begin, ev_end);
 
-int launch_step(uint64_t hash, const StepArgs &a, hipStream_t stream) {
+int launch_step(uint64_t hash, const StepArgs &a, hipStream_t stream, hipEvent_t ev_begin, hipEvent_t ev_end) {
     TG_FOR_EACH_MODEL(TG_LAUNCH)
     return TG_ERR_MODEL;
 }

@@ -161,8 +161,14 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
     const int *cpath = tab + PL::T_CPATH;
     const int tid = threadIdx.x;
     const int le = tid / LPE, sub = tid % LPE;
-    const int e = min(blockIdx.x * EPB + le, a.N - 1);   // tail lanes redo the last env, never store
-    const bool owner = blockIdx.x * EPB + le < a.N;
+    // XCD-aware chunk order: workgroups are dispatched round-robin over the 8
+    // XCDs, so workgroup b takes env chunk (b % 8) * (nb / 8) + b / 8 and each
+    // XCD's L2 sees a contiguous env range (the [KC][N] composite cache rows
+    // of neighbouring chunks share 128-B lines)
+    const int nb = gridDim.x;
+    const int chunk = (nb % 8 == 0) ? (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8 : blockIdx.x;
+    const int e = min(chunk * EPB + le, a.N - 1);   // tail lanes redo the last env, never store
+    const bool owner = chunk * EPB + le < a.N;
     TG_PROF_INIT
 
     for (int i = tid; i < M::NG; i += EPB * LPE) {

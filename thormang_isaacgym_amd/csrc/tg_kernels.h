@@ -30,7 +30,9 @@ struct StepArgs {
     uint8_t *dirty;           // [N]
 };
 
-int launch_step(uint64_t hash, const StepArgs &a, hipStream_t stream);
+// ev_begin / ev_end (optional) are recorded around the step kernel itself
+int launch_step(uint64_t hash, const StepArgs &a, hipStream_t stream, hipEvent_t ev_begin = nullptr,
+                hipEvent_t ev_end = nullptr);
 int launch_compose(uint64_t hash, const StepArgs &a, hipStream_t stream);
 int compiled_hashes(uint64_t *out, int cap);
 int model_kc(uint64_t hash);

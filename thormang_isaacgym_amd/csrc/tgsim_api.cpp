@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/tg_gogoro.h"
@@ -51,6 +52,11 @@ struct tg_sim {
     float *env_origin = nullptr;
     uint8_t *dirty = nullptr;
     std::vector<void *> allocs;
+    // kernel timing (tg_set_kernel_timing): event pairs recorded, not yet read
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending, ev_free;
+    double timed_ms = 0.0;
+    int64_t timed_launches = 0;
 
     template <class T> int alloc(T **p, size_t count) {
         void *q = nullptr;
@@ -65,6 +71,8 @@ struct tg_sim {
     }
     ~tg_sim() {
         for (void *p : allocs) (void)hipFree(p);
+        for (auto *v : {&ev_pending, &ev_free})
+            for (auto &e : *v) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
     }
 };
 
@@ -342,9 +350,45 @@ int tg_apply_body_forces(tg_sim *s, const float *wrench) {
 int tg_simulate(tg_sim *s) {
     if (int rc = check_sim(s)) return rc;
     tg::StepArgs a = step_args(s);
-    int rc = tg::launch_step(s->hash, a, s->stream);
+    std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
+    if (s->timing) {
+        if (!s->ev_free.empty()) {
+            ev = s->ev_free.back();
+            s->ev_free.pop_back();
+        } else {
+            HIPCHK(hipEventCreate(&ev.first));
+            HIPCHK(hipEventCreate(&ev.second));
+        }
+        s->ev_pending.push_back(ev);
+    }
+    int rc = tg::launch_step(s->hash, a, s->stream, ev.first, ev.second);
     s->forces_pending = false;   // apply_rigid_body_force_tensors acts for one simulate call
     if (rc) return fail(rc, "step launch failed: %s", hipGetErrorString(hipGetLastError()));
+    return TG_OK;
+}
+
+int tg_set_kernel_timing(tg_sim *s, int32_t enable) {
+    if (int rc = check_sim(s)) return rc;
+    s->timing = enable != 0;
+    return TG_OK;
+}
+
+int tg_read_kernel_timing(tg_sim *s, double *total_ms, int64_t *launches) {
+    if (int rc = check_sim(s)) return rc;
+    if (!total_ms || !launches) return fail(TG_ERR_ARG, "tg_read_kernel_timing: null argument");
+    for (auto &e : s->ev_pending) {
+        HIPCHK(hipEventSynchronize(e.second));
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, e.first, e.second));
+        s->timed_ms += ms;
+        s->timed_launches += 1;
+        s->ev_free.push_back(e);
+    }
+    s->ev_pending.clear();
+    *total_ms = s->timed_ms;
+    *launches = s->timed_launches;
+    s->timed_ms = 0.0;
+    s->timed_launches = 0;
     return TG_OK;
 }
 

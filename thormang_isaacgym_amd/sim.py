@@ -129,6 +129,16 @@ class Sim:
     def sync(self):
         check(lib().tg_sync(self._h), "sync")
 
+    def set_kernel_timing(self, enable: bool):
+        """Bracket every articulation step kernel with HIP events on the sim stream."""
+        check(lib().tg_set_kernel_timing(self._h, int(bool(enable))), "set_kernel_timing")
+
+    def read_kernel_timing(self):
+        """(total kernel ms, launches) since the last read; waits for the recorded launches."""
+        ms, n = C.c_double(), C.c_int64()
+        check(lib().tg_read_kernel_timing(self._h, C.byref(ms), C.byref(n)), "read_kernel_timing")
+        return ms.value, n.value
+
     def close(self):
         if getattr(self, "_h", None):
             lib().tg_sim_destroy(self._h)
