@@ -41,101 +41,130 @@ __device__ __forceinline__ float prop(const StepArgs &a, int f, int e, int d) {
 
 // ---------------------------------------------------------------- compose
 // Per-env group composites from the locked joint positions (centre of each
-// lock window) and the per-link mass scale (domain randomisation).
+// lock window) and the per-link mass scale (domain randomisation).  One
+// wavefront per env (envs that are not dirty exit at once): link poses in
+// their group-root frame level by level (lane = link), per-link mass terms in
+// parallel, then lane g sums group g's links in link order (deterministic, the
+// order of oracle/physics_ref.c) and writes the group's cache rows.
 template <class M> __global__ __launch_bounds__(64) void compose_kernel(StepArgs a) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    const int e = blockIdx.x;
     if (e >= a.N || !a.dirty[e]) return;
     using CL = CompLayout<M>;
-    M3 TR[M::NL];
-    V3 TP[M::NL];
-    float gm[M::NG];
-    V3 gc[M::NG];
+    __shared__ float T[M::NL][12];    // link pose in its group-root frame: R (9), p (3)
+    __shared__ float LM[M::NL][10];   // link mass, com (group frame), inertia about com (group axes, 6)
+    const int lane = threadIdx.x;
+    auto wsync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    auto ldT = [&](int l, M3 &R, V3 &P) {
 #pragma unroll
-    for (int g = 0; g < M::NG; ++g) { gm[g] = 0.f; gc[g] = v3(0, 0, 0); }
-#pragma unroll
-    for (int l = 0; l < M::NL; ++l) {
-        if (M::link_is_group_root[l]) {
-            TR[l] = eye3();
-            TP[l] = v3(0, 0, 0);
-        } else {
-            const int p = M::link_parent[l];
-            const float *o = M::link_origin[l];
-            M3 Ro{{o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7], o[8]}};
-            V3 to = v3(o[9], o[10], o[11]);
-            const int d = M::link_dof[l];
-            if (d >= 0) {
-                const float q = 0.5f * (prop(a, TG_PROP_LOWER, e, d) + prop(a, TG_PROP_UPPER, e, d));
-                const float *ax = M::link_axis[l];
-                if (M::link_jtype[l] == TG_JOINT_REVOLUTE) Ro = mul(Ro, rot_axis(ax[0], ax[1], ax[2], q));
-                else if (M::link_jtype[l] == TG_JOINT_PRISMATIC) to = to + q * mul(Ro, v3(ax[0], ax[1], ax[2]));
+        for (int k = 0; k < 9; ++k) R.a[k] = T[l][k];
+        P = v3(T[l][9], T[l][10], T[l][11]);
+    };
+    for (int lev = 0; lev <= M::NLEV; ++lev) {
+        for (int l = lane; l < M::NL; l += 64) {
+            if (M::link_level[l] != lev) continue;
+            M3 R = eye3();
+            V3 P = v3(0, 0, 0);
+            if (lev > 0) {
+                const float *o = M::link_origin[l];
+                M3 Ro{{o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7], o[8]}};
+                V3 to = v3(o[9], o[10], o[11]);
+                const int d = M::link_dof[l];
+                if (d >= 0) {
+                    const float q = 0.5f * (prop(a, TG_PROP_LOWER, e, d) + prop(a, TG_PROP_UPPER, e, d));
+                    const float *ax = M::link_axis[l];
+                    if (M::link_jtype[l] == TG_JOINT_REVOLUTE) Ro = mul(Ro, rot_axis(ax[0], ax[1], ax[2], q));
+                    else if (M::link_jtype[l] == TG_JOINT_PRISMATIC) to = to + q * mul(Ro, v3(ax[0], ax[1], ax[2]));
+                }
+                M3 Rp;
+                V3 Pp;
+                ldT(M::link_parent[l], Rp, Pp);
+                R = mul(Rp, Ro);
+                P = Pp + mul(Rp, to);
             }
-            TR[l] = mul(TR[p], Ro);
-            TP[l] = TP[p] + mul(TR[p], to);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) T[l][k] = R.a[k];
+            T[l][9] = P.x; T[l][10] = P.y; T[l][11] = P.z;
         }
-        const float s = a.mass_scale ? a.mass_scale[(size_t)e * M::NL + l] : 1.0f;
-        const float ml = M::link_inertia[l][0] * s;
-        const V3 cg = mul(TR[l], v3(M::link_inertia[l][1], M::link_inertia[l][2], M::link_inertia[l][3])) + TP[l];
-        gm[M::link_group[l]] += ml;
-        gc[M::link_group[l]] = gc[M::link_group[l]] + ml * cg;
+        wsync();
     }
-    float gI[M::NG][6];
-#pragma unroll
-    for (int g = 0; g < M::NG; ++g) {
-        gc[g] = (gm[g] > 0.f ? 1.0f / gm[g] : 0.f) * gc[g];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) gI[g][k] = 0.f;
-    }
-#pragma unroll
-    for (int l = 0; l < M::NL; ++l) {
-        const int g = M::link_group[l];
+    for (int l = lane; l < M::NL; l += 64) {
+        M3 R;
+        V3 P;
+        ldT(l, R, P);
         const float s = a.mass_scale ? a.mass_scale[(size_t)e * M::NL + l] : 1.0f;
         const float *in = M::link_inertia[l];
-        const float ml = in[0] * s;
-        M3 Il{{in[4] * s, in[7] * s, in[8] * s, in[7] * s, in[5] * s, in[9] * s, in[8] * s, in[9] * s, in[6] * s}};
-        M3 RI = mul(mul(TR[l], Il), transpose(TR[l]));
-        V3 dd = mul(TR[l], v3(in[1], in[2], in[3])) + TP[l] - gc[g];
-        float d2 = dot(dd, dd);
-        gI[g][0] += RI.a[0] + ml * (d2 - dd.x * dd.x);
-        gI[g][1] += RI.a[4] + ml * (d2 - dd.y * dd.y);
-        gI[g][2] += RI.a[8] + ml * (d2 - dd.z * dd.z);
-        gI[g][3] += RI.a[1] - ml * dd.x * dd.y;
-        gI[g][4] += RI.a[2] - ml * dd.x * dd.z;
-        gI[g][5] += RI.a[5] - ml * dd.y * dd.z;
+        const V3 cg = mul(R, v3(in[1], in[2], in[3])) + P;
+        const M3 Il{{in[4] * s, in[7] * s, in[8] * s, in[7] * s, in[5] * s, in[9] * s, in[8] * s, in[9] * s, in[6] * s}};
+        const M3 RI = mul(mul(R, Il), transpose(R));
+        LM[l][0] = in[0] * s;
+        LM[l][1] = cg.x; LM[l][2] = cg.y; LM[l][3] = cg.z;
+        LM[l][4] = RI.a[0]; LM[l][5] = RI.a[4]; LM[l][6] = RI.a[8];
+        LM[l][7] = RI.a[1]; LM[l][8] = RI.a[2]; LM[l][9] = RI.a[5];
     }
+    wsync();
     float *c = a.comp;
     const size_t N = a.N;
-#pragma unroll
-    for (int g = 0; g < M::NG; ++g) {
+    for (int g = lane; g < M::NG; g += 64) {
+        const int nl = M::group_nlinks[g];
+        float gm = 0.f;
+        V3 gc = v3(0, 0, 0);
+        for (int i = 0; i < nl; ++i) {
+            const int l = M::group_links[g][i];
+            gm += LM[l][0];
+            gc = gc + LM[l][0] * v3(LM[l][1], LM[l][2], LM[l][3]);
+        }
+        gc = (gm > 0.f ? 1.0f / gm : 0.f) * gc;
+        float gI[6] = {0, 0, 0, 0, 0, 0};
+        for (int i = 0; i < nl; ++i) {
+            const int l = M::group_links[g][i];
+            const float ml = LM[l][0];
+            const V3 dd = v3(LM[l][1], LM[l][2], LM[l][3]) - gc;
+            const float d2 = dot(dd, dd);
+            gI[0] += LM[l][4] + ml * (d2 - dd.x * dd.x);
+            gI[1] += LM[l][5] + ml * (d2 - dd.y * dd.y);
+            gI[2] += LM[l][6] + ml * (d2 - dd.z * dd.z);
+            gI[3] += LM[l][7] - ml * dd.x * dd.y;
+            gI[4] += LM[l][8] - ml * dd.x * dd.z;
+            gI[5] += LM[l][9] - ml * dd.y * dd.z;
+        }
         float *ci = c + CL::inertia(g) * N + e;
-        ci[0] = gm[g];
-        ci[N] = gc[g].x; ci[2 * N] = gc[g].y; ci[3 * N] = gc[g].z;
+        ci[0] = gm;
+        ci[N] = gc.x; ci[2 * N] = gc.y; ci[3 * N] = gc.z;
 #pragma unroll
-        for (int k = 0; k < 6; ++k) ci[(4 + k) * N] = gI[g][k];
+        for (int k = 0; k < 6; ++k) ci[(4 + k) * N] = gI[k];
         if (g > 0) {
-            const int r = M::group_root[g], p = M::link_parent[r];
+            const int r = M::group_root[g];
             const float *o = M::link_origin[r];
-            M3 Ro{{o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7], o[8]}};
-            M3 R = mul(TR[p], Ro);
-            V3 t = TP[p] + mul(TR[p], v3(o[9], o[10], o[11]));
+            const M3 Ro{{o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7], o[8]}};
+            M3 Rp;
+            V3 Pp;
+            ldT(M::link_parent[r], Rp, Pp);
+            const M3 R = mul(Rp, Ro);
+            const V3 t = Pp + mul(Rp, v3(o[9], o[10], o[11]));
             float *cx = c + CL::xtree(g) * N + e;
 #pragma unroll
             for (int k = 0; k < 9; ++k) cx[k * N] = R.a[k];
             cx[9 * N] = t.x; cx[10 * N] = t.y; cx[11 * N] = t.z;
         }
     }
-#pragma unroll
-    for (int s = 0; s < M::NS; ++s) {
-        const int l = M::shape_link[s];
-        const float *o = M::shape_pose[s];
-        M3 Ro{{o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7], o[8]}};
-        M3 R = mul(TR[l], Ro);
-        V3 t = TP[l] + mul(TR[l], v3(o[9], o[10], o[11]));
-        float *cs = c + CL::shape(s) * N + e;
+    for (int sh = lane; sh < M::NS; sh += 64) {
+        const float *o = M::shape_pose[sh];
+        const M3 Ro{{o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7], o[8]}};
+        M3 Rl;
+        V3 Pl;
+        ldT(M::shape_link[sh], Rl, Pl);
+        const M3 R = mul(Rl, Ro);
+        const V3 t = Pl + mul(Rl, v3(o[9], o[10], o[11]));
+        float *cs = c + CL::shape(sh) * N + e;
 #pragma unroll
         for (int k = 0; k < 9; ++k) cs[k * N] = R.a[k];
         cs[9 * N] = t.x; cs[10 * N] = t.y; cs[11 * N] = t.z;
     }
-    a.dirty[e] = 0;
+    if (lane == 0) a.dirty[e] = 0;
 }
 
 // ---------------------------------------------------------------- contact row layout
@@ -165,8 +194,7 @@ namespace tg {
 // M::EPB envs x M::LPE lanes per workgroup (Thormang: 16 envs, 151 KB of LDS).
 
 template <class M> int launch_model(const StepArgs &a, hipStream_t stream, hipEvent_t ev_begin, hipEvent_t ev_end) {
-    const dim3 cgrid((a.N + 63) / 64), cblock(64);
-    hipLaunchKernelGGL(compose_kernel<M>, cgrid, cblock, 0, stream, a);
+    hipLaunchKernelGGL(compose_kernel<M>, dim3(a.N), dim3(64), 0, stream, a);
     constexpr size_t bytes = ParLayout<M>::template bytes<M::EPB>();
     static_assert(bytes <= 160 * 1024, "LDS budget");
     static bool attr = false;
@@ -193,8 +221,7 @@ int launch_step(uint64_t hash, const StepArgs &a, hipStream_t stream, hipEvent_t
 
 #define TG_COMPOSE(MODEL)                                                                     \
     if (hash == MODEL::hash) {                                                                \
-        dim3 grid((a.N + 63) / 64), block(64);                                                \
-        hipLaunchKernelGGL(compose_kernel<MODEL>, grid, block, 0, stream, a);                 \
+        hipLaunchKernelGGL(compose_kernel<MODEL>, dim3(a.N), dim3(64), 0, stream, a);          \
         return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;                              \
     }
 
