@@ -90,8 +90,8 @@ def cpu_baseline(task_name: str, num_envs: int, threads: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=300)
-    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--task", default="ThormangWalk")
     ap.add_argument("--num-envs", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -52,6 +52,10 @@ extern "C" {
 #endif
 
 #define TG_OK 0
+/* joint limits: damping and implicit stiffness ramp in over this distance past
+ * the limit (rad or m), keeping the step continuous at the limit */
+#define TG_LIMIT_RAMP 0.01f
+
 #define TG_ERR_ARG -1
 #define TG_ERR_HIP -2
 #define TG_ERR_MODEL -3

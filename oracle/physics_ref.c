@@ -312,9 +312,15 @@ typedef struct {
 
 static real prop(const Env *e, int f, int d) { return e->props[f * e->prop_stride + d]; }
 
-/* ABA pass 1+2+3 with the given generalised state; fills qdd (dof-indexed) and a0. */
+/* ABA pass 1+2+3 with the given generalised state; fills qdd (dof-indexed) and a0.
+ * Position/velocity drives are implicit (h*kd + h^2*kp folded into D).  Effort
+ * limits follow "implicit, then clamp" (the drive impulse of an implicit solver
+ * clamped to effort*h): with qdd_prev == NULL every drive is implicit and
+ * unclamped; with the accelerations of that first solve, a drive whose implicit
+ * end-of-substep torque te - K*qdd exceeds its effort becomes the explicit
+ * torque +-effort (continuous at the limit, exact beyond it). */
 static void aba(const Env *e, Work *w, real h, const real *q, const real *qd, const V6 v0, real *qdd, V6 a0,
-                int with_bias) {
+                int with_bias, const real *qdd_prev) {
     const tg_model_desc *m = e->m;
     int G = m->num_groups;
     for (int g = 0; g < G; ++g) {
@@ -398,8 +404,10 @@ static void aba(const Env *e, Work *w, real h, const real *q, const real *qd, co
             real kp = prop(e, TG_PROP_STIFFNESS, d), kd = prop(e, TG_PROP_DAMPING, d), eff = prop(e, TG_PROP_EFFORT, d);
             if (mode == TG_DOF_MODE_POS || mode == TG_DOF_MODE_VEL) {
                 real te = kp * (e->pos_tgt[d] - q[d] - h * qd[d]) + kd * (e->vel_tgt[d] - qd[d]);
-                if (fabs(te) <= eff) { tau += te; Dimp += h * kd + h * h * kp; }
-                else tau += te > 0 ? eff : -eff;
+                real K = h * kd + h * h * kp;
+                real ti = qdd_prev ? te - K * qdd_prev[d] : 0;
+                if (!qdd_prev || fabs(ti) <= eff) { tau += te; Dimp += K; }
+                else tau += ti > 0 ? eff : -eff;
             } else if (mode == TG_DOF_MODE_EFFORT && e->act) {
                 real a = e->act[d];
                 tau += a > eff ? eff : (a < -eff ? -eff : a);
@@ -407,8 +415,20 @@ static void aba(const Env *e, Work *w, real h, const real *q, const real *qd, co
             real lo = prop(e, TG_PROP_LOWER, d), hi = prop(e, TG_PROP_UPPER, d);
             real qp = q[d] + h * qd[d];
             real kl = e->sp->limit_stiffness * D0 / (h * h), cl = e->sp->limit_damping * D0 / h;
-            if (qp < lo && lo > -1e30) { tau += kl * (lo - qp) - cl * qd[d]; Dimp += h * cl + h * h * kl; }
-            else if (qp > hi && hi < 1e30) { tau += kl * (hi - qp) - cl * qd[d]; Dimp += h * cl + h * h * kl; }
+            /* limit spring k(lo - qp) plus damping; the damping and the implicit
+             * terms ramp in over the first TG_LIMIT_RAMP past the limit, so the
+             * step is continuous when a joint reaches its limit */
+            if (qp < lo && lo > -1e30) {
+                real r = (lo - qp) / TG_LIMIT_RAMP;
+                r = r > 1 ? 1 : r;
+                tau += kl * (lo - qp) - r * cl * qd[d];
+                Dimp += r * (h * cl + h * h * kl);
+            } else if (qp > hi && hi < 1e30) {
+                real r = (qp - hi) / TG_LIMIT_RAMP;
+                r = r > 1 ? 1 : r;
+                tau += kl * (hi - qp) - r * cl * qd[d];
+                Dimp += r * (h * cl + h * h * kl);
+            }
         } else {
             /* impulse response: same effective inertia as the dynamics pass */
             Dimp = w->D[g] - D0;
@@ -465,6 +485,19 @@ static void aba(const Env *e, Work *w, real h, const real *q, const real *qd, co
     }
 }
 
+/* does any position/velocity drive's implicit torque te - K*qdd exceed its effort? */
+static int drives_saturated(const Env *e, Work *w, real h, const real *q, const real *qd, const real *qdd) {
+    for (int g = 1; g < e->m->num_groups; ++g) {
+        int d = w->gdof[g];
+        int mode = (int)lrint(prop(e, TG_PROP_DRIVE_MODE, d));
+        if (mode != TG_DOF_MODE_POS && mode != TG_DOF_MODE_VEL) continue;
+        real kp = prop(e, TG_PROP_STIFFNESS, d), kd = prop(e, TG_PROP_DAMPING, d), eff = prop(e, TG_PROP_EFFORT, d);
+        real te = kp * (e->pos_tgt[d] - q[d] - h * qd[d]) + kd * (e->vel_tgt[d] - qd[d]);
+        if (fabs(te - (h * kd + h * h * kp) * qdd[d]) > eff) return 1;
+    }
+    return 0;
+}
+
 /* velocity of group g's spatial velocity for generalised velocity (qd, v0) with current X */
 static void group_vels(const tg_model_desc *m, Work *w, const real *qd, const V6 v0, V6 *vg) {
     memcpy(vg[0], v0, sizeof(V6));
@@ -511,8 +544,8 @@ static void impulse_response(const Env *e, Work *w, const V6 *fi, real *dqd, V6 
     }
 }
 
-/* Contact rows.  Per shape, the active points (closest torus point, sphere
- * bottom, box corners within the speculative margin) each get a NORMAL row;
+/* Contact rows.  Per shape, the contact points (closest torus point, sphere
+ * bottom, the 4 corners of a box's lowest face) each get a NORMAL row;
  * the shape's points form one friction patch (PhysX-style patch friction)
  * with two tangent rows at the patch centroid, coupled by a Coulomb cone
  * mu*sum(normal), and one torsional row about the normal limited by
@@ -594,13 +627,20 @@ static int collect_rows(const Env *e, Work *w, real h, Row *rows, Patch *patches
                 ++np;
             }
         }
+        /* every point carries a speculative normal row (continuous in the
+         * state: a row only pushes when the point would pass the rest offset
+         * within the substep).  The friction patch is anchored at the
+         * centroid of the points weighted by w = clamp((margin - phi)/margin,
+         * 0, 1) (plain centroid when no point is within the margin), with
+         * r_eff the weighted mean planar distance to it. */
         Patch *P = &patches[np_];
         P->n0 = nr;
-        P->nn = 0;
-        V3 cen = {0, 0, 0};
+        P->nn = np;
+        V3 cen = {0, 0, 0}, cen0 = {0, 0, 0};
+        real wk[8], wsum = 0;
+        const real margin = e->sp->contact_margin;
         for (int k = 0; k < np; ++k) {
             real phi = pts[k][2];
-            if (phi > e->sp->contact_margin) continue;
             Row *r = &rows[nr++];
             r->g = g; r->type = ROW_NORMAL; r->angular = 0; r->patch = np_;
             V3 rel;
@@ -613,17 +653,16 @@ static int collect_rows(const Env *e, Work *w, real h, Row *rows, Patch *patches
                 r->target = e->sp->baumgarte * (rest - phi) / h;
                 if (r->target > e->sp->max_depenetration_velocity) r->target = e->sp->max_depenetration_velocity;
             }
-            for (int j = 0; j < 3; ++j) cen[j] += pts[k][j];
-            P->nn++;
+            real wv = (margin - phi) / margin;
+            wk[k] = wv < 0 ? 0 : (wv > 1 ? 1 : wv);
+            wsum += wk[k];
+            for (int j = 0; j < 3; ++j) { cen[j] += wk[k] * pts[k][j]; cen0[j] += pts[k][j]; }
         }
-        if (P->nn == 0) continue;
-        for (int j = 0; j < 3; ++j) cen[j] /= P->nn;
+        for (int j = 0; j < 3; ++j) cen[j] = wsum > 0 ? cen[j] / wsum : cen0[j] / np;
         P->reff = 0;
-        for (int k = P->n0; k < P->n0 + P->nn; ++k) {
-            V3 pw_;
-            m3_v(w->Rw[g], rows[k].r, pw_);
-            real dx = pw_[0] + w->pw[g][0] - cen[0], dy = pw_[1] + w->pw[g][1] - cen[1];
-            P->reff += sqrt(dx * dx + dy * dy) / P->nn;
+        for (int k = 0; k < np; ++k) {
+            real dx = pts[k][0] - cen[0], dy = pts[k][1] - cen[1];
+            P->reff += (wsum > 0 ? wk[k] / wsum : 1.0 / np) * sqrt(dx * dx + dy * dy);
         }
         P->mu = 0.5 * (e->mu[s] + e->sp->ground_friction);
         /* tangent basis: rolling direction for tori (axis x n), else world x */
@@ -748,7 +787,12 @@ void oracle_physics_step_env(const tg_model_desc *m, const tg_sim_params *sp, fl
         memcpy(w.Rw[0], R, sizeof(M3));
         memcpy(w.pw[0], pos, sizeof(V3));
         V6 a0;
-        aba(&e, &w, h, q, qd, v0, qdd, a0, 1);
+        aba(&e, &w, h, q, qd, v0, qdd, a0, 1, NULL);
+        if (drives_saturated(&e, &w, h, q, qd, qdd)) {
+            real qdd0[MAXD];
+            memcpy(qdd0, qdd, sizeof(real) * D);
+            aba(&e, &w, h, q, qd, v0, qdd, a0, 1, qdd0);
+        }
         real qds[MAXD];
         V6 v0s;
         memcpy(qds, qd, sizeof(real) * D);

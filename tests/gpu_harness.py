@@ -138,6 +138,54 @@ def gogoro_env_vs_oracle(num_envs=64, steps=20, seed=0, policy=None, max_steps=1
     return err
 
 
+def sync_oracle_from_gpu(orc, env):
+    """Teacher forcing: copy every task/state buffer the GPU env shares with its
+    kernels into the oracle env, so the next step starts from identical state."""
+    for k, t in env._buf_tensors.items():
+        if t is None or k not in orc.a:
+            continue
+        dst = orc.a[k]
+        src = t.detach().cpu().numpy()
+        dst[...] = src.reshape(dst.shape).astype(dst.dtype, copy=False)
+
+
+def forced_step_errors(env, orc, act_fn, steps, act_to_orc=lambda a: a):
+    """1-step GPU-vs-oracle errors along a GPU trajectory (oracle re-synced from
+    the GPU state before every step).  Returns max errors and exact-match flags."""
+    import torch
+    err = {"obs": 0.0, "rew": 0.0, "root": 0.0, "reset_equal": True, "timeout_equal": True, "steps": steps,
+           "resets": 0}
+    obs = orc.a["obs_buf"].copy()
+    for t in range(steps):
+        sync_oracle_from_gpu(orc, env)
+        act = act_fn(obs)
+        obs_d, rew, reset, extras = env.step(torch.from_numpy(act).to("cuda:0"))
+        o_obs, o_rew, o_reset, o_to = orc.step(act_to_orc(act))
+        g_obs = obs_d["obs"].cpu().numpy()
+        err["obs"] = max(err["obs"], float(np.abs(g_obs - o_obs).max()))
+        err["rew"] = max(err["rew"], float(np.abs(rew.cpu().numpy() - o_rew).max()))
+        err["root"] = max(err["root"], float(np.abs(env.root_tensor.cpu().numpy() - orc.a["root"]).max()))
+        err["reset_equal"] &= bool(np.array_equal(reset.cpu().numpy(), o_reset))
+        err["timeout_equal"] &= bool(np.array_equal(extras["time_outs"].cpu().numpy().astype(np.uint8), o_to))
+        err["resets"] += int(o_reset.sum())
+        obs = g_obs
+    return err
+
+
+def gogoro_forced(num_envs=64, steps=1000, seed=0, max_steps=300):
+    cfg = parity_cfg(num_envs, max_steps=max_steps)
+    env = make_gpu_gogoro(cfg, NumpyDraws(seed))
+    orc = OracleGogoro(parity_cfg(num_envs, max_steps=max_steps), NumpyDraws(seed))
+    return forced_step_errors(env, orc, balance_policy, steps, act_to_orc=lambda a: a[:, 0])
+
+
+def walk_forced(num_envs=32, steps=1000, seed=0, task="ThormangWalk"):
+    env = make_gpu_walk(walk_cfg(num_envs, task), NumpyDraws(seed))
+    orc = OracleWalk(walk_cfg(num_envs, task), NumpyDraws(seed))
+    rs = np.random.default_rng(seed + 100)
+    return forced_step_errors(env, orc, lambda o: rs.uniform(-0.5, 0.5, (num_envs, orc.D)).astype(np.float32), steps)
+
+
 # ----------------------------------------------------------------------------- ThormangWalk
 class OracleWalk:
     """CPU restatement of the ThormangWalk env step (oracle/walk_task.c around
@@ -199,6 +247,7 @@ class OracleWalk:
         physics_step(self.desc, self.sp, a["root"], a["dof_state"], self.props, a["pos_target"],
                      np.zeros((n, D), np.float32), force=force, threads=self.threads)
         ids = np.nonzero(a["reset_buf"])[0]
+        self.reset_count = getattr(self, "reset_count", 0) + len(ids)
         rd = np.zeros((n, 4 + 2 * D), np.float32)
         for i in ids:
             rd[i] = self.src.uniform(4 + 2 * D)
@@ -222,6 +271,10 @@ def make_gpu_walk(cfg, draws):
     return ReplayWalk(cfg, "cuda:0", "cuda:0", -1, True, False, False)
 
 
+def n_resets(orc):
+    return getattr(orc, "reset_count", 0)
+
+
 def walk_env_vs_oracle(num_envs=32, steps=30, seed=0, task="ThormangWalk"):
     import torch
     env = make_gpu_walk(walk_cfg(num_envs, task), NumpyDraws(seed))
@@ -238,5 +291,8 @@ def walk_env_vs_oracle(num_envs=32, steps=30, seed=0, task="ThormangWalk"):
         err["root"] = max(err["root"], float(np.abs(env.root_tensor.cpu().numpy() - orc.a["root"]).max()))
         err["reset_equal"] &= bool(np.array_equal(reset.cpu().numpy(), o_reset))
         err["timeout_equal"] &= bool(np.array_equal(extras["time_outs"].cpu().numpy().astype(np.uint8), o_to))
+        if err["obs"] >= 1e-3 and "first_bad_step" not in err:
+            err["first_bad_step"] = t
+    err["resets"] = int(n_resets(orc))
     err["min_height"] = float(orc.a["root"][:, 2].min())
     return err

@@ -99,7 +99,8 @@ template <class M> struct ParLayout {
     static constexpr int SHP = LAM + K;              // per shape: mu, reff
     static constexpr int CGP = SHP + 2 * M::NSA;     // per contact group: world R (9), p (3)
     static constexpr int CGV = CGP + 12 * M::NCG;    // per contact group: free velocity (6)
-    static constexpr int TOTAL = CGV + 6 * M::NCG;
+    static constexpr int FLG = CGV + 6 * M::NCG;     // a drive exceeded its effort limit
+    static constexpr int TOTAL = FLG + 1;
     static constexpr int ES = TOTAL | 1;             // env stride
     // per-block ints after the env area
     static constexpr int T_GI = 0;
@@ -269,6 +270,16 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
     TG_PROF(0)
 
     for (int sub_i = 0; sub_i < a.substeps; ++sub_i) {
+        // Passes 1-3 run with every position/velocity drive implicit and
+        // unclamped; if some drive's implicit end-of-substep torque te - K*qdd
+        // exceeds its effort, they run once more with those drives as the
+        // explicit torque +-effort ("implicit, then clamp", as
+        // oracle/physics_ref.c aba()).  Between the two runs the F_GL slots of
+        // a drive group hold (te, K, effort) and F_UU holds qdd.
+        LDL6 rootf{};
+        SV a0 = sv0();
+#pragma unroll 1
+        for (int cp = 0; cp < 2; ++cp) {
         // ---- pass 1: root, then the schedule forward
         if (lead) {
             const V3 gl = mulT(R, grav);
@@ -343,16 +354,37 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
                 const float eff = cd[4];
                 if (mode == TG_DOF_MODE_POS || mode == TG_DOF_MODE_VEL) {
                     const float te = kp * (cd[7] - q - h * qd) + kd * (cd[8] - qd);
-                    if (fabsf(te) <= eff) { tau += te; Dimp += h * kd + h * h * kp; }
-                    else tau += te > 0.f ? eff : -eff;
-                } else if (mode == TG_DOF_MODE_EFFORT && a.act) {
-                    tau += fminf(fmaxf(cd[9], -eff), eff);
+                    const float K = h * kd + h * h * kp;
+                    bool implicit = true;
+                    if (cp == 0) {
+                        s(o + F_GL) = te;
+                        s(o + F_GL + 1) = K;
+                        s(o + F_GL + 2) = eff;
+                    } else {
+                        const float ti = te - K * s(o + F_UU);   // F_UU: qdd of the first solve
+                        if (fabsf(ti) > eff) {
+                            implicit = false;
+                            tau += ti > 0.f ? eff : -eff;
+                        }
+                    }
+                    if (implicit) { tau += te; Dimp += K; }
+                } else {
+                    if (cp == 0) s(o + F_GL + 1) = -1.f;
+                    if (mode == TG_DOF_MODE_EFFORT && a.act) tau += fminf(fmaxf(cd[9], -eff), eff);
                 }
                 const float lo = cd[5], hi = cd[6];
                 const float qp = q + h * qd;
                 const float kl = a.lim_k * D0 / (h * h), cl = a.lim_c * D0 / h;
-                if (qp < lo && lo > -1e30f) { tau += kl * (lo - qp) - cl * qd; Dimp += h * cl + h * h * kl; }
-                else if (qp > hi && hi < 1e30f) { tau += kl * (hi - qp) - cl * qd; Dimp += h * cl + h * h * kl; }
+                // limit spring + damping, damping/implicit terms ramped in past the limit
+                if (qp < lo && lo > -1e30f) {
+                    const float r = fminf((lo - qp) * (1.0f / TG_LIMIT_RAMP), 1.0f);
+                    tau += kl * (lo - qp) - r * cl * qd;
+                    Dimp += r * (h * cl + h * h * kl);
+                } else if (qp > hi && hi < 1e30f) {
+                    const float r = fminf((qp - hi) * (1.0f / TG_LIMIT_RAMP), 1.0f);
+                    tau += kl * (hi - qp) - r * cl * qd;
+                    Dimp += r * (h * cl + h * h * kl);
+                }
                 const float Dinv = 1.0f / (D0 + Dimp);
                 const float u = tau - dot(S, pA);
                 stsv(s, o + F_U, U);
@@ -369,8 +401,6 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
             TG_SYNC();
         }
         // root: every lane factors the root articulated inertia itself
-        LDL6 rootf{};
-        SV a0 = sv0();
         {
             SI IA0 = ldsi(s, F_IA);
             SV pA0 = ldsv(s, F_PA);
@@ -386,7 +416,10 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
         TG_SYNC();
         TG_PROF(2)
         // ---- pass 3: free accelerations (through the F_PA slots) and velocities
-        if (lead) stsv(s, F_PA, a0);
+        if (lead) {
+            stsv(s, F_PA, a0);
+            s(PL::FLG) = 0.f;
+        }
         TG_SYNC();
 #pragma unroll 1
         for (int t = 0; t < M::NSTEP; ++t) {
@@ -401,9 +434,16 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
                 const float qdd = (s(o + F_UU) - dot(ldsv(s, o + F_U), ap)) * s(o + F_DINV);
                 stsv(s, o + F_PA, ap + qdd * S);
                 s(o + F_QDS) = qd + h * qdd;
+                if (cp == 0) {
+                    s(o + F_UU) = qdd;
+                    const float K = s(o + F_GL + 1);
+                    if (K >= 0.f && fabsf(s(o + F_GL) - K * qdd) > s(o + F_GL + 2)) s(PL::FLG) = 1.f;
+                }
             }
             TG_SYNC();
         }
+        if (cp == 0 && s(PL::FLG) == 0.f) break;
+        }   // clamp pass
         SV v0s = v0 + h * a0;
         v0s.v = v0s.v + h * cross(v0.w, v0.v);
         if (fix_base) v0s = sv0();
@@ -464,33 +504,34 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
                     pts[2] = cw + fn - u1 + u2;
                     pts[3] = cw + fn + u1 + u2;
                 }
-                V3 cen = v3(0, 0, 0);
-                float nact = 0.f;
-                float onk[4];
+                // every point carries a speculative normal row; the friction patch
+                // is anchored at the centroid weighted by clamp((margin-phi)/margin)
+                V3 cen = v3(0, 0, 0), cen0 = v3(0, 0, 0);
+                float wk[4], wsum = 0.f;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     if (k >= nr) break;
                     const int ro = PL::ROW + (rb + k) * 8;
                     const float phi = pts[k].z;
-                    const float on = phi <= a.margin ? 1.f : 0.f;
-                    onk[k] = on;
                     stv3(s, ro, mulT(Rwg, pts[k] - pwg));
                     stv3(s, ro + 3, v3(0, 0, 1));
                     s(ro + 6) = phi > a.rest ? -(phi - a.rest) / h : fminf(a.baumgarte * (a.rest - phi) / h, a.max_depen);
-                    s(ro + 7) = on;
-                    cen = cen + on * pts[k];
-                    nact += on;
+                    s(ro + 7) = 1.f;
+                    wk[k] = fminf(fmaxf((a.margin - phi) / a.margin, 0.f), 1.f);
+                    wsum += wk[k];
+                    cen = cen + wk[k] * pts[k];
+                    cen0 = cen0 + pts[k];
                 }
-                cen = (nact > 0.f ? 1.f / nact : 0.f) * cen;
+                cen = wsum > 0.f ? (1.f / wsum) * cen : (1.f / nr) * cen0;
                 float re = 0.f;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     if (k >= nr) break;
                     const float dx = pts[k].x - cen.x, dy = pts[k].y - cen.y;
-                    re += onk[k] * sqrtf(dx * dx + dy * dy);
+                    re += (wsum > 0.f ? wk[k] / wsum : 1.f / nr) * sqrtf(dx * dx + dy * dy);
                 }
                 s(PL::SHP + 2 * sh) = 0.5f * (a.shape_mu[(size_t)e * M::NS + sh] + a.ground_mu);
-                s(PL::SHP + 2 * sh + 1) = nact > 0.f ? re / nact : 0.f;
+                s(PL::SHP + 2 * sh + 1) = re;
                 V3 t1 = v3(1, 0, 0);
                 if (kind == TG_SHAPE_TORUS) {
                     const V3 ax = v3(Rs.a[2], Rs.a[5], Rs.a[8]);
@@ -500,7 +541,7 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
                 }
                 const V3 t2 = cross(v3(0, 0, 1), t1);
                 const V3 rl = mulT(Rwg, cen - pwg);
-                const float fon = nact > 0.f ? 1.f : 0.f;
+                const float fon = 1.f;
                 for (int t = 0; t < 3; ++t) {
                     const int ro = PL::ROW + (rb + nr + t) * 8;
                     stv3(s, ro, rl);
