@@ -52,6 +52,27 @@ def kernel_bytes_per_env(task_name: str, env) -> int:
     return read + write
 
 
+def timed_region(step, steps: int, world: int, device, sync) -> float:
+    """Time exactly ``steps`` calls of ``step`` between barriers + device syncs
+    on both sides; with world > 1 return the max over ranks (all ranks get it)."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
 def committed_traffic(task_name: str, num_envs: int):
     """PMC HBM bytes per step-kernel launch from the newest committed summary for
     this workload (profiles/*/pmc_<task><envs>.json), or (None, None)."""
@@ -126,23 +147,10 @@ def main():
         step()
     env.sim.read_kernel_timing()
     env.sim.set_kernel_timing(True)
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed_region(step, args.steps, world, dev, torch.cuda.synchronize)
     env.sim.set_kernel_timing(False)
     tot_ms, launches = env.sim.read_kernel_timing()
     kern_ms = tot_ms / max(launches, 1)
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
     if rank != 0:
         if world > 1:
             torch.distributed.destroy_process_group()
