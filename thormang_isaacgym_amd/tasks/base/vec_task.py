@@ -186,6 +186,7 @@ class VecTask(Env):
         self.timeout_buf = torch.zeros(self.num_envs, device=dev, dtype=torch.bool)
         self.progress_buf = torch.zeros(self.num_envs, device=dev, dtype=torch.long)
         self.randomize_buf = torch.zeros(self.num_envs, device=dev, dtype=torch.long)
+        self.randomize_buf_bound = 0   # host-side upper bound of randomize_buf (see apply_randomizations)
         self.extras = {}
 
     def set_viewer(self):
@@ -294,9 +295,16 @@ class VecTask(Env):
             env_ids = torch.arange(self.num_envs, device=self.device)
         else:
             do_nonenv = (self.last_step - self.last_rand_step) >= rand_freq
-            rand_envs = (self.randomize_buf >= rand_freq) & (self.reset_buf != 0)
-            env_ids = torch.nonzero(rand_envs, as_tuple=False).squeeze(-1)
-            self.randomize_buf[rand_envs] = 0
+            # vec_task.py:559-563.  Nothing on the reference's path increments
+            # randomize_buf, so per-env re-sampling never fires there; a task that
+            # does increment it raises self.randomize_buf_bound (host-side upper
+            # bound), which keeps the usual path free of a device sync.
+            if self.randomize_buf_bound >= rand_freq:
+                rand_envs = (self.randomize_buf >= rand_freq) & (self.reset_buf != 0)
+                env_ids = torch.nonzero(rand_envs, as_tuple=False).squeeze(-1)
+                self.randomize_buf[rand_envs] = 0
+            else:
+                env_ids = torch.zeros(0, dtype=torch.long, device=self.device)
         if do_nonenv:
             self.last_rand_step = self.last_step
         for nonphysical in ("observations", "actions"):
