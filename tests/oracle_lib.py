@@ -20,7 +20,8 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
-        srcs = [os.path.join(REPO, "oracle", f) for f in ("gogoro_task.c", "physics_ref.c", "walk_task.c")]
+        srcs = [os.path.join(REPO, "oracle", f) for f in ("gogoro_task.c", "gogoro_paper_task.c", "physics_ref.c",
+                                                              "walk_task.c")]
         if not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in srcs):
             subprocess.run(["make", "-C", os.path.join(REPO, "oracle")], check=True, capture_output=True)
         _lib = C.CDLL(LIB)
@@ -32,6 +33,11 @@ def lib():
         _lib.oracle_walk_pre_physics.argtypes = [vp, vp, vp]
         _lib.oracle_walk_post_physics.argtypes = [vp, vp, vp, vp]
         _lib.oracle_walk_reset_env.argtypes = [vp, vp, C.c_int, vp]
+        _lib.oracle_paper_pre_physics.argtypes = [vp, vp, vp]
+        _lib.oracle_paper_reset_env.argtypes = [vp, vp, C.c_int, vp]
+        _lib.oracle_paper_post_physics.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+        _lib.oracle_paper_head_wrench.argtypes = [vp, vp]
+        _lib.oracle_paper_observation.argtypes = [vp, C.c_float, C.c_float, C.c_float, vp]
         _lib.oracle_physics_step.argtypes = [vp, vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_int]
     return _lib
 

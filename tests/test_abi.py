@@ -15,7 +15,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared_symbols():
     out = set()
-    for h in ("tgsim.h", "tg_gogoro.h", "tg_walk.h"):
+    for h in ("tgsim.h", "tg_gogoro.h", "tg_walk.h", "tg_gogoro_paper.h"):
         text = open(os.path.join(REPO, "include", h)).read()
         out |= set(re.findall(r"^(?:int|const char \*|uint64_t)\s*(tg_\w+)\(", text, re.M))
     return out
@@ -69,11 +69,14 @@ def test_struct_layouts_match_c():
 #include <stddef.h>
 #include "tg_gogoro.h"
 #include "tg_walk.h"
+#include "tg_gogoro_paper.h"
 int main(void){
  printf("%zu %zu %zu %zu %zu\n", sizeof(tg_model_desc), sizeof(tg_sim_params), sizeof(tg_state_view),
         sizeof(tg_gogoro_params), sizeof(tg_gogoro_buffers));
  printf("%zu %zu %zu %zu %zu\n", offsetof(tg_gogoro_params, max_episode_length), offsetof(tg_gogoro_params, seed),
         offsetof(tg_model_desc, model_hash), sizeof(tg_walk_params), sizeof(tg_walk_buffers));
+ printf("%zu %zu %zu %zu\n", sizeof(tg_paper_params), offsetof(tg_paper_params, head_com),
+        offsetof(tg_paper_params, seed), sizeof(tg_paper_buffers));
  return 0;}
 '''
     tmp = os.path.join(REPO, "oracle", "_build")
@@ -87,4 +90,6 @@ int main(void){
                                    abi.tg_gogoro_buffers)]
     offs = [abi.tg_gogoro_params.max_episode_length.offset, abi.tg_gogoro_params.seed.offset,
             abi.tg_model_desc.model_hash.offset, C.sizeof(abi.tg_walk_params), C.sizeof(abi.tg_walk_buffers)]
-    assert [int(x) for x in out] == sizes + offs
+    paper = [C.sizeof(abi.tg_paper_params), abi.tg_paper_params.head_com.offset, abi.tg_paper_params.seed.offset,
+             C.sizeof(abi.tg_paper_buffers)]
+    assert [int(x) for x in out] == sizes + offs + paper

@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("TG_LIB_PATH") or os.path.join(HERE, "libtgsim.so")
 
 _lib = None
 
-# (name, argtypes) -- every symbol declared in include/tgsim.h and include/tg_gogoro.h
+# (name, argtypes) -- every symbol declared in include/tgsim.h, tg_gogoro.h, tg_walk.h, tg_gogoro_paper.h
 _VP = C.c_void_p
 SIGNATURES = {
     "tg_sim_create": [C.POINTER(abi.tg_model_desc), C.POINTER(abi.tg_sim_params), C.c_int32, C.c_int32,
@@ -46,6 +46,11 @@ SIGNATURES = {
                                _VP, _VP, C.c_uint64],
     "tg_gogoro_reset_idx": [_VP, C.POINTER(abi.tg_gogoro_params), C.POINTER(abi.tg_gogoro_buffers), _VP,
                             C.c_int32, _VP, C.c_uint64],
+    "tg_paper_pre_physics": [_VP, C.POINTER(abi.tg_paper_params), C.POINTER(abi.tg_paper_buffers), _VP, C.c_uint64],
+    "tg_paper_post_physics": [_VP, C.POINTER(abi.tg_paper_params), C.POINTER(abi.tg_paper_buffers), _VP, _VP, _VP,
+                              _VP, _VP, C.c_uint64],
+    "tg_paper_reset_idx": [_VP, C.POINTER(abi.tg_paper_params), C.POINTER(abi.tg_paper_buffers), _VP, C.c_int32,
+                           _VP, C.c_uint64],
     "tg_walk_pre_physics": [_VP, C.POINTER(abi.tg_walk_params), C.POINTER(abi.tg_walk_buffers), _VP],
     "tg_walk_post_physics": [_VP, C.POINTER(abi.tg_walk_params), C.POINTER(abi.tg_walk_buffers), _VP, _VP,
                              C.c_uint64],

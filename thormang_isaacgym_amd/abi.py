@@ -85,6 +85,35 @@ class tg_gogoro_buffers(C.Structure):
         "dof_props", "env_dirty")]
 
 
+class tg_paper_params(C.Structure):
+    """include/tg_gogoro_paper.h"""
+    _fields_ = [
+        ("num_envs", C.c_int32), ("num_dof", C.c_int32), ("num_groups", C.c_int32),
+        ("dof_steer", C.c_int32), ("dof_rear", C.c_int32), ("dof_base_x", C.c_int32), ("dof_base_y", C.c_int32),
+        ("dof_base_z", C.c_int32), ("max_episode_length", C.c_int64),
+        ("speed_freq_update", C.c_int32), ("yaw_freq_update", C.c_int32),
+        ("command_delay", F2), ("imu_filter_noise", F2), ("imu_noise", F2), ("speed_sensor_noise", F2),
+        ("speed_sensor_offset", F2), ("imu_x_offset", F2), ("speed_range", F2), ("steering_offset", F2),
+        ("steering_damping_range", F2), ("seat_offset_x_range", F2), ("seat_offset_y_range", F2),
+        ("seat_offset_z_range", F2),
+        ("max_steering", C.c_float), ("max_tilt", C.c_float), ("spawn_z", C.c_float), ("start_speed", C.c_float),
+        ("push_force", C.c_float), ("push_interval", C.c_int32), ("push_max_envs", C.c_int32),
+        ("use_steer_delay", C.c_int32), ("random_damping", C.c_int32), ("center_robot", C.c_int32),
+        ("push_robot", C.c_int32), ("debug_start_speed", C.c_int32),
+        ("damping_stiffness", C.c_float), ("damping_effort", C.c_float), ("damping_velocity", C.c_float),
+        ("head_com", C.c_float * 3), ("group0_com", C.c_float * 3), ("seed", C.c_uint64),
+    ]
+
+
+class tg_paper_buffers(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in (
+        "obs_buf", "buffer_obs", "buffer_obs_noisy", "rew_buf", "reset_buf", "progress_buf", "timeout_buf",
+        "curent_command", "command_history", "steer_delay", "steer_offsets", "curent_speed", "curent_speed_offset",
+        "curent_imu_x_offset", "curent_damping_cfg", "yaw_command", "speed_no_noise", "perturbation", "root_reset",
+        "thormang_pose", "root", "dof_state", "pos_target", "vel_target", "dof_props", "body_force", "env_dirty",
+        "scratch")]
+
+
 TG_WALK_MAX_DOF = 40
 F40 = C.c_float * TG_WALK_MAX_DOF
 

@@ -31,6 +31,7 @@ UNITS = {
     # task math must follow the reference's fp32 operation order
     "gogoro_task.hip": ["-O3", "-ffp-contract=off"],
     "walk_task.hip": ["-O3", "-ffp-contract=off"],
+    "gogoro_paper_task.hip": ["-O3", "-ffp-contract=off"],
     "tgsim_api.cpp": ["-O2", "-x", "hip"],
 }
 

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "../../include/tg_gogoro.h"
+#include "../../include/tg_gogoro_paper.h"
 #include "../../include/tg_walk.h"
 #include "../../include/tgsim.h"
 
@@ -46,6 +47,11 @@ int launch_gogoro_post(const tg_gogoro_params &p, const tg_gogoro_buffers &b, co
 int launch_gogoro_reset_idx(const tg_gogoro_params &p, const tg_gogoro_buffers &b, const int32_t *ids, int n,
                             const float *reset_draws, uint64_t counter, hipStream_t stream);
 
+int launch_paper_pre(const tg_paper_params &p, const tg_paper_buffers &b, const float *actions, hipStream_t s);
+int launch_paper_post(const tg_paper_params &p, const tg_paper_buffers &b, const float *rd, const float *nd,
+                      const float *sd, const float *yd, const float *pd, uint64_t counter, hipStream_t s);
+int launch_paper_reset_idx(const tg_paper_params &p, const tg_paper_buffers &b, const int32_t *ids, int n,
+                           const float *rd, uint64_t counter, hipStream_t s);
 int launch_walk_pre(const tg_walk_params &p, const tg_walk_buffers &b, const float *actions, hipStream_t s);
 int launch_walk_post(const tg_walk_params &p, const tg_walk_buffers &b, const float *rd, const float *pd,
                      uint64_t counter, hipStream_t s);

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../include/tg_gogoro.h"
+#include "../../include/tg_gogoro_paper.h"
 #include "../../include/tgsim.h"
 #include "tg_kernels.h"
 
@@ -461,6 +462,51 @@ int tg_walk_reset_idx(tg_sim *s, const tg_walk_params *p, const tg_walk_buffers 
     if (int rc = check_walk(s, p, b)) return rc;
     if (int rc = check_ids(s, ids, n)) return rc;
     if (int rc = tg::launch_walk_reset_idx(*p, *b, ids, n, reset_draws, counter, s->stream))
+        return fail(rc, "launch failed");
+    return TG_OK;
+}
+
+static int check_paper(tg_sim *s, const tg_paper_params *p, const tg_paper_buffers *b) {
+    if (int rc = check_sim(s)) return rc;
+    if (!p || !b) return fail(TG_ERR_ARG, "paper: null argument");
+    if (p->num_envs != s->N || p->num_dof != s->D || p->num_groups != s->G)
+        return fail(TG_ERR_ARG, "paper params do not match the sim (N %d/%d, D %d/%d, G %d/%d)", p->num_envs, s->N,
+                    p->num_dof, s->D, p->num_groups, s->G);
+    const int dofs[5] = {p->dof_steer, p->dof_rear, p->dof_base_x, p->dof_base_y, p->dof_base_z};
+    for (int d : dofs)
+        if (d < 0 || d >= p->num_dof) return fail(TG_ERR_ARG, "paper: dof index %d out of range", d);
+    if ((int)p->command_delay[1] != TG_PAPER_CMD_HIST)
+        return fail(TG_ERR_ARG, "paper: command_delay[1] must be %d", TG_PAPER_CMD_HIST);
+    if (!b->scratch || !b->buffer_obs || !b->buffer_obs_noisy || !b->obs_buf)
+        return fail(TG_ERR_ARG, "paper: missing history / scratch buffers");
+    if (p->push_robot && p->push_interval <= 0) return fail(TG_ERR_ARG, "paper: push_interval must be > 0");
+    return 0;
+}
+
+int tg_paper_pre_physics(tg_sim *s, const tg_paper_params *p, const tg_paper_buffers *b, const float *actions,
+                         uint64_t counter) {
+    (void)counter;
+    if (int rc = check_paper(s, p, b)) return rc;
+    if (!actions) return fail(TG_ERR_ARG, "paper: null actions");
+    if (int rc = tg::launch_paper_pre(*p, *b, actions, s->stream)) return fail(rc, "launch failed");
+    return TG_OK;
+}
+
+int tg_paper_post_physics(tg_sim *s, const tg_paper_params *p, const tg_paper_buffers *b, const float *reset_draws,
+                          const float *noise_draws, const float *speed_draws, const float *yaw_draws,
+                          const float *push_draws, uint64_t counter) {
+    if (int rc = check_paper(s, p, b)) return rc;
+    if (int rc = tg::launch_paper_post(*p, *b, reset_draws, noise_draws, speed_draws, yaw_draws, push_draws, counter,
+                                       s->stream))
+        return fail(rc, "launch failed");
+    return TG_OK;
+}
+
+int tg_paper_reset_idx(tg_sim *s, const tg_paper_params *p, const tg_paper_buffers *b, const int32_t *ids, int32_t n,
+                       const float *reset_draws, uint64_t counter) {
+    if (int rc = check_paper(s, p, b)) return rc;
+    if (int rc = check_ids(s, ids, n)) return rc;
+    if (int rc = tg::launch_paper_reset_idx(*p, *b, ids, n, reset_draws, counter, s->stream))
         return fail(rc, "launch failed");
     return TG_OK;
 }

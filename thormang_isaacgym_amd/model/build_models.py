@@ -13,6 +13,9 @@ product path needs the URDF files.
   (gogoro_new.py:654,677) long before the rider's head can reach the ground.
   Locked joints: every ``joints_pos`` entry of cfg/task/Gogoro.yaml:61-93 plus
   the seat joints base_x/y/z (gogoro_new.py:257-262,562-572).
+* ``gogoro_v12`` -- ``scooter_V12.urdf``, the asset of the unregistered "paper"
+  variant (tasks/gogoro_realistic_turning_sim_paper.py:203): same joint tree and
+  tyres as V13, different link inertias.
 * ``thormang`` -- ``assets/urdf/gogoro/urdf/thormang3.urdf`` (44 links, 33
   revolute DOFs) for the walk task, which the reference does not contain
   (SURVEY.md §8 a11).  That URDF carries placeholder inertias (1.0 kg m^2 on
@@ -43,8 +46,8 @@ GOGORO_LOCKED = [
 ]
 
 
-def build_gogoro():
-    m = load_urdf(f"{ASSETS}/urdf/scooter_V13.urdf", "gogoro", mesh_root=f"{ASSETS}/meshes",
+def build_gogoro(urdf="scooter_V13.urdf", name="gogoro"):
+    m = load_urdf(f"{ASSETS}/urdf/{urdf}", name, mesh_root=f"{ASSETS}/meshes",
                   shape_friction={"back": 0.98, "front": 0.9})
     m.shapes = [s for s in m.shapes if s.kind == "torus"]
     m.build_groups(GOGORO_LOCKED)
@@ -71,7 +74,9 @@ def main():
     out = os.path.join(HERE, "compiled")
     os.makedirs(out, exist_ok=True)
     from thormang_isaacgym_amd.model.kat_models import all_models
-    for m in [build_gogoro(), build_thormang()] + all_models():
+    # gogoro_v12: the asset of the "paper" variant (tasks/gogoro_realistic_turning_sim_paper.py:203;
+    # same tree as V13, different link inertias), same locks (cfg/task/Gogoro_paper.yaml joints_pos)
+    for m in [build_gogoro(), build_gogoro("scooter_V12.urdf", "gogoro_v12"), build_thormang()] + all_models():
         with open(os.path.join(out, f"{m.name}.json"), "w") as f:
             f.write(m.to_json())
         print(m.name, "links", m.num_bodies, "dofs", m.num_dof, "groups", m.num_groups, "active", len(m.active_dofs),

@@ -161,7 +161,6 @@ class Gogoro(VecTask):
                 raise RuntimeError(f"task buffer {k} must be contiguous on {self.device}")
             setattr(b, k, t.data_ptr())
         self._buf_tensors = pairs
-        self._buf_tensors = pairs
         return b
 
     def _counter(self) -> int:
