@@ -108,6 +108,14 @@ template <class M> __global__ __launch_bounds__(64) void compose_kernel(StepArgs
     wsync();
     float *c = a.comp;
     const size_t N = a.N;
+    // the cache is written in joint-aligned group frames (axis e_z, codegen gq):
+    // v_new = Q^T v_old, I_new = Q^T I Q, placements R' = Q_p^T R Q_g, t' = Q_p^T t
+    auto gq = [](int g) {
+        M3 Q;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) Q.a[k] = M::gq[g][k];
+        return Q;
+    };
     for (int g = lane; g < M::NG; g += 64) {
         const int nl = M::group_nlinks[g];
         float gm = 0.f;
@@ -131,11 +139,15 @@ template <class M> __global__ __launch_bounds__(64) void compose_kernel(StepArgs
             gI[4] += LM[l][8] - ml * dd.x * dd.z;
             gI[5] += LM[l][9] - ml * dd.y * dd.z;
         }
+        const M3 Qg = gq(g);
+        const V3 gcq = mulT(Qg, gc);
+        float gIq[6];
+        sym_from(gIq, mul(mul(transpose(Qg), sym_to(gI)), Qg));
         float *ci = c + CL::inertia(g) * N + e;
         ci[0] = gm;
-        ci[N] = gc.x; ci[2 * N] = gc.y; ci[3 * N] = gc.z;
+        ci[N] = gcq.x; ci[2 * N] = gcq.y; ci[3 * N] = gcq.z;
 #pragma unroll
-        for (int k = 0; k < 6; ++k) ci[(4 + k) * N] = gI[k];
+        for (int k = 0; k < 6; ++k) ci[(4 + k) * N] = gIq[k];
         if (g > 0) {
             const int r = M::group_root[g];
             const float *o = M::link_origin[r];
@@ -143,8 +155,9 @@ template <class M> __global__ __launch_bounds__(64) void compose_kernel(StepArgs
             M3 Rp;
             V3 Pp;
             ldT(M::link_parent[r], Rp, Pp);
-            const M3 R = mul(Rp, Ro);
-            const V3 t = Pp + mul(Rp, v3(o[9], o[10], o[11]));
+            const M3 Qp = gq(M::parent[g]);
+            const M3 R = mul(mul(transpose(Qp), mul(Rp, Ro)), Qg);
+            const V3 t = mulT(Qp, Pp + mul(Rp, v3(o[9], o[10], o[11])));
             float *cx = c + CL::xtree(g) * N + e;
 #pragma unroll
             for (int k = 0; k < 9; ++k) cx[k * N] = R.a[k];
@@ -157,8 +170,9 @@ template <class M> __global__ __launch_bounds__(64) void compose_kernel(StepArgs
         M3 Rl;
         V3 Pl;
         ldT(M::shape_link[sh], Rl, Pl);
-        const M3 R = mul(Rl, Ro);
-        const V3 t = Pl + mul(Rl, v3(o[9], o[10], o[11]));
+        const M3 Qg = gq(M::shape_group[sh]);
+        const M3 R = mul(transpose(Qg), mul(Rl, Ro));
+        const V3 t = mulT(Qg, Pl + mul(Rl, v3(o[9], o[10], o[11])));
         float *cs = c + CL::shape(sh) * N + e;
 #pragma unroll
         for (int k = 0; k < 9; ++k) cs[k * N] = R.a[k];

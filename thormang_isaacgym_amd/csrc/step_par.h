@@ -86,7 +86,7 @@ __device__ __forceinline__ void stsi(const LE &s, int o, const SI &I) {
 __device__ __forceinline__ Xf ldx(const LE &s, int g) { return Xf{ldm3(s, g * GF + F_E), ldv3(s, g * GF + F_R)}; }
 
 // per-group model table in LDS (ints; axis as float bits), built once per block
-enum : int { GI_PARENT = 0, GI_DOF = 1, GI_JT = 2, GI_AX = 3, GI_NCH = 6, GI_CH = 7 };
+enum : int { GI_PARENT = 0, GI_DOF = 1, GI_JT = 2, GI_NCH = 3, GI_CH = 4 };
 
 template <class M> struct ParLayout {
     static constexpr int K = M::NROWS;
@@ -110,16 +110,31 @@ template <class M> struct ParLayout {
     template <int EPB> static constexpr size_t bytes() { return ((size_t)EPB * ES + T_TOTAL) * 4; }
 };
 
+// Group frames are joint-aligned (model/codegen.py gq, applied by
+// compose_kernel): every motion subspace is S = (e_z, 0) (revolute) or
+// (0, e_z) (prismatic), so S-products are component selects.
 struct GInfo {
     int parent, dof, jt;
-    V3 ax;
-    __device__ __forceinline__ SV S() const { return jt == TG_JOINT_REVOLUTE ? SV{ax, v3(0, 0, 0)} : SV{v3(0, 0, 0), ax}; }
 };
 
 template <class M> __device__ __forceinline__ GInfo ginfo(const int *gi, int g) {
     const int *p = gi + g * ParLayout<M>::GIW;
-    return GInfo{p[GI_PARENT], p[GI_DOF], p[GI_JT], v3(__int_as_float(p[GI_AX]), __int_as_float(p[GI_AX + 1]),
-                                                        __int_as_float(p[GI_AX + 2]))};
+    return GInfo{p[GI_PARENT], p[GI_DOF], p[GI_JT]};
+}
+
+__device__ __forceinline__ float dotS(int jt, const SV &x) { return jt == TG_JOINT_REVOLUTE ? x.w.z : x.v.z; }
+__device__ __forceinline__ SV addS(int jt, SV x, float a) {   // x + a S
+    if (jt == TG_JOINT_REVOLUTE) x.w.z += a;
+    else x.v.z += a;
+    return x;
+}
+__device__ __forceinline__ SV colS(int jt, const SI &I) {   // I S
+    return jt == TG_JOINT_REVOLUTE ? SV{v3(I.A[4], I.A[5], I.A[2]), v3(I.B[6], I.B[7], I.B[8])}
+                                   : SV{v3(I.B[2], I.B[5], I.B[8]), v3(I.C[4], I.C[5], I.C[2])};
+}
+__device__ __forceinline__ SV crmS(int jt, const SV &v, float qd) {   // v x (qd S)
+    const V3 wz = v3(v.w.y * qd, -v.w.x * qd, 0.f);
+    return jt == TG_JOINT_REVOLUTE ? SV{wz, v3(v.v.y * qd, -v.v.x * qd, 0.f)} : SV{v3(0, 0, 0), wz};
 }
 
 // world pose of group g by walking up to the root: R_g = R_0 E_a1^T ... E_g^T
@@ -177,9 +192,6 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
         p[GI_PARENT] = M::parent[i];
         p[GI_DOF] = M::gdof[i];
         p[GI_JT] = M::jtype[i];
-        p[GI_AX] = __float_as_int(M::axis[i][0]);
-        p[GI_AX + 1] = __float_as_int(M::axis[i][1]);
-        p[GI_AX + 2] = __float_as_int(M::axis[i][2]);
         p[GI_NCH] = M::nchild[i];
         for (int c = 0; c < M::MAXC; ++c) p[GI_CH + c] = M::child[i][c];
     }
@@ -307,12 +319,22 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
                 for (int k = 0; k < 9; ++k) Rpc.a[k] = ck[k];
                 V3 tr = v3(ck[9], ck[10], ck[11]);
                 const float qg = s(o + F_Q);
-                if (G.jt == TG_JOINT_REVOLUTE) Rpc = mul(Rpc, rot_axis(G.ax.x, G.ax.y, G.ax.z, qg));
-                else tr = tr + qg * mul(Rpc, G.ax);
+                if (G.jt == TG_JOINT_REVOLUTE) {   // Rpc * Rz(q)
+                    float sq, cq;
+                    __sincosf(qg, &sq, &cq);
+#pragma unroll
+                    for (int r = 0; r < 3; ++r) {
+                        const float c0 = Rpc.a[3 * r], c1 = Rpc.a[3 * r + 1];
+                        Rpc.a[3 * r] = c0 * cq + c1 * sq;
+                        Rpc.a[3 * r + 1] = c1 * cq - c0 * sq;
+                    }
+                } else {
+                    tr = tr + qg * v3(Rpc.a[2], Rpc.a[5], Rpc.a[8]);
+                }
                 const Xf X{transpose(Rpc), tr};
                 stm3(s, o + F_E, X.E);
                 stv3(s, o + F_R, tr);
-                const SV vg = xmotion(X, ldsv(s, G.parent * GF + F_V)) + s(o + F_QD) * G.S();
+                const SV vg = addS(G.jt, xmotion(X, ldsv(s, G.parent * GF + F_V)), s(o + F_QD));
                 const V3 gl = mul(X.E, ldv3(s, G.parent * GF + F_GL));
                 stsv(s, o + F_V, vg);
                 stv3(s, o + F_GL, gl);
@@ -336,7 +358,6 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
             if (g > 0) {
                 const int o = g * GF;
                 const GInfo G = ginfo<M>(gi, g);
-                const SV S = G.S();
                 SI IA = ldsi(s, o + F_IA);
                 SV pA = ldsv(s, o + F_PA);
                 const int nch = gi[g * GIW + GI_NCH];
@@ -345,9 +366,9 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
                     si_add(IA, ldsi(s, ch * GF + F_IA));
                     pA = pA + ldsv(s, ch * GF + F_PA);
                 }
-                const SV U = mul(IA, S);
+                const SV U = colS(G.jt, IA);
                 const float q = s(o + F_Q), qd = s(o + F_QD);
-                const float D0 = dot(S, U) + cd[0];
+                const float D0 = dotS(G.jt, U) + cd[0];
                 float Dimp = 0.f, tau = 0.f;
                 const int mode = (int)rintf(cd[1]);
                 const float kp = cd[2], kd = cd[3];
@@ -386,13 +407,13 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
                     Dimp += r * (h * cl + h * h * kl);
                 }
                 const float Dinv = 1.0f / (D0 + Dimp);
-                const float u = tau - dot(S, pA);
+                const float u = tau - dotS(G.jt, pA);
                 stsv(s, o + F_U, U);
                 s(o + F_DINV) = Dinv;
                 s(o + F_UU) = u;
                 SI Ia = IA;
                 si_sub_outer(Ia, U, Dinv);
-                const SV cb = crm(ldsv(s, o + F_V), qd * S);
+                const SV cb = crmS(G.jt, ldsv(s, o + F_V), qd);
                 const SV pa = pA + mul(Ia, cb) + (u * Dinv) * U;
                 const Xf X = ldx(s, g);
                 stsi(s, o + F_IA, si_to_parent(Ia, X));     // contribution to the parent
@@ -427,12 +448,11 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
             if (g > 0) {
                 const int o = g * GF;
                 const GInfo G = ginfo<M>(gi, g);
-                const SV S = G.S();
                 const float qd = s(o + F_QD);
-                const SV cb = crm(ldsv(s, o + F_V), qd * S);
+                const SV cb = crmS(G.jt, ldsv(s, o + F_V), qd);
                 const SV ap = xmotion(ldx(s, g), ldsv(s, G.parent * GF + F_PA)) + cb;
                 const float qdd = (s(o + F_UU) - dot(ldsv(s, o + F_U), ap)) * s(o + F_DINV);
-                stsv(s, o + F_PA, ap + qdd * S);
+                stsv(s, o + F_PA, addS(G.jt, ap, qdd));
                 s(o + F_QDS) = qd + h * qdd;
                 if (cp == 0) {
                     s(o + F_UU) = qdd;
@@ -461,7 +481,7 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
                 SV v = v0s;
                 for (int i = 0; i < M::cpath_len[c]; ++i) {
                     const int hg = cpath[c * M::MAXD + i];
-                    v = xmotion(ldx(s, hg), v) + s(hg * GF + F_QDS) * ginfo<M>(gi, hg).S();
+                    v = addS(ginfo<M>(gi, hg).jt, xmotion(ldx(s, hg), v), s(hg * GF + F_QDS));
                 }
                 stsv(s, PL::CGV + 6 * c, v);
             }
@@ -587,7 +607,7 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
                     du[i] = 0.f;
                     if (i < lk) {
                         const int g = pk[i];
-                        const float u = -dot(ginfo<M>(gi, g).S(), p);
+                        const float u = -dotS(ginfo<M>(gi, g).jt, p);
                         du[i] = u;
                         const SV pa = p + (u * s(g * GF + F_DINV)) * ldsv(s, g * GF + F_U);
                         p = xTforce(ldx(s, g), pa);
@@ -605,7 +625,7 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
                             const SV ap = xmotion(ldx(s, hg), av);
                             const float dui = (i < lk && pk[i] == hg) ? du[i] : 0.0f;
                             const float x = (dui - dot(ldsv(s, hg * GF + F_U), ap)) * s(hg * GF + F_DINV);
-                            av = ap + x * ginfo<M>(gi, hg).S();
+                            av = addS(M::jtype[hg], ap, x);
                         }
                     }
                     dvc[c] = av;
@@ -672,7 +692,7 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
                     SV p = ldsv(s, o + F_PA);
                     const int nch = gi[g * GIW + GI_NCH];
                     for (int c = 0; c < nch; ++c) p = p + ldsv(s, gi[g * GIW + GI_CH + c] * GF + F_PA);
-                    const float u = -dot(ginfo<M>(gi, g).S(), p);
+                    const float u = -dotS(ginfo<M>(gi, g).jt, p);
                     s(o + F_UU) = u;
                     const SV pa = p + (u * s(o + F_DINV)) * ldsv(s, o + F_U);
                     stsv(s, o + F_PA, xTforce(ldx(s, g), pa));
@@ -696,7 +716,7 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
                     const GInfo G = ginfo<M>(gi, g);
                     const SV ap = xmotion(ldx(s, g), ldsv(s, G.parent * GF + F_PA));
                     const float x = (s(o + F_UU) - dot(ldsv(s, o + F_U), ap)) * s(o + F_DINV);
-                    stsv(s, o + F_PA, ap + x * G.S());
+                    stsv(s, o + F_PA, addS(G.jt, ap, x));
                     s(o + F_QDS) += x;
                 }
                 TG_SYNC();

@@ -68,6 +68,21 @@ def lane_schedule(parent, lanes):
     return steps or [[-1] * lanes]
 
 
+def axis_frame(a) -> np.ndarray:
+    """Rotation Q (row-major 3x3) whose third column is the unit joint axis ``a``:
+    the step kernel works in joint-aligned group frames (v_old = Q v_new), where
+    every joint axis is e_z.  Q = I when ``a`` already is e_z."""
+    a = np.asarray(a, np.float64)
+    a = a / np.linalg.norm(a)
+    if np.allclose(a, [0, 0, 1]):
+        return np.eye(3)
+    ref = np.array([1.0, 0, 0]) if abs(a[0]) < 0.9 else np.array([0, 1.0, 0])
+    b1 = np.cross(ref, a)
+    b1 /= np.linalg.norm(b1)
+    b2 = np.cross(a, b1)
+    return np.stack([b1, b2, a], 1)
+
+
 def emit(m: Model, cname: str) -> str:
     d = ModelDesc(m)
     a = d.arrays
@@ -76,6 +91,7 @@ def emit(m: Model, cname: str) -> str:
     gdof = [int(a["link_dof"][r]) if g > 0 else -1 for g, r in enumerate(gr)]
     gtype = [int(a["link_jtype"][r]) if g > 0 else 0 for g, r in enumerate(gr)]
     gaxis = [a["link_axis"][r] for r in gr]
+    gq = [np.eye(3) if g == 0 else axis_frame(gaxis[g]) for g in range(G)]
     sgroup = [int(a["link_group"][l]) for l in a["shape_link"]]
     nrows_n = [shape_rows(int(k)) for k in a["shape_kind"]]
     gpar = [int(x) for x in a["group_parent"]]
@@ -122,6 +138,7 @@ def emit(m: Model, cname: str) -> str:
         f"  static constexpr int gdof[{G}] = {_arr(gdof)};",
         f"  static constexpr int jtype[{G}] = {_arr(gtype)};",
         f"  static constexpr float axis[{G}][3] = {_arr([_arr(x, _f) for x in gaxis])};",
+        f"  static constexpr float gq[{G}][9] = {_arr([_arr(q.reshape(-1), _f) for q in gq])};  // joint-aligned frames",
         f"  static constexpr int shape_group[{max(S, 1)}] = {_arr(sgroup or [0])};",
         f"  static constexpr int shape_kind[{max(S, 1)}] = {_arr(list(a['shape_kind']) or [0])};",
         f"  static constexpr int shape_nrows[{max(S, 1)}] = {_arr(nrows_n or [0])};",
