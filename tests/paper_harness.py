@@ -88,6 +88,12 @@ class OraclePaper:
             lib().oracle_paper_head_wrench(C.byref(self.p), C.byref(self.b))
         return a["obs_buf"], a["rew_buf"], a["reset_buf"], a["timeout_buf"]
 
+    def step(self, actions):
+        """pre -> oracle physics -> post (actions [N] or [N,1])."""
+        self.pre(np.asarray(actions, np.float32).reshape(-1))
+        self.physics()
+        return self.post()
+
     def physics(self, env_spacing=1.0):
         """One control step of the fp64 oracle engine (the product's tg_simulate)."""
         if self.desc is None:

@@ -84,7 +84,7 @@ def test_gpu_paper_kernels_replay_reference(name):
     print(name, "max obs err", err)
 
 
-def _env_vs_oracle(sw, n=64, steps=80, seed=3):
+def _env_vs_oracle(sw, n=64, steps=80, seed=3, forced=False):
     from tests.gpu_harness import NumpyDraws
     from tests.paper_harness import OraclePaper
     from thormang_isaacgym_amd.cfg import load_task_cfg
@@ -100,6 +100,9 @@ def _env_vs_oracle(sw, n=64, steps=80, seed=3):
     orc = OraclePaper(load_task_cfg("GogoroPaper", num_envs=n) | {"env": cfg["env"], "noises": cfg["noises"]},
                       NumpyDraws(seed), full, root_origins=env_origins(n, 1.0))
     rs = np.random.default_rng(seed + 7)
+    if forced:
+        from tests.gpu_harness import forced_step_errors
+        return forced_step_errors(env, orc, lambda o: rs.uniform(-1, 1, (n, 1)).astype(np.float32), steps)
     err = {"obs": 0.0, "rew": 0.0, "reset_equal": True, "timeout_equal": True, "resets": 0}
     for t in range(steps):
         act = rs.uniform(-1, 1, (n, 1)).astype(np.float32)
@@ -124,11 +127,24 @@ def test_gpu_paper_env_matches_oracle_fixed_base():
     assert err["reset_equal"] and err["timeout_equal"], err
 
 
+FLIPPED = dict(DEBUGFIXBASE=False, USE_STEER_DELAY=True, RANDOM_DAMPING=True, CENTER_ROBOT=False)
+
+
 def test_gpu_paper_env_matches_oracle_free_base_flags_flipped():
-    """Free base, per-env steering delay, random steering damping, random seat offsets, pushes."""
+    """Free base, per-env steering delay, random steering damping, random seat
+    offsets, pushes; random actions make the scooters fall, and the reward's
+    tanh(50 x^2) terms amplify fp32-vs-fp64 drift, so the free-running horizon
+    is 25 steps and the long horizon is teacher-forced below."""
     _cuda()
-    err = _env_vs_oracle(dict(DEBUGFIXBASE=False, USE_STEER_DELAY=True, RANDOM_DAMPING=True, CENTER_ROBOT=False),
-                         steps=40)
+    err = _env_vs_oracle(FLIPPED, steps=25)
+    print(err)
+    assert err["obs"] < 1e-3 and err["rew"] < 1e-3, err
+    assert err["reset_equal"] and err["timeout_equal"], err
+
+
+def test_gpu_paper_free_base_step_matches_oracle_along_300_steps():
+    _cuda()
+    err = _env_vs_oracle(FLIPPED, steps=300, forced=True)
     print(err)
     assert err["obs"] < 1e-3 and err["rew"] < 1e-3, err
     assert err["reset_equal"] and err["timeout_equal"], err

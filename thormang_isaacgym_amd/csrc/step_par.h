@@ -156,6 +156,18 @@ __device__ __forceinline__ void world_pose(const LE &s, const int *gi, int giw, 
 // operations execute in program order: an env-level "barrier" only has to stop
 // the compiler from moving LDS accesses across it (no s_barrier, and no
 // s_waitcnt on the prefetched global loads still in flight).
+// sum over the 8 lanes of an env with DPP moves (row half-mirror, then quad
+// swaps): every lane ends with the total, no LDS round trip
+template <int CTRL> __device__ __forceinline__ float dpp(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float sum8(float v) {
+    v += dpp<0x141>(v);   // row_half_mirror: lane i <-> 7 - i
+    v += dpp<0x4E>(v);    // quad_perm [2,3,0,1]
+    v += dpp<0xB1>(v);    // quad_perm [1,0,3,2]
+    return v;
+}
+
 #define TG_SYNC()                                          \
     do {                                                   \
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); \
@@ -638,43 +650,83 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
             // impulse accumulators (F_PA slots) cleared by all lanes
             for (int g = sub; g < M::NG; g += LPE) stsv(s, g * GF + F_PA, sv0());
             TG_SYNC();
-            // projected Gauss-Seidel with patch friction (lead lane)
-            if (lead) {
+            // projected Gauss-Seidel with patch friction, all LPE lanes of the env:
+            // each lane holds W's columns j = sub + LPE*jj and the full multiplier
+            // vector in registers; a row's W*lambda is an 8-lane reduction, so
+            // every lane computes the same update (no LDS traffic in the sweeps)
+            {
+                static_assert(LPE == 8, "sum8 reduces over 8 lanes");
+                constexpr int JL = (K + LPE - 1) / LPE;
+                float wc[K][JL], vf[K], tg[K], onr[K], wd[K], lam[K], my[JL];
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+#pragma unroll
+                    for (int jj = 0; jj < JL; ++jj) {
+                        const int j = sub + LPE * jj;
+                        wc[i][jj] = j < K ? s(PL::W + i * K + j) : 0.f;
+                    }
+                    vf[i] = s(PL::VFREE + i);
+                    tg[i] = s(PL::ROW + i * 8 + 6);
+                    onr[i] = s(PL::ROW + i * 8 + 7);
+                    wd[i] = s(PL::W + i * K + i);
+                    lam[i] = 0.f;
+                }
+#pragma unroll
+                for (int jj = 0; jj < JL; ++jj) my[jj] = 0.f;
+                auto row_v = [&](int i) {   // vfree_i + (W lambda)_i
+                    float part = 0.f;
+#pragma unroll
+                    for (int jj = 0; jj < JL; ++jj) part += wc[i][jj] * my[jj];
+                    return vf[i] + sum8(part);
+                };
+                auto set_lam = [&](int i, float v) {
+                    lam[i] = v;
+#pragma unroll
+                    for (int jj = 0; jj < JL; ++jj)
+                        if (sub + LPE * jj == i) my[jj] = v;
+                };
 #pragma unroll 1
                 for (int it = 0; it < a.iters; ++it) {
+#pragma unroll
                     for (int sh = 0; sh < M::NS; ++sh) {
                         const int rb = row_base<M>(sh), nr = M::shape_nrows[sh];
                         float Nsum = 0.f;
-                        for (int k = 0; k < nr; ++k) {
-                            const int i = rb + k;
-                            float vi = s(PL::VFREE + i);
 #pragma unroll
-                            for (int j = 0; j < K; ++j) vi += s(PL::W + i * K + j) * s(PL::LAM + j);
-                            const float l = s(PL::LAM + i) + (s(PL::ROW + i * 8 + 6) - vi) / s(PL::W + i * K + i);
-                            const float li = s(PL::ROW + i * 8 + 7) * fmaxf(l, 0.f);
-                            s(PL::LAM + i) = li;
+                        for (int k = 0; k < 4; ++k) {
+                            if (k >= nr) break;
+                            const int i = rb + k;
+                            const float vi = row_v(i);
+                            const float l = lam[i] + (tg[i] - vi) / wd[i];
+                            const float li = onr[i] * fmaxf(l, 0.f);
+                            set_lam(i, li);
                             Nsum += li;
                         }
                         const int f = rb + nr;
                         const float mu = s(PL::SHP + 2 * sh), reff = s(PL::SHP + 2 * sh + 1);
+#pragma unroll
                         for (int t = 0; t < 3; ++t) {
                             const int i = f + t;
-                            float vi = s(PL::VFREE + i);
-#pragma unroll
-                            for (int j = 0; j < K; ++j) vi += s(PL::W + i * K + j) * s(PL::LAM + j);
-                            s(PL::LAM + i) = s(PL::LAM + i) - vi / s(PL::W + i * K + i);
+                            const float vi = row_v(i);
+                            set_lam(i, lam[i] - vi / wd[i]);
                             if (t == 1) {
-                                const float l0 = s(PL::LAM + f), l1 = s(PL::LAM + f + 1);
+                                const float l0 = lam[f], l1 = lam[f + 1];
                                 const float lt = sqrtf(l0 * l0 + l1 * l1), lim = mu * Nsum;
                                 const float sc = lt > lim ? (lt > 0.f ? lim / lt : 0.f) : 1.f;
-                                s(PL::LAM + f) = l0 * sc;
-                                s(PL::LAM + f + 1) = l1 * sc;
+                                set_lam(f, l0 * sc);
+                                set_lam(f + 1, l1 * sc);
                             }
                         }
                         const float lim3 = mu * Nsum * reff;
-                        s(PL::LAM + f + 2) = fminf(fmaxf(s(PL::LAM + f + 2), -lim3), lim3);
+                        set_lam(f + 2, fminf(fmaxf(lam[f + 2], -lim3), lim3));
                     }
                 }
+                if (lead) {
+#pragma unroll
+                    for (int i = 0; i < K; ++i) s(PL::LAM + i) = lam[i];
+                }
+            }
+            TG_SYNC();
+            if (lead) {
                 // impulses into the contact groups' F_PA slots (p = -f convention)
                 for (int i = 0; i < K; ++i) {
                     const int g = M::shape_group[row_shape<M>(i)];
