@@ -5,8 +5,7 @@
 // Layout: EPB envs per workgroup, LPE lanes per env (LPE consecutive lanes of
 // one wavefront).  Each env's articulated state (per group: X, v, I^A, p^A, U,
 // D^-1, u, q, qd, qds, gravity-in-frame) lives in LDS at
-// lds[env * ES + group * GF + field]; ES is odd so the same field of the 8
-// envs of a wavefront falls in distinct banks.  At 16 envs x 2370 floats the
+// lds[env * ES + group * GF + field] with 16-byte aligned field blocks.  At 16 envs x 2370 floats the
 // Thormang block uses 148 KB of the 160 KB LDS of a CU; 4096 envs = 256
 // workgroups = one per CU.
 //
@@ -50,9 +49,11 @@ struct LE {
 };
 
 // per-group field offsets (GF floats per group)
+// (16-byte aligned blocks: X = E,r [0,12), v [12,18), I^A [20,41), p^A [44,50),
+// so the compiler can move them with ds_read/write_b128)
 enum : int {
-    F_E = 0, F_R = 9, F_V = 12, F_IA = 18, F_PA = 39, F_U = 45, F_DINV = 51, F_UU = 52, F_Q = 53, F_QD = 54,
-    F_QDS = 55, F_GL = 56, GF = 59
+    F_E = 0, F_R = 9, F_V = 12, F_Q = 18, F_QD = 19, F_IA = 20, F_DINV = 41, F_UU = 42, F_QDS = 43, F_PA = 44,
+    F_U = 50, F_GL = 56, GF = 60
 };
 
 __device__ __forceinline__ V3 ldv3(const LE &s, int o) { return v3(s(o), s(o + 1), s(o + 2)); }
@@ -101,7 +102,7 @@ template <class M> struct ParLayout {
     static constexpr int CGV = CGP + 12 * M::NCG;    // per contact group: free velocity (6)
     static constexpr int FLG = CGV + 6 * M::NCG;     // a drive exceeded its effort limit
     static constexpr int TOTAL = FLG + 1;
-    static constexpr int ES = TOTAL | 1;             // env stride
+    static constexpr int ES = (TOTAL + 3) & ~3;      // env stride (16-byte aligned)
     // per-block ints after the env area
     static constexpr int T_GI = 0;
     static constexpr int T_SCHED = M::NG * GIW;
@@ -182,7 +183,7 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
     using PL = ParLayout<M>;
     constexpr int K = PL::K;
     constexpr int GIW = PL::GIW;
-    extern __shared__ float lds_raw[];
+    extern __shared__ __attribute__((aligned(16))) float lds_raw[];
     int *tab = reinterpret_cast<int *>(lds_raw + EPB * PL::ES);
     const int *gi = tab + PL::T_GI;
     const int *sched = tab + PL::T_SCHED;
