@@ -94,7 +94,7 @@ template <class M> struct ParLayout {
     static constexpr int GIW = GI_CH + M::MAXC;
     // per-env floats
     static constexpr int W = M::NG * GF;             // K*K Delassus
-    static constexpr int ROW = W + K * K;            // K * 8: r(3) d(3) target on
+    static constexpr int ROW = W + K * K;            // K * 8: Jacobian (6) target on
     static constexpr int VFREE = ROW + K * 8;
     static constexpr int LAM = VFREE + K;
     static constexpr int SHP = LAM + K;              // per shape: mu, reff
@@ -546,8 +546,9 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
                     if (k >= nr) break;
                     const int ro = PL::ROW + (rb + k) * 8;
                     const float phi = pts[k].z;
-                    stv3(s, ro, mulT(Rwg, pts[k] - pwg));
-                    stv3(s, ro + 3, v3(0, 0, 1));
+                    // row Jacobian in the group frame: (r x d, d), d = Rwg^T e_z
+                    const V3 dl = v3(Rwg.a[6], Rwg.a[7], Rwg.a[8]);
+                    stsv(s, ro, SV{cross(mulT(Rwg, pts[k] - pwg), dl), dl});
                     s(ro + 6) = phi > a.rest ? -(phi - a.rest) / h : fminf(a.baumgarte * (a.rest - phi) / h, a.max_depen);
                     s(ro + 7) = 1.f;
                     wk[k] = fminf(fmaxf((a.margin - phi) / a.margin, 0.f), 1.f);
@@ -577,29 +578,16 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
                 const float fon = 1.f;
                 for (int t = 0; t < 3; ++t) {
                     const int ro = PL::ROW + (rb + nr + t) * 8;
-                    stv3(s, ro, rl);
-                    stv3(s, ro + 3, t == 0 ? t1 : (t == 1 ? t2 : v3(0, 0, 1)));
+                    const V3 dl = mulT(Rwg, t == 0 ? t1 : (t == 1 ? t2 : v3(0, 0, 1)));
+                    stsv(s, ro, t == 2 ? SV{dl, v3(0, 0, 0)} : SV{cross(rl, dl), dl});   // torsion row: angular
                     s(ro + 6) = 0.f;
                     s(ro + 7) = fon;
                 }
             }
             TG_SYNC();
-            // row helpers (row i on contact group cg(i))
-            auto row_is_ang = [&](int i) {
-                const int sh = row_shape<M>(i);
-                return i == row_base<M>(sh) + M::shape_nrows[sh] + 2;
-            };
-            auto rvel = [&](int i, const SV &vg) {
-                const int ro = PL::ROW + i * 8;
-                const M3 Rwg = ldm3(s, PL::CGP + 12 * M::shape_cg[row_shape<M>(i)]);
-                const V3 o = row_is_ang(i) ? mul(Rwg, vg.w) : mul(Rwg, vg.v + cross(vg.w, ldv3(s, ro)));
-                return dot(o, ldv3(s, ro + 3));
-            };
-            auto rforce = [&](int i, float lam) {
-                const int ro = PL::ROW + i * 8;
-                const V3 dl = mulT(ldm3(s, PL::CGP + 12 * M::shape_cg[row_shape<M>(i)]), ldv3(s, ro + 3));
-                return row_is_ang(i) ? SV{lam * dl, v3(0, 0, 0)} : SV{lam * cross(ldv3(s, ro), dl), lam * dl};
-            };
+            // row i: group-frame Jacobian J_i (6) -> velocity J_i . v, impulse lam J_i
+            auto rvel = [&](int i, const SV &vg) { return dot(ldsv(s, PL::ROW + i * 8), vg); };
+            auto rforce = [&](int i, float lam) { return lam * ldsv(s, PL::ROW + i * 8); };
             for (int i = sub; i < K; i += LPE) {
                 s(PL::VFREE + i) = rvel(i, ldsv(s, PL::CGV + 6 * M::shape_cg[row_shape<M>(i)]));
                 s(PL::LAM + i) = 0.f;
