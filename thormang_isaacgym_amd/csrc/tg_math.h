@@ -136,31 +136,55 @@ __device__ __forceinline__ void si_sub_outer(SI &I, const SV &U, float s) {
 #pragma unroll
         for (int j = 0; j < 3; ++j) I.B[3 * i + j] -= s * uw[i] * uv[j];
 }
-// X^T I X : express an inertia given at the child frame in the parent frame
+// X^T I X : express an inertia given at the child frame in the parent frame.
+// With X = [E 0; -E rx E] and I = [A B; B^T C]:
+//   C' = E^T C E,  B' = E^T B E + rx C',  A' = E^T A E + Y + Y^T - (rx C') rx,  Y = rx (E^T B E)^T
+// (symmetric blocks rotated as E^T (S E) keeping only the upper triangle).
+__device__ __forceinline__ void sym_rot(const float *S, const M3 &E, float *o) {   // o = E^T S E (sym)
+    const M3 T = mul(sym_to(S), E);
+    const int ii[6] = {0, 1, 2, 0, 0, 1}, jj[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const int i = ii[k], j = jj[k];
+        o[k] = E.a[i] * T.a[j] + E.a[3 + i] * T.a[3 + j] + E.a[6 + i] * T.a[6 + j];
+    }
+}
 __device__ __forceinline__ SI si_to_parent(const SI &I, const Xf &X) {
-    // rotate: R = E^T (child->parent)
-    M3 Et = transpose(X.E);
-    M3 A = mul(mul(Et, sym_to(I.A)), X.E);
-    M3 Bm = mul(mul(Et, M3{{I.B[0], I.B[1], I.B[2], I.B[3], I.B[4], I.B[5], I.B[6], I.B[7], I.B[8]}}), X.E);
-    M3 Cm = mul(mul(Et, sym_to(I.C)), X.E);
-    // translate by r: B' = B + [r]x C ; A' = A + [r]x B^T - B' [r]x
-    V3 r = X.r;
-    M3 rx = M3{{0, -r.z, r.y, r.z, 0, -r.x, -r.y, r.x, 0}};
-    M3 Bp = mul(rx, Cm);
-#pragma unroll
-    for (int k = 0; k < 9; ++k) Bp.a[k] += Bm.a[k];
-    M3 t1 = mul(rx, transpose(Bm));
-    M3 t2 = mul(Bp, rx);
     SI o;
-    M3 Ap;
+    sym_rot(I.A, X.E, o.A);
+    sym_rot(I.C, X.E, o.C);
+    const M3 Bq = mul(transpose(X.E), mul(M3{{I.B[0], I.B[1], I.B[2], I.B[3], I.B[4], I.B[5], I.B[6], I.B[7], I.B[8]}},
+                                          X.E));
+    const V3 r = X.r;
+    const M3 C = sym_to(o.C);
+    // Z = rx C'
+    M3 Z;
 #pragma unroll
-    for (int k = 0; k < 9; ++k) Ap.a[k] = A.a[k] + t1.a[k] - t2.a[k];
-    // symmetrise
-    o.A[0] = Ap.a[0]; o.A[1] = Ap.a[4]; o.A[2] = Ap.a[8];
-    o.A[3] = 0.5f * (Ap.a[1] + Ap.a[3]); o.A[4] = 0.5f * (Ap.a[2] + Ap.a[6]); o.A[5] = 0.5f * (Ap.a[5] + Ap.a[7]);
+    for (int j = 0; j < 3; ++j) {
+        Z.a[j] = r.y * C.a[6 + j] - r.z * C.a[3 + j];
+        Z.a[3 + j] = r.z * C.a[j] - r.x * C.a[6 + j];
+        Z.a[6 + j] = r.x * C.a[3 + j] - r.y * C.a[j];
+    }
 #pragma unroll
-    for (int k = 0; k < 9; ++k) o.B[k] = Bp.a[k];
-    sym_from(o.C, Cm);
+    for (int k = 0; k < 9; ++k) o.B[k] = Bq.a[k] + Z.a[k];
+    // Y = rx Bq^T: Y_ij = (r x Bq_row_j)_i
+    M3 Y;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const float b0 = Bq.a[3 * j], b1 = Bq.a[3 * j + 1], b2 = Bq.a[3 * j + 2];
+        Y.a[j] = r.y * b2 - r.z * b1;
+        Y.a[3 + j] = r.z * b0 - r.x * b2;
+        Y.a[6 + j] = r.x * b1 - r.y * b0;
+    }
+    // W = Z rx (symmetric): W_ij = (Z_row_i x r)_j
+    const int ii[6] = {0, 1, 2, 0, 0, 1}, jj[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const int i = ii[k], j = jj[k];
+        const float z0 = Z.a[3 * i], z1 = Z.a[3 * i + 1], z2 = Z.a[3 * i + 2];
+        const float w = j == 0 ? z1 * r.z - z2 * r.y : (j == 1 ? z2 * r.x - z0 * r.z : z0 * r.y - z1 * r.x);
+        o.A[k] += Y.a[3 * i + j] + Y.a[3 * j + i] - w;
+    }
     return o;
 }
 
