@@ -69,6 +69,8 @@ typedef struct tg_gogoro_params {
     int32_t num_envs;
     int32_t num_dof;
     int32_t dof_steer, dof_rear, dof_base_x, dof_base_y, dof_base_z;
+    int32_t terrain_spawn;         /* USE_TERAIN: reset z = root_reset[:,2], the per-env terrain
+                                      height - 0.03 clamped to [0, 100] (gogoro_new.py:523-534) */
     uint64_t seed;                 /* Philox key for device draws */
 } tg_gogoro_params;
 

@@ -171,6 +171,18 @@ int tg_set_body_mass_scale_indexed(tg_sim *sim, const float *scale, const int32_
 int tg_set_shape_friction_indexed(tg_sim *sim, const float *mu, const int32_t *ids, int32_t n);
 int tg_set_gravity(tg_sim *sim, const float *g3);
 int tg_apply_body_forces(tg_sim *sim, const float *wrench);
+/* Terrain ground (gym.add_triangle_mesh of the heightfield trimesh,
+ * tasks/gogoro_new.py:164-181 with terrain_utils.convert_heightfield_to_trimesh):
+ * heights [rows, cols] row-major on the HOST, vertex (i, j) at
+ * (origin_x + i*horizontal_scale, origin_y + j*horizontal_scale,
+ * heights[i][j]*vertical_scale), each cell split into the triangles
+ * (i,j)-(i+1,j+1)-(i,j+1) and (i,j)-(i+1,j)-(i+1,j+1); friction = the mesh's
+ * static/dynamic friction (combined with the shape's by averaging, like the
+ * plane's).  The z = 0 plane stays (gogoro_new.py:157-159 adds both): the
+ * ground is whichever surface is higher, and the plane outside the grid.
+ * rows = 0 removes the terrain. */
+int tg_set_heightfield(tg_sim *sim, const float *heights, int32_t rows, int32_t cols, float horizontal_scale,
+                       float vertical_scale, float origin_x, float origin_y, float friction);
 int tg_simulate(tg_sim *sim);
 int tg_sync(tg_sim *sim);
 const char *tg_last_error(void);

@@ -142,7 +142,7 @@ void oracle_gogoro_reset_env(const tg_gogoro_params *p, tg_gogoro_buffers *b, in
     float h = rot / 2.0f;
     float *root = b->root + 13 * e;
     memcpy(root, b->root_reset + 13 * e, 13 * sizeof(float));
-    root[2] = p->spawn_z;
+    if (!p->terrain_spawn) root[2] = p->spawn_z;
     root[3] = 0.0f;
     root[4] = 0.0f;
     root[5] = sinf(h);

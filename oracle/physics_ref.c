@@ -586,6 +586,94 @@ static real row_vel(const Work *w, const Row *r, const V6 *vg) {
     return dot3(out, r->d);
 }
 
+/* Terrain (tg_set_heightfield; gym.add_triangle_mesh of the
+ * convert_heightfield_to_trimesh mesh, tasks/gogoro_new.py:164-181): vertex
+ * (i, j) at (ox + i hs, oy + j hs, vs h[i][j]); cell (i, j) is split into
+ * (i,j)-(i+1,j+1)-(i,j+1) (fv >= fu) and (i,j)-(i+1,j)-(i+1,j+1) (fu >= fv).
+ * The z = 0 plane stays (gogoro_new.py:157-159 adds both), so the ground is
+ * the higher of the two.  Test infrastructure: one terrain for all envs. */
+static struct {
+    const float *h;
+    int rows, cols;
+    real hs, vs, ox, oy, mu;
+} g_hf;
+
+void oracle_set_heightfield(const float *heights, int rows, int cols, float hs, float vs, float ox, float oy,
+                            float friction) {
+    g_hf.h = rows > 0 ? heights : NULL;
+    g_hf.rows = rows;
+    g_hf.cols = cols;
+    g_hf.hs = hs;
+    g_hf.vs = vs;
+    g_hf.ox = ox;
+    g_hf.oy = oy;
+    g_hf.mu = friction;
+}
+
+/* height of the ground under (x, y); unit normal in n, *on_hf = terrain is the surface */
+static real ground_at(real x, real y, V3 n, int *on_hf) {
+    n[0] = 0; n[1] = 0; n[2] = 1;
+    *on_hf = 0;
+    if (!g_hf.h) return 0;
+    real u = (x - g_hf.ox) / g_hf.hs, v = (y - g_hf.oy) / g_hf.hs;
+    if (!(u >= 0 && v >= 0 && u <= g_hf.rows - 1 && v <= g_hf.cols - 1)) return 0;
+    int i = (int)u, j = (int)v;
+    if (i > g_hf.rows - 2) i = g_hf.rows - 2;
+    if (j > g_hf.cols - 2) j = g_hf.cols - 2;
+    real fu = u - i, fv = v - j;
+    const float *r0 = g_hf.h + (long)i * g_hf.cols + j, *r1 = r0 + g_hf.cols;
+    real h00 = g_hf.vs * r0[0], h01 = g_hf.vs * r0[1], h10 = g_hf.vs * r1[0], h11 = g_hf.vs * r1[1];
+    real gx, gy;
+    if (fu >= fv) { gx = h10 - h00; gy = h11 - h10; }
+    else          { gx = h11 - h01; gy = h01 - h00; }
+    real H = h00 + fu * gx + fv * gy;
+    if (!(H > 0)) return 0;
+    gx /= g_hf.hs;
+    gy /= g_hf.hs;
+    real inv = 1 / sqrt(gx * gx + gy * gy + 1);
+    n[0] = -gx * inv; n[1] = -gy * inv; n[2] = inv;
+    *on_hf = 1;
+    return H;
+}
+
+/* contact points of shape s (centre c, world rotation R) against the ground
+ * with normal n: the support point (torus, sphere) or the 4 corners of the
+ * box face whose outward normal points most against n */
+static int support_points(const tg_model_desc *m, int s, const M3 R, const V3 c, const V3 n, V3 *pts) {
+    if (m->shape_kind[s] == TG_SHAPE_TORUS) {
+        real Rm = m->shape_params[4 * s], rm = m->shape_params[4 * s + 1];
+        V3 a = {R[2], R[5], R[8]};
+        real an = dot3(a, n);
+        V3 d = {n[0] - an * a[0], n[1] - an * a[1], n[2] - an * a[2]};
+        real nd = sqrt(dot3(d, d));
+        if (nd < 1e-9) { d[0] = 1; d[1] = 0; d[2] = 0; nd = 1; }
+        for (int k = 0; k < 3; ++k) pts[0][k] = c[k] - Rm * d[k] / nd - rm * n[k];
+        return 1;
+    }
+    if (m->shape_kind[s] == TG_SHAPE_SPHERE) {
+        for (int k = 0; k < 3; ++k) pts[0][k] = c[k] - m->shape_params[4 * s] * n[k];
+        return 1;
+    }
+    if (m->shape_kind[s] == TG_SHAPE_BOX) {
+        V3 z;   /* box axes . n */
+        for (int k = 0; k < 3; ++k) z[k] = R[k] * n[0] + R[3 + k] * n[1] + R[6 + k] * n[2];
+        real zx = fabs(z[0]), zy = fabs(z[1]), zz = fabs(z[2]);
+        int ax = (zz >= zx && zz >= zy) ? 2 : (zy >= zx ? 1 : 0);
+        real sgn = z[ax] > 0 ? -1.0 : 1.0;
+        int a1 = ax == 0 ? 1 : 0, a2 = ax == 2 ? 1 : 2;
+        for (int k = 0; k < 4; ++k) {
+            V3 l = {0, 0, 0}, wv;
+            l[ax] = sgn * m->shape_params[4 * s + ax];
+            l[a1] = (k & 1 ? 1 : -1) * m->shape_params[4 * s + a1];
+            l[a2] = (k & 2 ? 1 : -1) * m->shape_params[4 * s + a2];
+            m3_v(R, l, wv);
+            for (int j = 0; j < 3; ++j) pts[k][j] = c[j] + wv[j];
+        }
+        return 4;
+    }
+    return 0;
+}
+
 static int collect_rows(const Env *e, Work *w, real h, Row *rows, Patch *patches, int *npatch) {
     const tg_model_desc *m = e->m;
     int nr = 0, np_ = 0;
@@ -596,37 +684,18 @@ static int collect_rows(const Env *e, Work *w, real h, Row *rows, Patch *patches
         m3_mul(w->Rw[g], w->shR[s], R);
         m3_v(w->Rw[g], w->shp[s], c);
         for (int k = 0; k < 3; ++k) c[k] += w->pw[g][k];
-        V3 pts[8];
-        int np = 0;
-        if (m->shape_kind[s] == TG_SHAPE_TORUS) {
-            real Rm = m->shape_params[4 * s], rm = m->shape_params[4 * s + 1];
-            V3 a = {R[2], R[5], R[8]};
-            V3 d = {-a[2] * a[0], -a[2] * a[1], 1 - a[2] * a[2]};
-            real nd = sqrt(dot3(d, d));
-            if (nd < 1e-9) { d[0] = 1; d[1] = 0; d[2] = 0; nd = 1; }
-            for (int k = 0; k < 3; ++k) pts[0][k] = c[k] - Rm * d[k] / nd;
-            pts[0][2] -= rm;
-            np = 1;
-        } else if (m->shape_kind[s] == TG_SHAPE_SPHERE) {
-            memcpy(pts[0], c, sizeof(V3));
-            pts[0][2] -= m->shape_params[4 * s];
-            np = 1;
-        } else if (m->shape_kind[s] == TG_SHAPE_BOX) {
-            /* the 4 corners of the face whose outward normal points most downward */
-            real zx = fabs(R[6]), zy = fabs(R[7]), zz = fabs(R[8]);
-            int ax = (zz >= zx && zz >= zy) ? 2 : (zy >= zx ? 1 : 0);
-            real sgn = R[6 + ax] > 0 ? -1.0 : 1.0;
-            int a1 = ax == 0 ? 1 : 0, a2 = ax == 2 ? 1 : 2;
-            for (int k = 0; k < 4; ++k) {
-                V3 l = {0, 0, 0}, wv;
-                l[ax] = sgn * m->shape_params[4 * s + ax];
-                l[a1] = (k & 1 ? 1 : -1) * m->shape_params[4 * s + a1];
-                l[a2] = (k & 2 ? 1 : -1) * m->shape_params[4 * s + a2];
-                m3_v(R, l, wv);
-                for (int j = 0; j < 3; ++j) pts[np][j] = c[j] + wv[j];
-                ++np;
-            }
+        /* patch normal n: the ground normal under the support point (found
+         * from the normal under the centre, refined once); e_z on the plane */
+        V3 pts[8], n = {0, 0, 1};
+        real gmu = e->sp->ground_friction;
+        if (g_hf.h) {
+            int th;
+            ground_at(c[0], c[1], n, &th);
+            support_points(m, s, R, c, n, pts);
+            ground_at(pts[0][0], pts[0][1], n, &th);
+            if (th) gmu = g_hf.mu;
         }
+        int np = support_points(m, s, R, c, n, pts);
         /* every point carries a speculative normal row (continuous in the
          * state: a row only pushes when the point would pass the rest offset
          * within the substep).  The friction patch is anchored at the
@@ -641,12 +710,18 @@ static int collect_rows(const Env *e, Work *w, real h, Row *rows, Patch *patches
         const real margin = e->sp->contact_margin;
         for (int k = 0; k < np; ++k) {
             real phi = pts[k][2];
+            if (g_hf.h) {   /* separation along the normal of the point's own triangle */
+                V3 nk;
+                int th;
+                real gz = ground_at(pts[k][0], pts[k][1], nk, &th);
+                phi = (pts[k][2] - gz) * nk[2];
+            }
             Row *r = &rows[nr++];
             r->g = g; r->type = ROW_NORMAL; r->angular = 0; r->patch = np_;
             V3 rel;
             for (int j = 0; j < 3; ++j) rel[j] = pts[k][j] - w->pw[g][j];
             m3T_v(w->Rw[g], rel, r->r);
-            r->d[0] = 0; r->d[1] = 0; r->d[2] = 1;
+            memcpy(r->d, n, sizeof(V3));
             real rest = e->sp->rest_offset;
             if (phi > rest) r->target = -(phi - rest) / h;
             else {
@@ -660,19 +735,23 @@ static int collect_rows(const Env *e, Work *w, real h, Row *rows, Patch *patches
         }
         for (int j = 0; j < 3; ++j) cen[j] = wsum > 0 ? cen[j] / wsum : cen0[j] / np;
         P->reff = 0;
-        for (int k = 0; k < np; ++k) {
-            real dx = pts[k][0] - cen[0], dy = pts[k][1] - cen[1];
-            P->reff += (wsum > 0 ? wk[k] / wsum : 1.0 / np) * sqrt(dx * dx + dy * dy);
+        for (int k = 0; k < np; ++k) {   /* distance in the contact plane */
+            V3 d = {pts[k][0] - cen[0], pts[k][1] - cen[1], pts[k][2] - cen[2]};
+            real dn = dot3(d, n);
+            for (int j = 0; j < 3; ++j) d[j] -= dn * n[j];
+            P->reff += (wsum > 0 ? wk[k] / wsum : 1.0 / np) * sqrt(dot3(d, d));
         }
-        P->mu = 0.5 * (e->mu[s] + e->sp->ground_friction);
-        /* tangent basis: rolling direction for tori (axis x n), else world x */
-        V3 t1 = {1, 0, 0}, n = {0, 0, 1}, t2;
+        P->mu = 0.5 * (e->mu[s] + gmu);
+        /* tangent basis: rolling direction for tori (axis x n), else world x in the plane */
+        V3 t1 = {1, 0, 0}, t2, x;
         if (m->shape_kind[s] == TG_SHAPE_TORUS) {
-            V3 a = {R[2], R[5], R[8]}, x;
+            V3 a = {R[2], R[5], R[8]};
             cross3(a, n, x);
-            real nx = sqrt(dot3(x, x));
-            if (nx > 1e-6) for (int j = 0; j < 3; ++j) t1[j] = x[j] / nx;
+        } else {
+            for (int j = 0; j < 3; ++j) x[j] = (j == 0) - n[0] * n[j];
         }
+        real nx = sqrt(dot3(x, x));
+        if (nx > 1e-6) for (int j = 0; j < 3; ++j) t1[j] = x[j] / nx;
         cross3(n, t1, t2);
         P->f0 = nr;
         V3 rel, rl;

@@ -50,7 +50,7 @@ def load_gogoro_model():
 
 
 class OracleGogoro:
-    def __init__(self, cfg, draws, env_spacing=1.0, threads=8):
+    def __init__(self, cfg, draws, env_spacing=1.0, threads=8, spawn_z=None):
         self.cfg = cfg
         self.src = draws
         self.threads = threads
@@ -75,6 +75,9 @@ class OracleGogoro:
         a["root"][:, 6] = 1.0
         a["root_reset"][:] = a["root"]
         a["root_reset"][:, 7:13] = 0
+        if spawn_z is not None:   # USE_TERAIN: per-env spawn heights in the reset template
+            a["root_reset"][:, 2] = spawn_z
+            self.p.terrain_spawn = 1
         self.b = abi.tg_gogoro_buffers(**{k: v.ctypes.data for k, v in a.items()})
         lo, hi = cfg["noises"]["speed_range"]
         a["curent_speed"][:] = np.float32(lo) + draws.uniform(n) * np.float32(hi - lo)
@@ -177,6 +180,45 @@ def gogoro_forced(num_envs=64, steps=1000, seed=0, max_steps=300):
     env = make_gpu_gogoro(cfg, NumpyDraws(seed))
     orc = OracleGogoro(parity_cfg(num_envs, max_steps=max_steps), NumpyDraws(seed))
     return forced_step_errors(env, orc, balance_policy, steps, act_to_orc=lambda a: a[:, 0])
+
+
+def gogoro_terrain(num_envs=64, steps=300, seed=0, max_steps=300, terrain_seed=5, forced=True):
+    """Gogoro with USE_TERAIN: the GPU env builds the Perlin terrain from the
+    CPU torch generator (seeded here), the oracle gets the same height samples,
+    origin and friction, and the envs' terrain spawn heights."""
+    import torch
+    from tests.oracle_lib import set_heightfield
+    from thormang_isaacgym_amd.tasks import gogoro as gmod
+    torch.manual_seed(terrain_seed)
+    saved, gmod.USE_TERAIN = gmod.USE_TERAIN, True
+    try:
+        env = make_gpu_gogoro(parity_cfg(num_envs, max_steps=max_steps), NumpyDraws(seed))
+    finally:
+        gmod.USE_TERAIN = saved
+    t = env.terrain
+    o = -float(env._terrain_start_mid)
+    set_heightfield(t.heightsamples.cpu().numpy(), t.V_scale, t.H_scale, o, o, friction=0.98)
+    try:
+        orc = OracleGogoro(parity_cfg(num_envs, max_steps=max_steps), NumpyDraws(seed),
+                           spawn_z=env.root_reset_tensor[:, 2].cpu().numpy())
+        if forced:
+            err = forced_step_errors(env, orc, balance_policy, steps, act_to_orc=lambda a: a[:, 0])
+        else:
+            err = {"obs": 0.0, "rew": 0.0, "root": 0.0, "reset_equal": True}
+            obs = orc.a["obs_buf"].copy()
+            for _ in range(steps):
+                act = balance_policy(obs)
+                obs_d, rew, reset, _ = env.step(torch.from_numpy(act).to("cuda:0"))
+                o_obs, o_rew, o_reset, _ = orc.step(act[:, 0])
+                err["obs"] = max(err["obs"], float(np.abs(obs_d["obs"].cpu().numpy() - o_obs).max()))
+                err["rew"] = max(err["rew"], float(np.abs(rew.cpu().numpy() - o_rew).max()))
+                err["root"] = max(err["root"], float(np.abs(env.root_tensor.cpu().numpy() - orc.a["root"]).max()))
+                err["reset_equal"] &= bool(np.array_equal(reset.cpu().numpy(), o_reset))
+                obs = o_obs.copy()
+        err["spawn_z_max"] = float(env.root_reset_tensor[:, 2].max())
+        return err
+    finally:
+        set_heightfield(None)
 
 
 def walk_forced(num_envs=32, steps=1000, seed=0, task="ThormangWalk"):

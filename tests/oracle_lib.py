@@ -39,6 +39,7 @@ def lib():
         _lib.oracle_paper_head_wrench.argtypes = [vp, vp]
         _lib.oracle_paper_observation.argtypes = [vp, C.c_float, C.c_float, C.c_float, vp]
         _lib.oracle_physics_step.argtypes = [vp, vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_int]
+        _lib.oracle_set_heightfield.argtypes = [vp, C.c_int, C.c_int] + [C.c_float] * 5
     return _lib
 
 
@@ -60,3 +61,18 @@ def physics_step(desc, sp, root, dof, props, pos_tgt, vel_tgt, act=None, force=N
         gravity = np.array(list(sp.gravity), np.float32)
     lib().oracle_physics_step(C.byref(desc.desc), C.byref(sp), n, ptr(root), ptr(dof), ptr(props), ptr(pos_tgt),
                               ptr(vel_tgt), ptr(act), ptr(force), ptr(mass_scale), ptr(mu), ptr(gravity), threads)
+
+
+_hf_keep = None   # the oracle keeps a pointer: hold the array while it is set
+
+
+def set_heightfield(heights, horizontal_scale=1.0, vertical_scale=1.0, origin_x=0.0, origin_y=0.0, friction=1.0):
+    """The oracle's terrain (tg_set_heightfield semantics); None = flat plane only."""
+    global _hf_keep
+    if heights is None:
+        lib().oracle_set_heightfield(None, 0, 0, 1.0, 1.0, 0.0, 0.0, 1.0)
+        _hf_keep = None
+        return
+    _hf_keep = np.ascontiguousarray(np.asarray(heights, np.float32))
+    r, c = _hf_keep.shape
+    lib().oracle_set_heightfield(ptr(_hf_keep), r, c, horizontal_scale, vertical_scale, origin_x, origin_y, friction)

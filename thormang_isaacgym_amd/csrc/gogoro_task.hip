@@ -91,7 +91,7 @@ __device__ void reset_env(const tg_gogoro_params &p, const tg_gogoro_buffers &b,
     const float *tpl = b.root_reset + 13 * (size_t)e;
     root[0] = tpl[0];
     root[1] = tpl[1];
-    root[2] = p.spawn_z;
+    root[2] = p.terrain_spawn ? tpl[2] : p.spawn_z;
     root[3] = 0.0f;
     root[4] = 0.0f;
     root[5] = sinf(hh);

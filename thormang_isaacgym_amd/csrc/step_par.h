@@ -176,6 +176,33 @@ __device__ __forceinline__ float sum8(float v) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); \
     } while (0)
 
+// Ground surface under world (x, y): the heightfield trimesh of
+// tg_set_heightfield (vertex (i,j) at (ox + i hs, oy + j hs, vs h[i][j]);
+// cell triangles (i,j)-(i+1,j+1)-(i,j+1) for fv >= fu and
+// (i,j)-(i+1,j)-(i+1,j+1) for fu >= fv) or the z = 0 plane, whichever is
+// higher.  Returns the height, the unit normal in n and whether the terrain
+// is the surface.  oracle/physics_ref.c ground_at is the same function.
+__device__ __forceinline__ float ground_at(const StepArgs &a, float x, float y, V3 &n, bool &on_hf) {
+    n = v3(0, 0, 1);
+    on_hf = false;
+    const float u = (x - a.hf_ox) / a.hf_hs, v = (y - a.hf_oy) / a.hf_hs;
+    if (!(u >= 0.f && v >= 0.f && u <= (float)(a.hf_rows - 1) && v <= (float)(a.hf_cols - 1))) return 0.f;
+    const int i = min((int)u, a.hf_rows - 2), j = min((int)v, a.hf_cols - 2);
+    const float fu = u - (float)i, fv = v - (float)j;
+    const float *r0 = a.hf + (size_t)i * a.hf_cols + j, *r1 = r0 + a.hf_cols;
+    const float h00 = a.hf_vs * r0[0], h01 = a.hf_vs * r0[1], h10 = a.hf_vs * r1[0], h11 = a.hf_vs * r1[1];
+    float H, gx, gy;
+    if (fu >= fv) { gx = h10 - h00; gy = h11 - h10; H = h00 + fu * gx + fv * gy; }
+    else          { gx = h11 - h01; gy = h01 - h00; H = h00 + fu * gx + fv * gy; }
+    if (!(H > 0.f)) return 0.f;
+    gx /= a.hf_hs;
+    gy /= a.hf_hs;
+    const float inv = 1.f / sqrtf(gx * gx + gy * gy + 1.f);
+    n = v3(-gx * inv, -gy * inv, inv);
+    on_hf = true;
+    return H;
+}
+
 template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a) {
     constexpr int LPE = M::LPE;
     static_assert(64 % LPE == 0, "an env's lanes must share a wavefront");
@@ -514,40 +541,62 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
                 V3 pts[4];
                 const int nr = M::shape_nrows[sh];
                 const int kind = M::shape_kind[sh];
-                if (kind == TG_SHAPE_TORUS) {
-                    const V3 ax = v3(Rs.a[2], Rs.a[5], Rs.a[8]);
-                    V3 dd = v3(-ax.z * ax.x, -ax.z * ax.y, 1.f - ax.z * ax.z);
-                    float nd = sqrtf(dot(dd, dd));
-                    if (nd < 1e-6f) { dd = v3(1, 0, 0); nd = 1.f; }
-                    pts[0] = cw - (M::shape_params[sh][0] / nd) * dd - v3(0, 0, M::shape_params[sh][1]);
-                } else if (kind == TG_SHAPE_SPHERE) {
-                    pts[0] = cw - v3(0, 0, M::shape_params[sh][0]);
-                } else {
-                    const float hx = M::shape_params[sh][0], hy = M::shape_params[sh][1], hz = M::shape_params[sh][2];
-                    const float zx = Rs.a[6], zy = Rs.a[7], zz = Rs.a[8];
-                    const float ax_ = fabsf(zx), ay_ = fabsf(zy), az_ = fabsf(zz);
-                    const V3 ex = v3(Rs.a[0], Rs.a[3], Rs.a[6]), ey = v3(Rs.a[1], Rs.a[4], Rs.a[7]),
-                             ez = v3(Rs.a[2], Rs.a[5], Rs.a[8]);
-                    V3 fn, u1, u2;
-                    if (az_ >= ax_ && az_ >= ay_) { fn = (zz > 0 ? -hz : hz) * ez; u1 = hx * ex; u2 = hy * ey; }
-                    else if (ay_ >= ax_) { fn = (zy > 0 ? -hy : hy) * ey; u1 = hx * ex; u2 = hz * ez; }
-                    else { fn = (zx > 0 ? -hx : hx) * ex; u1 = hy * ey; u2 = hz * ez; }
-                    pts[0] = cw + fn - u1 - u2;
-                    pts[1] = cw + fn + u1 - u2;
-                    pts[2] = cw + fn - u1 + u2;
-                    pts[3] = cw + fn + u1 + u2;
+                // patch normal n: the ground normal under the shape's support
+                // point (found from the normal under its centre, then refined
+                // once); e_z on the plane
+                V3 n = v3(0, 0, 1);
+                float gmu = a.ground_mu;
+                auto support = [&](V3 nn) {
+                    if (kind == TG_SHAPE_TORUS) {
+                        const V3 ax = v3(Rs.a[2], Rs.a[5], Rs.a[8]);
+                        V3 dd = nn - dot(ax, nn) * ax;
+                        float nd = sqrtf(dot(dd, dd));
+                        if (nd < 1e-6f) { dd = v3(1, 0, 0); nd = 1.f; }
+                        pts[0] = cw - (M::shape_params[sh][0] / nd) * dd - M::shape_params[sh][1] * nn;
+                    } else if (kind == TG_SHAPE_SPHERE) {
+                        pts[0] = cw - M::shape_params[sh][0] * nn;
+                    } else {
+                        // the 4 corners of the face whose outward normal points most against nn
+                        const float hx = M::shape_params[sh][0], hy = M::shape_params[sh][1], hz = M::shape_params[sh][2];
+                        const V3 ex = v3(Rs.a[0], Rs.a[3], Rs.a[6]), ey = v3(Rs.a[1], Rs.a[4], Rs.a[7]),
+                                 ez = v3(Rs.a[2], Rs.a[5], Rs.a[8]);
+                        const float zx = dot(ex, nn), zy = dot(ey, nn), zz = dot(ez, nn);
+                        const float ax_ = fabsf(zx), ay_ = fabsf(zy), az_ = fabsf(zz);
+                        V3 fn, u1, u2;
+                        if (az_ >= ax_ && az_ >= ay_) { fn = (zz > 0 ? -hz : hz) * ez; u1 = hx * ex; u2 = hy * ey; }
+                        else if (ay_ >= ax_) { fn = (zy > 0 ? -hy : hy) * ey; u1 = hx * ex; u2 = hz * ez; }
+                        else { fn = (zx > 0 ? -hx : hx) * ex; u1 = hy * ey; u2 = hz * ez; }
+                        pts[0] = cw + fn - u1 - u2;
+                        pts[1] = cw + fn + u1 - u2;
+                        pts[2] = cw + fn - u1 + u2;
+                        pts[3] = cw + fn + u1 + u2;
+                    }
+                };
+                if (a.hf) {
+                    bool th;
+                    ground_at(a, cw.x, cw.y, n, th);
+                    support(n);
+                    ground_at(a, pts[0].x, pts[0].y, n, th);
+                    if (th) gmu = a.hf_mu;
                 }
-                // every point carries a speculative normal row; the friction patch
-                // is anchored at the centroid weighted by clamp((margin-phi)/margin)
+                support(n);
+                // every point carries a speculative normal row along n; the friction
+                // patch is anchored at the centroid weighted by clamp((margin-phi)/margin)
+                const V3 dl = mulT(Rwg, n);
                 V3 cen = v3(0, 0, 0), cen0 = v3(0, 0, 0);
                 float wk[4], wsum = 0.f;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     if (k >= nr) break;
                     const int ro = PL::ROW + (rb + k) * 8;
-                    const float phi = pts[k].z;
-                    // row Jacobian in the group frame: (r x d, d), d = Rwg^T e_z
-                    const V3 dl = v3(Rwg.a[6], Rwg.a[7], Rwg.a[8]);
+                    float phi = pts[k].z;
+                    if (a.hf) {   // separation along the normal of the point's own triangle
+                        V3 nk;
+                        bool th;
+                        const float gz = ground_at(a, pts[k].x, pts[k].y, nk, th);
+                        phi = (pts[k].z - gz) * nk.z;
+                    }
+                    // row Jacobian in the group frame: (r x d, d), d = Rwg^T n
                     stsv(s, ro, SV{cross(mulT(Rwg, pts[k] - pwg), dl), dl});
                     s(ro + 6) = phi > a.rest ? -(phi - a.rest) / h : fminf(a.baumgarte * (a.rest - phi) / h, a.max_depen);
                     s(ro + 7) = 1.f;
@@ -561,25 +610,27 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     if (k >= nr) break;
-                    const float dx = pts[k].x - cen.x, dy = pts[k].y - cen.y;
-                    re += (wsum > 0.f ? wk[k] / wsum : 1.f / nr) * sqrtf(dx * dx + dy * dy);
+                    const V3 d = pts[k] - cen;
+                    const V3 dt = d - dot(d, n) * n;   // in the contact plane
+                    re += (wsum > 0.f ? wk[k] / wsum : 1.f / nr) * sqrtf(dot(dt, dt));
                 }
-                s(PL::SHP + 2 * sh) = 0.5f * (a.shape_mu[(size_t)e * M::NS + sh] + a.ground_mu);
+                s(PL::SHP + 2 * sh) = 0.5f * (a.shape_mu[(size_t)e * M::NS + sh] + gmu);
                 s(PL::SHP + 2 * sh + 1) = re;
+                // tangents: rolling direction (axis x n) for tori, else world x in the plane
                 V3 t1 = v3(1, 0, 0);
-                if (kind == TG_SHAPE_TORUS) {
-                    const V3 ax = v3(Rs.a[2], Rs.a[5], Rs.a[8]);
-                    const V3 x = cross(ax, v3(0, 0, 1));
+                {
+                    const V3 x = kind == TG_SHAPE_TORUS ? cross(v3(Rs.a[2], Rs.a[5], Rs.a[8]), n)
+                                                        : v3(1, 0, 0) - n.x * n;
                     const float nx = sqrtf(dot(x, x));
                     if (nx > 1e-6f) t1 = (1.f / nx) * x;
                 }
-                const V3 t2 = cross(v3(0, 0, 1), t1);
+                const V3 t2 = cross(n, t1);
                 const V3 rl = mulT(Rwg, cen - pwg);
                 const float fon = 1.f;
                 for (int t = 0; t < 3; ++t) {
                     const int ro = PL::ROW + (rb + nr + t) * 8;
-                    const V3 dl = mulT(Rwg, t == 0 ? t1 : (t == 1 ? t2 : v3(0, 0, 1)));
-                    stsv(s, ro, t == 2 ? SV{dl, v3(0, 0, 0)} : SV{cross(rl, dl), dl});   // torsion row: angular
+                    const V3 dt = mulT(Rwg, t == 0 ? t1 : (t == 1 ? t2 : n));
+                    stsv(s, ro, t == 2 ? SV{dt, v3(0, 0, 0)} : SV{cross(rl, dt), dt});   // torsion row: angular
                     s(ro + 6) = 0.f;
                     s(ro + 7) = fon;
                 }

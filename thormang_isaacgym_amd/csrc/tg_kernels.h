@@ -29,6 +29,9 @@ struct StepArgs {
     const float *mass_scale;  // [N,L] or null
     float *comp;              // [KC,N]
     uint8_t *dirty;           // [N]
+    const float *hf;          // terrain heights [rows, cols] or null (z = 0 plane)
+    int hf_rows, hf_cols;
+    float hf_hs, hf_vs, hf_ox, hf_oy, hf_mu;
 };
 
 // ev_begin / ev_end (optional) are recorded around the step kernel itself

@@ -52,6 +52,10 @@ struct tg_sim {
     float *props = nullptr, *force = nullptr, *mass_scale = nullptr, *shape_mu = nullptr, *comp = nullptr;
     float *env_origin = nullptr;
     uint8_t *dirty = nullptr;
+    // terrain heightfield (tg_set_heightfield)
+    float *hf = nullptr;
+    int hf_rows = 0, hf_cols = 0;
+    float hf_hs = 0.f, hf_vs = 0.f, hf_ox = 0.f, hf_oy = 0.f, hf_mu = 0.f;
     std::vector<void *> allocs;
     // kernel timing (tg_set_kernel_timing): event pairs recorded, not yet read
     bool timing = false;
@@ -72,6 +76,7 @@ struct tg_sim {
     }
     ~tg_sim() {
         for (void *p : allocs) (void)hipFree(p);
+        if (hf) (void)hipFree(hf);
         for (auto *v : {&ev_pending, &ev_free})
             for (auto &e : *v) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
     }
@@ -114,6 +119,14 @@ tg::StepArgs step_args(tg_sim *s) {
     a.mass_scale = s->mass_scale;
     a.comp = s->comp;
     a.dirty = s->dirty;
+    a.hf = s->hf_rows > 0 ? s->hf : nullptr;
+    a.hf_rows = s->hf_rows;
+    a.hf_cols = s->hf_cols;
+    a.hf_hs = s->hf_hs;
+    a.hf_vs = s->hf_vs;
+    a.hf_ox = s->hf_ox;
+    a.hf_oy = s->hf_oy;
+    a.hf_mu = s->hf_mu;
     return a;
 }
 }  // namespace
@@ -345,6 +358,33 @@ int tg_apply_body_forces(tg_sim *s, const float *wrench) {
     if (!wrench) return fail(TG_ERR_ARG, "null wrench tensor");
     if (int rc = copy_full(s, s->force, wrench, (size_t)s->N * s->G * 6)) return rc;
     s->forces_pending = true;
+    return TG_OK;
+}
+
+int tg_set_heightfield(tg_sim *s, const float *heights, int32_t rows, int32_t cols, float horizontal_scale,
+                       float vertical_scale, float origin_x, float origin_y, float friction) {
+    if (int rc = check_sim(s)) return rc;
+    if (rows == 0) {
+        s->hf_rows = s->hf_cols = 0;
+        return TG_OK;
+    }
+    if (!heights || rows < 2 || cols < 2) return fail(TG_ERR_ARG, "heightfield needs >= 2 x 2 samples");
+    if (!(horizontal_scale > 0.f)) return fail(TG_ERR_ARG, "heightfield horizontal_scale must be > 0");
+    HIPCHK(hipStreamSynchronize(s->stream));
+    if (s->hf) {
+        HIPCHK(hipFree(s->hf));
+        s->hf = nullptr;
+    }
+    const size_t bytes = (size_t)rows * cols * sizeof(float);
+    HIPCHK(hipMalloc(&s->hf, bytes));
+    HIPCHK(hipMemcpy(s->hf, heights, bytes, hipMemcpyHostToDevice));
+    s->hf_rows = rows;
+    s->hf_cols = cols;
+    s->hf_hs = horizontal_scale;
+    s->hf_vs = vertical_scale;
+    s->hf_ox = origin_x;
+    s->hf_oy = origin_y;
+    s->hf_mu = friction;
     return TG_OK;
 }
 

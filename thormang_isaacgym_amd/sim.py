@@ -123,6 +123,21 @@ class Sim:
     def apply_body_forces(self, wrench: torch.Tensor):
         check(lib().tg_apply_body_forces(self._h, _ptr(self._dev(wrench))), "apply_rigid_body_force_tensors")
 
+    def set_heightfield(self, heights, horizontal_scale: float = 1.0, vertical_scale: float = 1.0,
+                        origin_x: float = 0.0, origin_y: float = 0.0, friction: float = 1.0):
+        """gym.add_triangle_mesh of a heightfield trimesh (see tg_set_heightfield); None = flat plane."""
+        if heights is None:
+            check(lib().tg_set_heightfield(self._h, None, 0, 0, 1.0, 1.0, 0.0, 0.0, 1.0), "set_heightfield")
+            return
+        if isinstance(heights, torch.Tensor):
+            heights = heights.detach().cpu().numpy()
+        h = np.ascontiguousarray(np.asarray(heights, np.float32))
+        if h.ndim != 2:
+            raise ValueError(f"heightfield must be [rows, cols], got shape {h.shape}")
+        check(lib().tg_set_heightfield(self._h, h.ctypes.data_as(C.c_void_p), h.shape[0], h.shape[1],
+                                       float(horizontal_scale), float(vertical_scale), float(origin_x),
+                                       float(origin_y), float(friction)), "set_heightfield")
+
     def simulate(self):
         check(lib().tg_simulate(self._h), "simulate")
 

@@ -18,7 +18,10 @@ Differences from the reference, all deliberate:
   ``draw_source`` (tasks/gogoro_draws.py) replays the reference's
   ``torch.rand/randn`` call order exactly (parity tests);
 * the debug-line block (:392-420) -- viewer only, no buffer effects -- is not
-  reproduced, which removes its ~16 device->host syncs per step.
+  reproduced, which removes its ~16 device->host syncs per step;
+* ``USE_TERAIN`` (:26, :157-181, :523-534) hands the Perlin height samples to
+  the simulator (tg_set_heightfield) instead of a triangle mesh: the contact
+  kernel evaluates that mesh's surface directly (tasks/terrain.py).
 """
 from __future__ import annotations
 
@@ -33,6 +36,7 @@ from ..sim import load_model
 from .base.vec_task import VecTask
 from .gogoro_cfg import ASSET_OPTIONS, gogoro_params, initial_dof_props, thormang_pose
 from .gogoro_draws import post_draws, reset_draws
+from .terrain import Terrain
 
 # module-level switches of the reference (gogoro_new.py:22-27)
 DEBUGFIXBASE = False
@@ -49,8 +53,6 @@ class Gogoro(VecTask):
     draw_source = None
 
     def __init__(self, cfg, rl_device, sim_device, graphics_device_id, headless, virtual_screen_capture, force_render):
-        if USE_TERAIN:
-            raise NotImplementedError("Perlin terrain (gogoro_new.py:165-181) is not part of this build")
         if not INCREMENTAL_STEER:
             raise NotImplementedError("only the registered INCREMENTAL_STEER=True behaviour is fused")
         self.curent_step = 0
@@ -117,6 +119,9 @@ class Gogoro(VecTask):
         self.root_reset_tensor[:, 7:13] = 0
         self.curent_perturbations = torch.zeros(self.n_envs, self.num_rgbd, 3, device=self.device)
         self.params = gogoro_params(self.cfg, self.dof_name_to_id, self.n_envs, self.seed)
+        if self.terrain is not None:
+            self.root_reset_tensor[:, 2] = self._terrain_spawn_z()
+            self.params.terrain_spawn = 1
         self._bufs = self._make_buffers()
         self.reset_idx(torch.arange(0, self.n_envs, device=self.device).type(torch.long))
 
@@ -128,8 +133,39 @@ class Gogoro(VecTask):
         model = load_model("gogoro")
         asset_options = dict(ASSET_OPTIONS, fix_base_link=DEBUGFIXBASE)
         self.sim = self.create_sim_object(model, asset_options, env_spacing=self.env_spacing)
+        self.terrain = None
+        if USE_TERAIN:
+            self._create_ground_plane()
         self._create_envs(model)
         self.apply_randomizations(self.randomization_params)
+
+    #: grid pitch the terrain placement assumes (gogoro_new.py:171, = 2 x env_spacing)
+    terrain_env_pitch = 2
+
+    def _create_ground_plane(self):
+        """The Perlin terrain beside the z = 0 plane (gogoro_new.py:164-181):
+        a 512 x 512 heightfield drawn from the CPU torch generator, shifted by
+        -start_mid in x and y so the env grid sits in its middle, friction 0.98."""
+        self.terrain = Terrain()
+        envs_scale = self.terrain_env_pitch * int(np.sqrt(self.n_envs))
+        self._terrain_start_mid = int(self.terrain.Vx_size_m / 2 - envs_scale / 2)
+        o = -float(self._terrain_start_mid)
+        self.sim.set_heightfield(self.terrain.heightsamples, self.terrain.V_scale, self.terrain.H_scale, o, o,
+                                 friction=0.98)
+        self.terrain.heightsamples = self.terrain.heightsamples.to(self.device)
+
+    def _terrain_spawn_z(self) -> torch.Tensor:
+        """Per-env reset height on the terrain (gogoro_new.py:523-534): the
+        height sample under the env origin, minus 0.03, clamped to [0, 100]."""
+        t = self.terrain
+        sq = int(np.sqrt(self.n_envs))
+        smi = int(self._terrain_start_mid * (1 / t.V_scale))
+        e = torch.arange(self.n_envs, device=self.device, dtype=torch.int32)
+        step = self.terrain_env_pitch / t.V_scale
+        ix = smi + ((e % sq) * step).to(torch.int)
+        iy = smi + ((e // sq) * step).to(torch.int)
+        z = t.heightsamples[ix.long(), iy.long()] * t.H_scale - 0.03
+        return torch.clamp(z, 0, 100.0)
 
     def _create_envs(self, model):
         """DOF properties exactly as gogoro_new.py:231-294 sets them, for all envs at once."""
