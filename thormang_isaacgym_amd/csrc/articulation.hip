@@ -207,20 +207,27 @@ namespace tg {
 // compose (dirty envs only), then the tree-parallel LDS-resident step,
 // M::EPB envs x M::LPE lanes per workgroup (Thormang: 16 envs, 151 KB of LDS).
 
-template <class M> int launch_model(const StepArgs &a, hipStream_t stream, hipEvent_t ev_begin, hipEvent_t ev_end) {
-    hipLaunchKernelGGL(compose_kernel<M>, dim3(a.N), dim3(64), 0, stream, a);
+// HF: terrain heightfield present (tg_set_heightfield); the flat-ground
+// instantiation keeps the contact normal a compile-time e_z.
+template <class M, bool HF> int launch_par(const StepArgs &a, hipStream_t stream) {
     constexpr size_t bytes = ParLayout<M>::template bytes<M::EPB>();
     static_assert(bytes <= 160 * 1024, "LDS budget");
     static bool attr = false;
     if (!attr) {
-        if (hipFuncSetAttribute((const void *)step_par_kernel<M, M::EPB>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)bytes) != hipSuccess)
+        if (hipFuncSetAttribute((const void *)step_par_kernel<M, M::EPB, HF>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess)
             return TG_ERR_HIP;
         attr = true;
     }
+    hipLaunchKernelGGL((step_par_kernel<M, M::EPB, HF>), dim3((a.N + M::EPB - 1) / M::EPB), dim3(M::EPB * M::LPE),
+                       bytes, stream, a);
+    return 0;
+}
+
+template <class M> int launch_model(const StepArgs &a, hipStream_t stream, hipEvent_t ev_begin, hipEvent_t ev_end) {
+    hipLaunchKernelGGL(compose_kernel<M>, dim3(a.N), dim3(64), 0, stream, a);
     if (ev_begin && hipEventRecord(ev_begin, stream) != hipSuccess) return TG_ERR_HIP;
-    hipLaunchKernelGGL((step_par_kernel<M, M::EPB>), dim3((a.N + M::EPB - 1) / M::EPB), dim3(M::EPB * M::LPE), bytes,
-                       stream, a);
+    if (int rc = a.hf ? launch_par<M, true>(a, stream) : launch_par<M, false>(a, stream)) return rc;
     if (ev_end && hipEventRecord(ev_end, stream) != hipSuccess) return TG_ERR_HIP;
     return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
 }

@@ -203,7 +203,7 @@ __device__ __forceinline__ float ground_at(const StepArgs &a, float x, float y, 
     return H;
 }
 
-template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a) {
+template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a) {
     constexpr int LPE = M::LPE;
     static_assert(64 % LPE == 0, "an env's lanes must share a wavefront");
     using CL = CompLayout<M>;
@@ -572,7 +572,7 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
                         pts[3] = cw + fn + u1 + u2;
                     }
                 };
-                if (a.hf) {
+                if constexpr (HF) {
                     bool th;
                     ground_at(a, cw.x, cw.y, n, th);
                     support(n);
@@ -590,7 +590,7 @@ template <class M, int EPB> __global__ __launch_bounds__(EPB * M::LPE) void step
                     if (k >= nr) break;
                     const int ro = PL::ROW + (rb + k) * 8;
                     float phi = pts[k].z;
-                    if (a.hf) {   // separation along the normal of the point's own triangle
+                    if constexpr (HF) {   // separation along the normal of the point's own triangle
                         V3 nk;
                         bool th;
                         const float gz = ground_at(a, pts[k].x, pts[k].y, nk, th);
