@@ -56,3 +56,38 @@ def test_gpu_walk_step_matches_oracle_along_1000_steps():
     print(err)
     assert err["obs"] < 1e-3 and err["rew"] < 1e-3, err
     assert err["reset_equal"] and err["timeout_equal"], err
+
+
+def test_gpu_walk_8192_envs_step_matches_oracle():
+    """BASELINE config 4's per-GPU batch (8192 envs): teacher-forced steps of
+    every env against the oracle env (the partition a rank of the 8-GPU run
+    owns is this same batch with its own seed)."""
+    _cuda()
+    from tests.gpu_harness import walk_forced
+    err = walk_forced(num_envs=8192, steps=8, seed=11)
+    print(err)
+    assert err["obs"] < 1e-3 and err["rew"] < 1e-3, err
+    assert err["reset_equal"] and err["timeout_equal"], err
+
+
+def test_gpu_walk_dr_16384_envs():
+    """BASELINE config 5's per-GPU batch: ThormangWalkDR at 16384 envs with
+    mass / friction / push randomisation live; the pushes path is checked
+    step-by-step against the oracle env (teacher-forced), then the full DR
+    env runs 150 steps."""
+    _cuda()
+    from tests.gpu_harness import walk_forced
+    err = walk_forced(num_envs=16384, steps=4, seed=12, task="ThormangWalkDR")
+    print(err)
+    assert err["obs"] < 2e-3 and err["rew"] < 2e-3, err
+    assert err["reset_equal"], err
+    import thormang_isaacgym_amd as tia
+    n = 16384
+    env = tia.make(seed=2, task="ThormangWalkDR", num_envs=n, sim_device="cuda:0", rl_device="cuda:0")
+    g = torch.Generator(device="cuda:0").manual_seed(4)
+    resets = 0
+    for _ in range(150):
+        obs, rew, reset, extras = env.step(torch.rand(n, 33, device="cuda:0", generator=g) * 2 - 1)
+        resets += int(reset.sum())
+    assert torch.isfinite(obs["obs"]).all() and torch.isfinite(rew).all() and torch.isfinite(env.root_tensor).all()
+    assert resets > 0
