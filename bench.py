@@ -88,10 +88,16 @@ def committed_traffic(task_name: str, num_envs: int):
     return None, None
 
 
-def cpu_baseline(task_name: str, num_envs: int, threads: int):
+def cpu_baseline(task_name: str, num_envs: int, threads: int, terrain_env=None):
     from tests.gpu_harness import NumpyDraws, OracleGogoro, OracleWalk, parity_cfg, walk_cfg
+    if terrain_env is not None:   # same heightfield and spawn heights as the GPU env
+        from tests.oracle_lib import set_heightfield
+        t = terrain_env.terrain
+        o = -float(terrain_env._terrain_start_mid)
+        set_heightfield(t.heightsamples.cpu().numpy(), t.V_scale, t.H_scale, o, o, friction=0.98)
     if task_name == "Gogoro":
-        env = OracleGogoro(parity_cfg(num_envs), NumpyDraws(0), threads=threads)
+        spawn = None if terrain_env is None else terrain_env.root_reset_tensor[:, 2].cpu().numpy()
+        env = OracleGogoro(parity_cfg(num_envs), NumpyDraws(0), threads=threads, spawn_z=spawn)
         shape = (num_envs,)
     else:
         env = OracleWalk(walk_cfg(num_envs, task_name), NumpyDraws(0), threads=threads)
@@ -116,7 +122,11 @@ def main():
     ap.add_argument("--task", default="ThormangWalk")
     ap.add_argument("--num-envs", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--terrain", action="store_true",
+                    help="Gogoro only: the reference's USE_TERAIN Perlin terrain (gogoro_new.py:26)")
     args = ap.parse_args()
+    if args.terrain and args.task != "Gogoro":
+        ap.error("--terrain applies to the Gogoro task (the reference has terrain only there)")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -130,6 +140,10 @@ def main():
     import thormang_isaacgym_amd as tia
     from thormang_isaacgym_amd.cfg import load_task_cfg
     cfg = load_task_cfg(args.task, num_envs=args.num_envs, sim_device=dev)
+    if args.terrain:
+        from thormang_isaacgym_amd.tasks import gogoro as gogoro_task
+        gogoro_task.USE_TERAIN = True
+        torch.manual_seed(42 + rank)        # the terrain draws from the CPU generator, as the reference
     env = tia.make(seed=42 + rank, task=args.task, num_envs=args.num_envs, sim_device=dev, rl_device=dev, cfg=cfg)
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     N = args.num_envs
@@ -173,7 +187,8 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (actions U(-1,1), seed 1234+rank; model compiled from the reference URDF)",
-        "config": {"workload": f"{args.task} {N} envs/GPU, flat ground, dt {sim_cfg['dt']} s x "
+        "config": {"workload": f"{args.task} {N} envs/GPU, {'Perlin terrain' if args.terrain else 'flat ground'}, "
+                               f"dt {sim_cfg['dt']} s x "
                                f"{sim_cfg.get('substeps', 2)} substeps ({1.0 / sim_cfg['dt']:.1f} Hz control)",
                    "num_envs_per_gpu": N, "parallelism": f"env-dp{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -184,7 +199,8 @@ def main():
     }
     if not args.no_cpu_baseline and world == 1:
         try:
-            out["cpu_baseline"] = cpu_baseline(args.task, N, threads=min(16, os.cpu_count() or 1))
+            out["cpu_baseline"] = cpu_baseline(args.task, N, threads=min(16, os.cpu_count() or 1),
+                                               terrain_env=env if args.terrain else None)
         except Exception as exc:  # baseline is reported, never the measured value
             out["cpu_baseline"] = {"value": None, "error": repr(exc)}
     print(json.dumps(out), flush=True)

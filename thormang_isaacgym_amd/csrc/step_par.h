@@ -20,7 +20,10 @@
 //   Delassus columns                            -- one column per lane, the
 //          impulse's up-walk kept in registers (path-restricted: only the
 //          ancestors of the contact group and the root->contact-group paths)
-//   PGS                                         -- lane 0 of the env
+//   PGS                                         -- all LPE lanes: W columns and
+//          the multipliers in registers, row sums by DPP reduction
+//   terrain (HF instantiation)                  -- ground_at: heightfield
+//          trimesh height/normal under each shape, rows along that normal
 // The root (group 0) quantities that every lane needs (pose, base velocity,
 // root LDL factor) are computed redundantly in all lanes of the env.
 #pragma once
