@@ -15,9 +15,9 @@ namespace tg {
 __device__ __forceinline__ float clampw(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
 __global__ __launch_bounds__(256) void walk_pre_kernel(tg_walk_params p, tg_walk_buffers b, const float *actions) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int D = p.num_dof;
-    if (t >= (size_t)p.num_envs * D) return;
+    const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;   // num_envs * num_dof < 2^32
+    const unsigned D = (unsigned)p.num_dof;
+    if (t >= (unsigned)p.num_envs * D) return;
     const int d = (int)(t % D);
     float a = clampw(actions[t], -p.clip_actions, p.clip_actions);
     b.actions[t] = a;
