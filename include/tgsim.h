@@ -184,6 +184,13 @@ int tg_apply_body_forces(tg_sim *sim, const float *wrench);
 int tg_set_heightfield(tg_sim *sim, const float *heights, int32_t rows, int32_t cols, float horizontal_scale,
                        float vertical_scale, float origin_x, float origin_y, float friction);
 int tg_simulate(tg_sim *sim);
+/* refresh_rigid_body_state_tensor on the tensor from acquire_rigid_body_state_tensor
+ * (IsaacGym tensor API; SURVEY §8b lists it on the boundary, the reference
+ * tasks do not read it): out [N, L, 13] device, caller-owned, links in model
+ * order (model.links): world origin position (3), orientation quat xyzw (4),
+ * linear velocity of the link's centre of mass (3, the root-state convention),
+ * angular velocity (3); from the current root and dof state, stream-ordered. */
+int tg_rigid_body_states(tg_sim *sim, float *out);
 int tg_sync(tg_sim *sim);
 const char *tg_last_error(void);
 uint64_t tg_compiled_model_hashes(uint64_t *out, int32_t cap); /* returns count */

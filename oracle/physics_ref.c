@@ -960,3 +960,90 @@ void oracle_physics_step(const tg_model_desc *m, const tg_sim_params *sp, int n,
                                 gravity);
     }
 }
+
+/* World state of every link (tg_rigid_body_states): root link from the root
+ * state (its linear velocity is the root link's com velocity), then every
+ * link from its parent in model order: R_l = R_p Ro Rj(q), p_l = p_p + R_p (to
+ * + q s); w_l = w_p + qd a_w (revolute); v_l(origin) = v_p + w_p x (p_l - p_p)
+ * + qd a_w (prismatic), a_w = R_p Ro a.  out[e][l] = (p, quat xyzw, com
+ * velocity, w).  Test infrastructure (fp64). */
+static void m3_to_quat_d(const M3 R, real *q) {
+    real tr = R[0] + R[4] + R[8];
+    if (tr > 0) {
+        real s = 0.5 / sqrt(tr + 1);
+        q[3] = 0.25 / s; q[0] = (R[7] - R[5]) * s; q[1] = (R[2] - R[6]) * s; q[2] = (R[3] - R[1]) * s;
+    } else if (R[0] > R[4] && R[0] > R[8]) {
+        real s = 2 * sqrt(1 + R[0] - R[4] - R[8]);
+        q[3] = (R[7] - R[5]) / s; q[0] = 0.25 * s; q[1] = (R[1] + R[3]) / s; q[2] = (R[2] + R[6]) / s;
+    } else if (R[4] > R[8]) {
+        real s = 2 * sqrt(1 + R[4] - R[0] - R[8]);
+        q[3] = (R[2] - R[6]) / s; q[0] = (R[1] + R[3]) / s; q[1] = 0.25 * s; q[2] = (R[5] + R[7]) / s;
+    } else {
+        real s = 2 * sqrt(1 + R[8] - R[0] - R[4]);
+        q[3] = (R[3] - R[1]) / s; q[0] = (R[2] + R[6]) / s; q[1] = (R[5] + R[7]) / s; q[2] = 0.25 * s;
+    }
+}
+
+void oracle_rigid_body_states(const tg_model_desc *m, int n, const float *root, const float *dof, float *out) {
+    int L = m->num_links, D = m->num_dofs;
+    for (int e = 0; e < n; ++e) {
+        M3 R[MAXL];
+        V3 P[MAXL], W[MAXL], V[MAXL];
+        const float *r = root + 13L * e;
+        const float *q = dof + 2L * e * D;
+        for (int l = 0; l < L; ++l) {
+            int p = m->link_parent[l];
+            const float *in = m->link_inertia + 10 * l;
+            V3 c = {in[1], in[2], in[3]}, Rc;
+            if (p < 0) {
+                real qq[4] = {r[3], r[4], r[5], r[6]};
+                real nq = sqrt(qq[0] * qq[0] + qq[1] * qq[1] + qq[2] * qq[2] + qq[3] * qq[3]);
+                for (int k = 0; k < 4; ++k) qq[k] /= nq;
+                quat_to_m3(qq, R[l]);
+                for (int k = 0; k < 3; ++k) { P[l][k] = r[k]; W[l][k] = r[10 + k]; }
+                m3_v(R[l], c, Rc);
+                V3 wxc;
+                cross3(W[l], Rc, wxc);
+                for (int k = 0; k < 3; ++k) V[l][k] = r[7 + k] - wxc[k];
+                continue;
+            }
+            const float *o = m->link_origin + 12 * l;
+            M3 Ro, Rj;
+            V3 to = {o[9], o[10], o[11]}, ax = {m->link_axis[3 * l], m->link_axis[3 * l + 1], m->link_axis[3 * l + 2]};
+            for (int k = 0; k < 9; ++k) Ro[k] = o[k];
+            int d = m->link_dof[l];
+            real qq = d >= 0 ? q[2 * d] : 0.0, qd = d >= 0 ? q[2 * d + 1] : 0.0;
+            V3 s, aw;
+            m3_v(Ro, ax, s);
+            m3_v(R[p], s, aw);
+            memcpy(W[l], W[p], sizeof(V3));
+            if (m->link_jtype[l] == TG_JOINT_REVOLUTE) {
+                axis_angle(ax, qq, Rj);
+                m3_mul(Ro, Rj, Ro);
+                for (int k = 0; k < 3; ++k) W[l][k] += qd * aw[k];
+            } else if (m->link_jtype[l] == TG_JOINT_PRISMATIC) {
+                for (int k = 0; k < 3; ++k) to[k] += qq * s[k];
+            }
+            m3_mul(R[p], Ro, R[l]);
+            V3 t, dp, wxd;
+            m3_v(R[p], to, t);
+            for (int k = 0; k < 3; ++k) { P[l][k] = P[p][k] + t[k]; dp[k] = t[k]; }
+            cross3(W[p], dp, wxd);
+            for (int k = 0; k < 3; ++k) V[l][k] = V[p][k] + wxd[k];
+            if (m->link_jtype[l] == TG_JOINT_PRISMATIC)
+                for (int k = 0; k < 3; ++k) V[l][k] += qd * aw[k];
+        }
+        for (int l = 0; l < L; ++l) {
+            const float *in = m->link_inertia + 10 * l;
+            V3 c = {in[1], in[2], in[3]}, Rc, wxc;
+            m3_v(R[l], c, Rc);
+            cross3(W[l], Rc, wxc);
+            real qo[4];
+            m3_to_quat_d(R[l], qo);
+            float *o = out + (13L * L) * e + 13L * l;
+            for (int k = 0; k < 3; ++k) o[k] = (float)P[l][k];
+            for (int k = 0; k < 4; ++k) o[3 + k] = (float)qo[k];
+            for (int k = 0; k < 3; ++k) { o[7 + k] = (float)(V[l][k] + wxc[k]); o[10 + k] = (float)W[l][k]; }
+        }
+    }
+}

@@ -40,6 +40,7 @@ def lib():
         _lib.oracle_paper_observation.argtypes = [vp, C.c_float, C.c_float, C.c_float, vp]
         _lib.oracle_physics_step.argtypes = [vp, vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_int]
         _lib.oracle_set_heightfield.argtypes = [vp, C.c_int, C.c_int] + [C.c_float] * 5
+        _lib.oracle_rigid_body_states.argtypes = [vp, C.c_int, vp, vp, vp]
     return _lib
 
 
@@ -76,3 +77,12 @@ def set_heightfield(heights, horizontal_scale=1.0, vertical_scale=1.0, origin_x=
     _hf_keep = np.ascontiguousarray(np.asarray(heights, np.float32))
     r, c = _hf_keep.shape
     lib().oracle_set_heightfield(ptr(_hf_keep), r, c, horizontal_scale, vertical_scale, origin_x, origin_y, friction)
+
+
+def rigid_body_states(desc, root, dof):
+    """[N, L, 13] world link states from root [N,13] / dof [N*D,2] (tg_rigid_body_states semantics)."""
+    n = root.shape[0]
+    out = np.zeros((n, desc.model.num_bodies, 13), np.float32)
+    lib().oracle_rigid_body_states(C.byref(desc.desc), n, ptr(np.ascontiguousarray(root, np.float32)),
+                                   ptr(np.ascontiguousarray(dof, np.float32)), ptr(out))
+    return out

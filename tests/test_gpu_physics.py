@@ -105,3 +105,30 @@ def test_gpu_free_fall_exact():
     h = 0.005
     np.testing.assert_allclose(r[:, 9], -9.81 * h * n, rtol=1e-5)
     np.testing.assert_allclose(r[:, 2], 10.0 - 9.81 * h * h * n * (n + 1) / 2, atol=1e-4)
+
+
+@pytest.mark.parametrize("name", ["thormang", "gogoro"])
+def test_gpu_rigid_body_states_match_oracle(name):
+    """refresh_rigid_body_state_tensor (tg_rigid_body_states) vs the oracle's
+    link states on random root / dof states."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs the MI355X")
+    from tests.oracle_lib import rigid_body_states
+    from tests.test_rigid_body_states import random_state
+    from thormang_isaacgym_amd import abi
+    from thormang_isaacgym_amd.sim import Sim, load_model
+    m = load_model(name)
+    n = 256
+    root, dof = random_state(m, n, np.random.default_rng(5))
+    sp = abi.sim_params_from_cfg({"dt": 0.01, "substeps": 1, "gravity": [0, 0, -9.81]}, {}, n)
+    s = Sim(m, sp, n, "cuda:0")
+    s.root_state.copy_(torch.from_numpy(root))
+    s.dof_state.copy_(torch.from_numpy(dof))
+    rb = s.acquire_rigid_body_state_tensor()
+    s.refresh_rigid_body_state_tensor()
+    g = rb.view(n, m.num_bodies, 13).cpu().numpy()
+    o = rigid_body_states(abi.ModelDesc(m), root, dof)
+    sgn = np.sign(np.sum(g[..., 3:7] * o[..., 3:7], axis=-1, keepdims=True))
+    np.testing.assert_allclose(g[..., :3], o[..., :3], atol=3e-5)
+    np.testing.assert_allclose(g[..., 3:7] * sgn, o[..., 3:7], atol=3e-5)
+    np.testing.assert_allclose(g[..., 7:13], o[..., 7:13], atol=2e-4, rtol=1e-4)

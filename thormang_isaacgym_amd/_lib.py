@@ -36,6 +36,7 @@ SIGNATURES = {
     "tg_apply_body_forces": [_VP, _VP],
     "tg_set_heightfield": [_VP, _VP, C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float],
     "tg_simulate": [_VP],
+    "tg_rigid_body_states": [_VP, _VP],
     "tg_sync": [_VP],
     "tg_last_error": [],
     "tg_set_kernel_timing": [_VP, C.c_int32],

@@ -181,6 +181,107 @@ template <class M> __global__ __launch_bounds__(64) void compose_kernel(StepArgs
     if (lane == 0) a.dirty[e] = 0;
 }
 
+// ---------------------------------------------------------------- rigid-body states
+// World state of every link (acquire/refresh_rigid_body_state_tensor): one
+// wavefront per env, links level by level (lane = link): R_l = R_p Ro Rj(q),
+// p_l = p_p + R_p (to + q s), w_l = w_p + qd R_p Ro a (revolute),
+// v_l = v_p + w_p x (p_l - p_p) + qd R_p Ro a (prismatic), v_l at the link
+// origin; out[e][l] = (p_l, quat(R_l) xyzw, v_l + w_l x R_l c_l, w_l).
+// The same function as oracle/physics_ref.c oracle_rigid_body_states.
+__device__ __forceinline__ void m3_to_quat(const M3 &R, float &x, float &y, float &z, float &w) {
+    const float m00 = R.a[0], m11 = R.a[4], m22 = R.a[8], tr = m00 + m11 + m22;
+    if (tr > 0.f) {
+        const float s = 0.5f / sqrtf(tr + 1.f);
+        w = 0.25f / s; x = (R.a[7] - R.a[5]) * s; y = (R.a[2] - R.a[6]) * s; z = (R.a[3] - R.a[1]) * s;
+    } else if (m00 > m11 && m00 > m22) {
+        const float s = 2.f * sqrtf(1.f + m00 - m11 - m22);
+        w = (R.a[7] - R.a[5]) / s; x = 0.25f * s; y = (R.a[1] + R.a[3]) / s; z = (R.a[2] + R.a[6]) / s;
+    } else if (m11 > m22) {
+        const float s = 2.f * sqrtf(1.f + m11 - m00 - m22);
+        w = (R.a[2] - R.a[6]) / s; x = (R.a[1] + R.a[3]) / s; y = 0.25f * s; z = (R.a[5] + R.a[7]) / s;
+    } else {
+        const float s = 2.f * sqrtf(1.f + m22 - m00 - m11);
+        w = (R.a[3] - R.a[1]) / s; x = (R.a[2] + R.a[6]) / s; y = (R.a[5] + R.a[7]) / s; z = 0.25f * s;
+    }
+}
+
+template <class M> __global__ __launch_bounds__(64) void body_state_kernel(const float *root, const float *dof, int n,
+                                                                           float *out) {
+    const int e = blockIdx.x;
+    if (e >= n) return;
+    __shared__ float T[M::NL][18];   // R (9), p (3), w (3), v at the origin (3)
+    const int lane = threadIdx.x;
+    const float *r = root + 13 * (size_t)e;
+    const float *q = dof + 2 * (size_t)e * M::ND;
+    auto wsync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    for (int lev = 0; lev <= M::NLEV; ++lev) {
+        for (int l = lane; l < M::NL; l += 64) {
+            if (M::link_level[l] != lev) continue;
+            M3 R;
+            V3 P, W, V;
+            if (M::link_parent[l] < 0) {
+                float qx = r[3], qy = r[4], qz = r[5], qw = r[6];
+                const float in = rsqrtf(qx * qx + qy * qy + qz * qz + qw * qw);
+                R = quat_to_m3(qx * in, qy * in, qz * in, qw * in);
+                P = v3(r[0], r[1], r[2]);
+                W = v3(r[10], r[11], r[12]);
+                const V3 c = v3(M::link_inertia[l][1], M::link_inertia[l][2], M::link_inertia[l][3]);
+                V = v3(r[7], r[8], r[9]) - cross(W, mul(R, c));   // root state: velocity of the root link's com
+            } else {
+                const int pl = M::link_parent[l];
+                M3 Rp;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) Rp.a[k] = T[pl][k];
+                const V3 Pp = v3(T[pl][9], T[pl][10], T[pl][11]);
+                const V3 Wp = v3(T[pl][12], T[pl][13], T[pl][14]), Vp = v3(T[pl][15], T[pl][16], T[pl][17]);
+                const float *o = M::link_origin[l];
+                M3 Ro{{o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7], o[8]}};
+                V3 to = v3(o[9], o[10], o[11]);
+                const int d = M::link_dof[l];
+                const float qq = d >= 0 ? q[2 * d] : 0.f, qd = d >= 0 ? q[2 * d + 1] : 0.f;
+                const float *ax = M::link_axis[l];
+                const V3 axw = mul(Rp, mul(Ro, v3(ax[0], ax[1], ax[2])));   // joint axis, world
+                W = Wp;
+                if (M::link_jtype[l] == TG_JOINT_REVOLUTE) {
+                    Ro = mul(Ro, rot_axis(ax[0], ax[1], ax[2], qq));
+                    W = W + qd * axw;
+                } else if (M::link_jtype[l] == TG_JOINT_PRISMATIC) {
+                    to = to + qq * mul(Ro, v3(ax[0], ax[1], ax[2]));
+                }
+                R = mul(Rp, Ro);
+                P = Pp + mul(Rp, to);
+                V = Vp + cross(Wp, P - Pp);
+                if (M::link_jtype[l] == TG_JOINT_PRISMATIC) V = V + qd * axw;
+            }
+#pragma unroll
+            for (int k = 0; k < 9; ++k) T[l][k] = R.a[k];
+            T[l][9] = P.x; T[l][10] = P.y; T[l][11] = P.z;
+            T[l][12] = W.x; T[l][13] = W.y; T[l][14] = W.z;
+            T[l][15] = V.x; T[l][16] = V.y; T[l][17] = V.z;
+        }
+        wsync();
+    }
+    for (int l = lane; l < M::NL; l += 64) {
+        M3 R;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) R.a[k] = T[l][k];
+        const V3 W = v3(T[l][12], T[l][13], T[l][14]);
+        const V3 c = v3(M::link_inertia[l][1], M::link_inertia[l][2], M::link_inertia[l][3]);
+        const V3 vc = v3(T[l][15], T[l][16], T[l][17]) + cross(W, mul(R, c));
+        float qx, qy, qz, qw;
+        m3_to_quat(R, qx, qy, qz, qw);
+        float *o = out + ((size_t)e * M::NL + l) * 13;
+        o[0] = T[l][9]; o[1] = T[l][10]; o[2] = T[l][11];
+        o[3] = qx; o[4] = qy; o[5] = qz; o[6] = qw;
+        o[7] = vc.x; o[8] = vc.y; o[9] = vc.z;
+        o[10] = W.x; o[11] = W.y; o[12] = W.z;
+    }
+}
+
 // ---------------------------------------------------------------- contact row layout
 // rows of shape s: shape_nrows[s] normal rows, then friction t1, t2 and torsion
 template <class M> __device__ __forceinline__ constexpr int row_shape(int i) {
@@ -261,6 +362,17 @@ extern "C" int tg_prof_read(unsigned long long *out, int n) {
 
 #define TG_HASH(MODEL) if (n < cap) out[n] = MODEL::hash; ++n;
 #define TG_KC(MODEL) if (hash == MODEL::hash) return MODEL::KC;
+
+#define TG_BODY_STATES(MODEL)                                                                              \
+    if (hash == MODEL::hash) {                                                                             \
+        hipLaunchKernelGGL(body_state_kernel<MODEL>, dim3(n), dim3(64), 0, stream, root, dof, n, out);   \
+        return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;                                           \
+    }
+
+int launch_body_states(uint64_t hash, const float *root, const float *dof, int n, float *out, hipStream_t stream) {
+    TG_FOR_EACH_MODEL(TG_BODY_STATES)
+    return TG_ERR_MODEL;
+}
 
 int compiled_hashes(uint64_t *out, int cap) {
     int n = 0;

@@ -39,6 +39,7 @@ int launch_step(uint64_t hash, const StepArgs &a, hipStream_t stream, hipEvent_t
                 hipEvent_t ev_end = nullptr);
 int launch_compose(uint64_t hash, const StepArgs &a, hipStream_t stream);
 int compiled_hashes(uint64_t *out, int cap);
+int launch_body_states(uint64_t hash, const float *root, const float *dof, int n, float *out, hipStream_t stream);
 int model_kc(uint64_t hash);
 
 int launch_gogoro_pre(const tg_gogoro_params &p, const tg_gogoro_buffers &b, const float *actions,

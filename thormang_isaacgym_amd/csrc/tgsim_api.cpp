@@ -408,6 +408,14 @@ int tg_simulate(tg_sim *s) {
     return TG_OK;
 }
 
+int tg_rigid_body_states(tg_sim *s, float *out) {
+    if (int rc = check_sim(s)) return rc;
+    if (!out) return fail(TG_ERR_ARG, "tg_rigid_body_states: null output");
+    if (int rc = tg::launch_body_states(s->hash, s->root, s->dof, (int)s->N, out, s->stream))
+        return fail(rc, "rigid-body state launch failed");
+    return TG_OK;
+}
+
 int tg_set_kernel_timing(tg_sim *s, int32_t enable) {
     if (int rc = check_sim(s)) return rc;
     s->timing = enable != 0;

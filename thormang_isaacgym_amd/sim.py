@@ -141,6 +141,18 @@ class Sim:
     def simulate(self):
         check(lib().tg_simulate(self._h), "simulate")
 
+    def acquire_rigid_body_state_tensor(self) -> torch.Tensor:
+        """gym.acquire_rigid_body_state_tensor: [N*L, 13] world link states
+        (origin pos, quat xyzw, com linvel, angvel), links in model order;
+        filled by refresh_rigid_body_state_tensor."""
+        if getattr(self, "rigid_body_state", None) is None:
+            self.rigid_body_state = torch.zeros(self.num_envs * self.L, 13, dtype=torch.float32, device=self.device)
+        return self.rigid_body_state
+
+    def refresh_rigid_body_state_tensor(self):
+        rb = self.acquire_rigid_body_state_tensor()
+        check(lib().tg_rigid_body_states(self._h, _ptr(rb)), "refresh_rigid_body_state_tensor")
+
     def sync(self):
         check(lib().tg_sync(self._h), "sync")
 
