@@ -218,9 +218,9 @@ template <class M> __global__ __launch_bounds__(64) void body_state_kernel(const
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
-    for (int lev = 0; lev <= M::NLEV; ++lev) {
+    for (int lev = 0; lev <= M::NDEPTH; ++lev) {
         for (int l = lane; l < M::NL; l += 64) {
-            if (M::link_level[l] != lev) continue;
+            if (M::link_depth[l] != lev) continue;
             M3 R;
             V3 P, W, V;
             if (M::link_parent[l] < 0) {

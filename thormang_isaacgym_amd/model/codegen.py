@@ -123,6 +123,10 @@ def emit(m: Model, cname: str) -> str:
     level = [0] * L
     for l in range(L):                      # parents precede children
         level[l] = 0 if l in groot else level[lpar[l]] + 1
+    # rigid-body states: link depth in the whole tree (world FK level by level)
+    wdepth = [0] * L
+    for l in range(L):
+        wdepth[l] = 0 if lpar[l] < 0 else wdepth[lpar[l]] + 1
     glinks = [[l for l in range(L) if lgrp[l] == g] for g in range(G)]
     maxgl = max(len(x) for x in glinks)
     maxc = max(1, max(len(c) for c in children))
@@ -173,6 +177,8 @@ def emit(m: Model, cname: str) -> str:
         f"  static constexpr int dof_locked[{D}] = {_arr(a['dof_locked'])};",
         f"  static constexpr int NLEV = {max(level)}, MAXGL = {maxgl};",
         f"  static constexpr int link_level[{L}] = {_arr(level)};",
+        f"  static constexpr int NDEPTH = {max(wdepth)};",
+        f"  static constexpr int link_depth[{L}] = {_arr(wdepth)};",
         f"  static constexpr int group_nlinks[{G}] = {_arr([len(x) for x in glinks])};",
         f"  static constexpr int group_links[{G}][{maxgl}] = "
         f"{_arr([_arr(x + [-1] * (maxgl - len(x))) for x in glinks])};",
