@@ -87,6 +87,8 @@ __device__ __forceinline__ void stsi(const LE &s, int o, const SI &I) {
 #pragma unroll
     for (int k = 0; k < 9; ++k) s(o + 6 + k) = I.B[k];
 }
+// scratch float x of the contact phase, laid over the groups' I^A slots
+__device__ __forceinline__ int scr(int x) { return (x / 21) * GF + F_IA + x % 21; }
 __device__ __forceinline__ Xf ldx(const LE &s, int g) { return Xf{ldm3(s, g * GF + F_E), ldv3(s, g * GF + F_R)}; }
 
 // per-group model table in LDS (ints; axis as float bits), built once per block
@@ -213,6 +215,14 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
     using PL = ParLayout<M>;
     constexpr int K = PL::K;
     constexpr int GIW = PL::GIW;
+    // Impulse application by superposition: each Delassus column j leaves its
+    // up-walk joint impulses du_j (path order) and root response a_j in the
+    // I^A slots (dead between pass 2's root solve and the next substep), and
+    // the application becomes u_g = sum_j lam_j du_j, da0 = sum_j lam_j a_j,
+    // then the top-down pass.  Models whose columns do not fit keep the
+    // bottom-up pass.
+    constexpr int SW = M::MAXD + 6;
+    constexpr bool SUPER = K > 0 && K * SW <= M::NG * 21;
     extern __shared__ __attribute__((aligned(16))) float lds_raw[];
     int *tab = reinterpret_cast<int *>(lds_raw + EPB * PL::ES);
     const int *gi = tab + PL::T_GI;
@@ -669,6 +679,14 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
                     }
                 }
                 const SV aj = fix_base ? sv0() : ldl6_solve(rootf, -1.0f * p);
+                if constexpr (SUPER) {
+#pragma unroll
+                    for (int i = 0; i < M::MAXD; ++i)
+                        if (i < lk) s(scr(j * SW + i)) = du[i];
+                    const float av[6] = {aj.w.x, aj.w.y, aj.w.z, aj.v.x, aj.v.y, aj.v.z};
+#pragma unroll
+                    for (int k = 0; k < 6; ++k) s(scr(j * SW + M::MAXD + k)) = av[k];
+                }
                 SV dvc[M::NCG];
 #pragma unroll
                 for (int c = 0; c < M::NCG; ++c) {
@@ -690,9 +708,10 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
             }
             TG_SYNC();
             TG_PROF(5)
-            // impulse accumulators (F_PA slots) cleared by all lanes
-            for (int g = sub; g < M::NG; g += LPE) stsv(s, g * GF + F_PA, sv0());
-            TG_SYNC();
+            if constexpr (!SUPER) {   // impulse accumulators (F_PA slots) cleared by all lanes
+                for (int g = sub; g < M::NG; g += LPE) stsv(s, g * GF + F_PA, sv0());
+                TG_SYNC();
+            }
             // projected Gauss-Seidel with patch friction, all LPE lanes of the env:
             // each lane holds W's columns j = sub + LPE*jj and the full multiplier
             // vector in registers; a row's W*lambda is an 8-lane reduction, so
@@ -769,33 +788,60 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
                 }
             }
             TG_SYNC();
-            if (lead) {
-                // impulses into the contact groups' F_PA slots (p = -f convention)
-                for (int i = 0; i < K; ++i) {
-                    const int g = M::shape_group[row_shape<M>(i)];
-                    stsv(s, g * GF + F_PA, ldsv(s, g * GF + F_PA) + (-1.0f) * rforce(i, s(PL::LAM + i)));
+            SV da0 = sv0();
+            if constexpr (SUPER) {
+                TG_PROF(6)
+                // joint impulses u_g = sum_j lam_j du_j on the contact paths (0 elsewhere),
+                // one contact group at a time (paths may share ancestors)
+                for (int g = sub; g < M::NG; g += LPE) s(g * GF + F_UU) = 0.f;
+                TG_SYNC();
+#pragma unroll
+                for (int c = 0; c < M::NCG; ++c) {
+                    for (int i = sub; i < M::cpath_len[c]; i += LPE) {
+                        float acc = 0.f;
+#pragma unroll
+                        for (int j = 0; j < K; ++j)
+                            if (M::shape_cg[row_shape<M>(j)] == c) acc += s(PL::LAM + j) * s(scr(j * SW + i));
+                        s(cpath[c * M::MAXD + i] * GF + F_UU) += acc;
+                    }
+                    TG_SYNC();
                 }
-            }
-            TG_SYNC();
-            TG_PROF(6)
-            // impulse application: bottom-up gather, root solve, top-down
-#pragma unroll 1
-            for (int t = M::NSTEP - 1; t >= 0; --t) {
-                const int g = sched[t * LPE + sub];
-                if (g > 0) {
-                    const int o = g * GF;
-                    SV p = ldsv(s, o + F_PA);
-                    const int nch = gi[g * GIW + GI_NCH];
-                    for (int c = 0; c < nch; ++c) p = p + ldsv(s, gi[g * GIW + GI_CH + c] * GF + F_PA);
-                    const float u = -dotS(ginfo<M>(gi, g).jt, p);
-                    s(o + F_UU) = u;
-                    const SV pa = p + (u * s(o + F_DINV)) * ldsv(s, o + F_U);
-                    stsv(s, o + F_PA, xTforce(ldx(s, g), pa));
+                if (!fix_base) {
+                    float d6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int j = 0; j < K; ++j) {
+                        const float l = s(PL::LAM + j);
+#pragma unroll
+                        for (int k = 0; k < 6; ++k) d6[k] += l * s(scr(j * SW + M::MAXD + k));
+                    }
+                    da0 = SV{v3(d6[0], d6[1], d6[2]), v3(d6[3], d6[4], d6[5])};
+                }
+            } else {
+                if (lead) {
+                    // impulses into the contact groups' F_PA slots (p = -f convention)
+                    for (int i = 0; i < K; ++i) {
+                        const int g = M::shape_group[row_shape<M>(i)];
+                        stsv(s, g * GF + F_PA, ldsv(s, g * GF + F_PA) + (-1.0f) * rforce(i, s(PL::LAM + i)));
+                    }
                 }
                 TG_SYNC();
-            }
-            SV da0 = sv0();
-            {
+                TG_PROF(6)
+                // impulse application: bottom-up gather, root solve, top-down
+#pragma unroll 1
+                for (int t = M::NSTEP - 1; t >= 0; --t) {
+                    const int g = sched[t * LPE + sub];
+                    if (g > 0) {
+                        const int o = g * GF;
+                        SV p = ldsv(s, o + F_PA);
+                        const int nch = gi[g * GIW + GI_NCH];
+                        for (int c = 0; c < nch; ++c) p = p + ldsv(s, gi[g * GIW + GI_CH + c] * GF + F_PA);
+                        const float u = -dotS(ginfo<M>(gi, g).jt, p);
+                        s(o + F_UU) = u;
+                        const SV pa = p + (u * s(o + F_DINV)) * ldsv(s, o + F_U);
+                        stsv(s, o + F_PA, xTforce(ldx(s, g), pa));
+                    }
+                    TG_SYNC();
+                }
                 SV p0 = ldsv(s, F_PA);
                 for (int c = 0; c < M::nchild[0]; ++c) p0 = p0 + ldsv(s, M::child[0][c] * GF + F_PA);
                 if (!fix_base) da0 = ldl6_solve(rootf, -1.0f * p0);
