@@ -3,6 +3,8 @@
 Needs the profiling build:
     TG_EXTRA_FLAGS=-DTG_SECTION_PROF TG_LIB_NAME=libtgsim_prof.so python thormang_isaacgym_amd/build_ext.py
     TG_LIB_PATH=thormang_isaacgym_amd/libtgsim_prof.so python scripts/section_prof.py
+Add -DTG_CLAMP_COUNT to also count the drive-clamp reruns (ThormangWalk: 0 %,
+Gogoro: 40 % of env-substeps; the counters' atomics then inflate pass 1).
 """
 import ctypes as C
 import os
@@ -31,6 +33,9 @@ def main():
     tot = sum(buf[:len(NAMES)])
     for n, v in zip(NAMES, buf):
         print(f"{n:14s} {v / tot * 100:6.2f} %  {v:14d}")
+    if buf[12]:
+        print(f"drive-clamp rerun: {buf[13] / buf[12] * 100:.1f} % of env-substeps, "
+              f"{buf[15] / max(buf[14], 1) * 100:.1f} % of wavefront-substeps")
 
 
 if __name__ == "__main__":

@@ -345,6 +345,13 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
         SV a0 = sv0();
 #pragma unroll 1
         for (int cp = 0; cp < 2; ++cp) {
+#if defined(TG_SECTION_PROF) && defined(TG_CLAMP_COUNT)
+        // counters (perturb the pass-1 timing, hence a separate switch):
+        // [12] env-substeps, [13] env-substeps with the clamp rerun,
+        // [14] wave-substeps, [15] wave-substeps that rerun
+        if (lead && owner) atomicAdd(&tg_prof_acc[12 + cp], 1ull);
+        if (tid % 64 == 0) atomicAdd(&tg_prof_acc[14 + cp], 1ull);
+#endif
         // ---- pass 1: root, then the schedule forward
         if (lead) {
             const V3 gl = mulT(R, grav);
