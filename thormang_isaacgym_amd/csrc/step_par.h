@@ -106,13 +106,19 @@ template <class M> struct ParLayout {
     static constexpr int CGP = SHP + 2 * M::NSA;     // per contact group: world R (9), p (3)
     static constexpr int CGV = CGP + 12 * M::NCG;    // per contact group: free velocity (6)
     static constexpr int FLG = CGV + 6 * M::NCG;     // a drive exceeded its effort limit
-    static constexpr int TOTAL = FLG + 1;
-    static constexpr int ES = (TOTAL + 3) & ~3;      // env stride (16-byte aligned)
     // per-block ints after the env area
     static constexpr int T_GI = 0;
     static constexpr int T_SCHED = M::NG * GIW;
     static constexpr int T_CPATH = T_SCHED + M::NSTEP * M::LPE;   // [NCG][MAXD]
     static constexpr int T_TOTAL = T_CPATH + M::NCG * M::MAXD;
+    // SEPC (when the LDS has room): pass 2 writes each group's contribution to
+    // its parent (I^a 21 at +0, p^a 6 at +24) and pass 3 its acceleration (+0)
+    // into a separate 32-float block, so pass 1's rigid inertias and bias
+    // forces survive and the drive-clamp rerun starts at pass 2
+    static constexpr int CB = (FLG + 1 + 3) & ~3;
+    static constexpr bool SEPC = ((size_t)M::EPB * (CB + 32 * M::NG) + T_TOTAL) * 4 <= 160 * 1024;
+    static constexpr int TOTAL = SEPC ? CB + 32 * M::NG : FLG + 1;
+    static constexpr int ES = (TOTAL + 3) & ~3;      // env stride (16-byte aligned)
     template <int EPB> static constexpr size_t bytes() { return ((size_t)EPB * ES + T_TOTAL) * 4; }
 };
 
@@ -223,6 +229,10 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
     // bottom-up pass.
     constexpr int SW = M::MAXD + 6;
     constexpr bool SUPER = K > 0 && K * SW <= M::NG * 21;
+    constexpr bool SEPC = PL::SEPC;
+    auto ia_c = [](int g) { return SEPC ? PL::CB + 32 * g : g * GF + F_IA; };        // pass-2 contribution I^a
+    auto pa_c = [](int g) { return SEPC ? PL::CB + 32 * g + 24 : g * GF + F_PA; };   // pass-2 contribution p^a
+    auto ac_s = [](int g) { return SEPC ? PL::CB + 32 * g : g * GF + F_PA; };        // pass-3 acceleration
     extern __shared__ __attribute__((aligned(16))) float lds_raw[];
     int *tab = reinterpret_cast<int *>(lds_raw + EPB * PL::ES);
     const int *gi = tab + PL::T_GI;
@@ -352,7 +362,10 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
         if (lead && owner) atomicAdd(&tg_prof_acc[12 + cp], 1ull);
         if (tid % 64 == 0) atomicAdd(&tg_prof_acc[14 + cp], 1ull);
 #endif
-        // ---- pass 1: root, then the schedule forward
+        // ---- pass 1: root, then the schedule forward (SEPC: not rerun, its
+        // results are intact)
+        int gn;
+        if (!SEPC || cp == 0) {
         if (lead) {
             const V3 gl = mulT(R, grav);
             stsv(s, F_V, v0);
@@ -361,7 +374,7 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
         }
         TG_SYNC();
         float nk[22];
-        int gn = sched[sub];
+        gn = sched[sub];
         if (gn > 0) load_kin(gn, nk);
 #pragma unroll 1
         for (int t = 0; t < M::NSTEP; ++t) {
@@ -402,6 +415,7 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
             }
             TG_SYNC();
         }
+        }   // pass 1
         TG_PROF(1)
         // ---- pass 2: schedule backward, children contributions gathered
         float nd[10];
@@ -423,8 +437,8 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
                 const int nch = gi[g * GIW + GI_NCH];
                 for (int c = 0; c < nch; ++c) {
                     const int ch = gi[g * GIW + GI_CH + c];
-                    si_add(IA, ldsi(s, ch * GF + F_IA));
-                    pA = pA + ldsv(s, ch * GF + F_PA);
+                    si_add(IA, ldsi(s, ia_c(ch)));
+                    pA = pA + ldsv(s, pa_c(ch));
                 }
                 const SV U = colS(G.jt, IA);
                 const float q = s(o + F_Q), qd = s(o + F_QD);
@@ -476,8 +490,8 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
                 const SV cb = crmS(G.jt, ldsv(s, o + F_V), qd);
                 const SV pa = pA + mul(Ia, cb) + (u * Dinv) * U;
                 const Xf X = ldx(s, g);
-                stsi(s, o + F_IA, si_to_parent(Ia, X));     // contribution to the parent
-                stsv(s, o + F_PA, xTforce(X, pa));
+                stsi(s, ia_c(g), si_to_parent(Ia, X));     // contribution to the parent
+                stsv(s, pa_c(g), xTforce(X, pa));
             }
             TG_SYNC();
         }
@@ -486,8 +500,8 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
             SI IA0 = ldsi(s, F_IA);
             SV pA0 = ldsv(s, F_PA);
             for (int c = 0; c < M::nchild[0]; ++c) {
-                si_add(IA0, ldsi(s, M::child[0][c] * GF + F_IA));
-                pA0 = pA0 + ldsv(s, M::child[0][c] * GF + F_PA);
+                si_add(IA0, ldsi(s, ia_c(M::child[0][c])));
+                pA0 = pA0 + ldsv(s, pa_c(M::child[0][c]));
             }
             if (!fix_base) {
                 rootf = ldl6(IA0);
@@ -498,7 +512,7 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
         TG_PROF(2)
         // ---- pass 3: free accelerations (through the F_PA slots) and velocities
         if (lead) {
-            stsv(s, F_PA, a0);
+            stsv(s, ac_s(0), a0);
             s(PL::FLG) = 0.f;
         }
         TG_SYNC();
@@ -510,9 +524,9 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
                 const GInfo G = ginfo<M>(gi, g);
                 const float qd = s(o + F_QD);
                 const SV cb = crmS(G.jt, ldsv(s, o + F_V), qd);
-                const SV ap = xmotion(ldx(s, g), ldsv(s, G.parent * GF + F_PA)) + cb;
+                const SV ap = xmotion(ldx(s, g), ldsv(s, ac_s(G.parent))) + cb;
                 const float qdd = (s(o + F_UU) - dot(ldsv(s, o + F_U), ap)) * s(o + F_DINV);
-                stsv(s, o + F_PA, addS(G.jt, ap, qdd));
+                stsv(s, ac_s(g), addS(G.jt, ap, qdd));
                 s(o + F_QDS) = qd + h * qdd;
                 if (cp == 0) {
                     s(o + F_UU) = qdd;
