@@ -33,6 +33,14 @@ def main():
     tot = sum(buf[:len(NAMES)])
     for n, v in zip(NAMES, buf):
         print(f"{n:14s} {v / tot * 100:6.2f} %  {v:14d}")
+    L.tg_cprof_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    cb = (C.c_ulonglong * 8)()
+    L.tg_cprof_read(cb, 8)
+    ctot = sum(cb[:4])
+    if ctot:
+        print("compose_kernel (cycles summed over composed envs):")
+        for n, v in zip(["loads + local joint", "level FK + link mass", "group sums + cache rows", "shapes"], cb):
+            print(f"  {n:26s} {v / ctot * 100:6.2f} %  {v:14d}")
     if buf[12]:
         print(f"drive-clamp rerun: {buf[13] / buf[12] * 100:.1f} % of env-substeps, "
               f"{buf[15] / max(buf[14], 1) * 100:.1f} % of wavefront-substeps")

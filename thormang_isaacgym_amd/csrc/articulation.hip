@@ -46,12 +46,44 @@ __device__ __forceinline__ float prop(const StepArgs &a, int f, int e, int d) {
 // their group-root frame level by level (lane = link), per-link mass terms in
 // parallel, then lane g sums group g's links in link order (deterministic, the
 // order of oracle/physics_ref.c) and writes the group's cache rows.
+#ifdef TG_SECTION_PROF
+__device__ unsigned long long tg_cprof_acc[8];   // compose sections, lane 0 of every composed env
+#define TG_CPROF_INIT unsigned long long tg_c0 = clock64();
+#define TG_CPROF(k)                                                              \
+    {                                                                            \
+        const unsigned long long t1 = clock64();                                \
+        if (threadIdx.x == 0) atomicAdd(&tg_cprof_acc[k], t1 - tg_c0);           \
+        tg_c0 = t1;                                                              \
+    }
+#else
+#define TG_CPROF_INIT
+#define TG_CPROF(k)
+#endif
+
+// groups with more links than this are summed by wave reductions (lane = link)
+constexpr int COMPOSE_SERIAL_MAX = 8;
+template <class M> constexpr int max_small_group() {
+    int m = 0;
+    for (int g = 0; g < M::NG; ++g)
+        if (M::group_nlinks[g] <= COMPOSE_SERIAL_MAX && M::group_nlinks[g] > m) m = M::group_nlinks[g];
+    return m;
+}
+template <int NV> __device__ __forceinline__ void wave_sum_n(float *v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[k] += __shfl_xor(v[k], m, 64);
+}
+
 template <class M> __global__ __launch_bounds__(64) void compose_kernel(StepArgs a) {
     const int e = blockIdx.x;
     if (e >= a.N || !a.dirty[e]) return;
+    TG_CPROF_INIT
     using CL = CompLayout<M>;
+    static_assert(M::NL <= 64 && M::NG <= 64 && M::NS <= 64, "compose: one lane per link / group / shape");
     __shared__ float T[M::NL][12];    // link pose in its group-root frame: R (9), p (3)
-    __shared__ float LM[M::NL][10];   // link mass, com (group frame), inertia about com (group axes, 6)
+    __shared__ float LM[M::NL + 1][10];   // link mass, com (group frame), inertia about com (group axes, 6); row NL = 0
+    __shared__ int GL[M::NG][M::MAXGL];   // group links, padded with NL (the zero row) so the sums run branch-free
     const int lane = threadIdx.x;
     auto wsync = [] {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -63,27 +95,79 @@ template <class M> __global__ __launch_bounds__(64) void compose_kernel(StepArgs
         for (int k = 0; k < 9; ++k) R.a[k] = T[l][k];
         P = v3(T[l][9], T[l][10], T[l][11]);
     };
-    for (int lev = 0; lev <= M::NLEV; ++lev) {
-        for (int l = lane; l < M::NL; l += 64) {
-            if (M::link_level[l] != lev) continue;
-            M3 R = eye3();
-            V3 P = v3(0, 0, 0);
-            if (lev > 0) {
-                const float *o = M::link_origin[l];
-                M3 Ro{{o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7], o[8]}};
-                V3 to = v3(o[9], o[10], o[11]);
-                const int d = M::link_dof[l];
-                if (d >= 0) {
-                    const float q = 0.5f * (prop(a, TG_PROP_LOWER, e, d) + prop(a, TG_PROP_UPPER, e, d));
-                    const float *ax = M::link_axis[l];
-                    if (M::link_jtype[l] == TG_JOINT_REVOLUTE) Ro = mul(Ro, rot_axis(ax[0], ax[1], ax[2], q));
-                    else if (M::link_jtype[l] == TG_JOINT_PRISMATIC) to = to + q * mul(Ro, v3(ax[0], ax[1], ax[2]));
-                }
+    auto ld9 = [](const float *o) { return M3{{o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7], o[8]}}; };
+    // ---- every model constant and per-env input this lane needs, loaded up
+    // front as one batch (the level loop below then runs on LDS only while
+    // the group / shape loads are still in flight)
+    for (int i = lane; i < M::NG * M::MAXGL; i += 64) {
+        const int k = M::group_links[i / M::MAXGL][i % M::MAXGL];
+        GL[i / M::MAXGL][i % M::MAXGL] = k < 0 ? M::NL : k;
+    }
+    if (lane < 10) LM[M::NL][lane] = 0.f;
+    const int l = lane;                      // lane = link
+    const bool lact = l < M::NL;
+    M3 Rl = eye3();
+    V3 tl = v3(0, 0, 0);
+    int lev = -1, par = 0;
+    float msc = 1.f, lin[10];
+    if (lact) {
+        lev = M::link_level[l];
+        par = M::link_parent[l];
+#pragma unroll
+        for (int k = 0; k < 10; ++k) lin[k] = M::link_inertia[l][k];
+        if (lev > 0) {
+            const float *o = M::link_origin[l];
+            Rl = ld9(o);
+            tl = v3(o[9], o[10], o[11]);
+            const int d = M::link_dof[l];
+            if (d >= 0) {
+                const float q = 0.5f * (prop(a, TG_PROP_LOWER, e, d) + prop(a, TG_PROP_UPPER, e, d));
+                const float *ax = M::link_axis[l];
+                if (M::link_jtype[l] == TG_JOINT_REVOLUTE) Rl = mul(Rl, rot_axis(ax[0], ax[1], ax[2], q));
+                else if (M::link_jtype[l] == TG_JOINT_PRISMATIC) tl = tl + q * mul(Rl, v3(ax[0], ax[1], ax[2]));
+            }
+        }
+        if (a.mass_scale) msc = a.mass_scale[(size_t)e * M::NL + l];
+    }
+    const int g = lane;                      // lane = group
+    const bool gact = g < M::NG;
+    int gnl = 0, gpl = 0;
+    M3 Qg = eye3(), Qp = eye3(), Rgo = eye3();
+    V3 tgo = v3(0, 0, 0);
+    if (gact) {
+        gnl = M::group_nlinks[g];
+        Qg = ld9(M::gq[g]);
+        if (g > 0) {
+            Qp = ld9(M::gq[M::parent[g]]);
+            const int r = M::group_root[g];
+            gpl = M::link_parent[r];
+            Rgo = ld9(M::link_origin[r]);
+            tgo = v3(M::link_origin[r][9], M::link_origin[r][10], M::link_origin[r][11]);
+        }
+    }
+    const int sh = lane;                     // lane = shape
+    const bool sact = sh < M::NS;
+    int sl = 0;
+    M3 Qs = eye3(), Rso = eye3();
+    V3 tso = v3(0, 0, 0);
+    if (sact) {
+        sl = M::shape_link[sh];
+        Qs = ld9(M::gq[M::shape_group[sh]]);
+        Rso = ld9(M::shape_pose[sh]);
+        tso = v3(M::shape_pose[sh][9], M::shape_pose[sh][10], M::shape_pose[sh][11]);
+    }
+    TG_CPROF(0)
+    // ---- link poses in their group-root frame, level by level (LDS only)
+    M3 R = eye3();
+    V3 P = v3(0, 0, 0);
+    for (int lv = 0; lv <= M::NLEV; ++lv) {
+        if (lev == lv) {
+            if (lv > 0) {
                 M3 Rp;
                 V3 Pp;
-                ldT(M::link_parent[l], Rp, Pp);
-                R = mul(Rp, Ro);
-                P = Pp + mul(Rp, to);
+                ldT(par, Rp, Pp);
+                R = mul(Rp, Rl);
+                P = Pp + mul(Rp, tl);
             }
 #pragma unroll
             for (int k = 0; k < 9; ++k) T[l][k] = R.a[k];
@@ -91,55 +175,93 @@ template <class M> __global__ __launch_bounds__(64) void compose_kernel(StepArgs
         }
         wsync();
     }
-    for (int l = lane; l < M::NL; l += 64) {
-        M3 R;
-        V3 P;
-        ldT(l, R, P);
-        const float s = a.mass_scale ? a.mass_scale[(size_t)e * M::NL + l] : 1.0f;
-        const float *in = M::link_inertia[l];
-        const V3 cg = mul(R, v3(in[1], in[2], in[3])) + P;
-        const M3 Il{{in[4] * s, in[7] * s, in[8] * s, in[7] * s, in[5] * s, in[9] * s, in[8] * s, in[9] * s, in[6] * s}};
+    if (lact) {   // per-link mass terms
+        const float s = msc;
+        const V3 cg = mul(R, v3(lin[1], lin[2], lin[3])) + P;
+        const M3 Il{{lin[4] * s, lin[7] * s, lin[8] * s, lin[7] * s, lin[5] * s, lin[9] * s, lin[8] * s, lin[9] * s,
+                     lin[6] * s}};
         const M3 RI = mul(mul(R, Il), transpose(R));
-        LM[l][0] = in[0] * s;
+        LM[l][0] = lin[0] * s;
         LM[l][1] = cg.x; LM[l][2] = cg.y; LM[l][3] = cg.z;
         LM[l][4] = RI.a[0]; LM[l][5] = RI.a[4]; LM[l][6] = RI.a[8];
         LM[l][7] = RI.a[1]; LM[l][8] = RI.a[2]; LM[l][9] = RI.a[5];
     }
     wsync();
+    TG_CPROF(1)
+    // ---- group sums in link order (deterministic, the order of
+    // oracle/physics_ref.c), written to the cache in joint-aligned group
+    // frames (axis e_z, codegen gq): v' = Q^T v, I' = Q^T I Q, placements
+    // R' = Q_p^T R Q_g, t' = Q_p^T t
     float *c = a.comp;
     const size_t N = a.N;
-    // the cache is written in joint-aligned group frames (axis e_z, codegen gq):
-    // v_new = Q^T v_old, I_new = Q^T I Q, placements R' = Q_p^T R Q_g, t' = Q_p^T t
-    auto gq = [](int g) {
-        M3 Q;
+    // large groups (the scooter's root group holds the locked rider: 55 links)
+    // by wave reductions over lane = link, in tree order; the others by their
+    // own lane in link order
+    float bm = 0.f, bI[6] = {0, 0, 0, 0, 0, 0};
+    V3 bc = v3(0, 0, 0);
 #pragma unroll
-        for (int k = 0; k < 9; ++k) Q.a[k] = M::gq[g][k];
-        return Q;
-    };
-    for (int g = lane; g < M::NG; g += 64) {
-        const int nl = M::group_nlinks[g];
+    for (int gb = 0; gb < M::NG; ++gb) {
+        if constexpr (M::MAXGL > COMPOSE_SERIAL_MAX) {
+            if (M::group_nlinks[gb] <= COMPOSE_SERIAL_MAX) continue;
+            const bool mine = lact && M::link_group[l] == gb;
+            float v4[4] = {0.f, 0.f, 0.f, 0.f};
+            if (mine) { v4[0] = LM[l][0]; v4[1] = LM[l][0] * LM[l][1]; v4[2] = LM[l][0] * LM[l][2]; v4[3] = LM[l][0] * LM[l][3]; }
+            wave_sum_n<4>(v4);
+            const float im = v4[0] > 0.f ? 1.0f / v4[0] : 0.f;
+            const V3 gcb = v3(v4[1] * im, v4[2] * im, v4[3] * im);
+            float v6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            if (mine) {
+                const float ml = LM[l][0];
+                const V3 dd = v3(LM[l][1], LM[l][2], LM[l][3]) - gcb;
+                const float d2 = dot(dd, dd);
+                v6[0] = LM[l][4] + ml * (d2 - dd.x * dd.x);
+                v6[1] = LM[l][5] + ml * (d2 - dd.y * dd.y);
+                v6[2] = LM[l][6] + ml * (d2 - dd.z * dd.z);
+                v6[3] = LM[l][7] - ml * dd.x * dd.y;
+                v6[4] = LM[l][8] - ml * dd.x * dd.z;
+                v6[5] = LM[l][9] - ml * dd.y * dd.z;
+            }
+            wave_sum_n<6>(v6);
+            if (lane == gb) {
+                bm = v4[0];
+                bc = gcb;
+#pragma unroll
+                for (int k = 0; k < 6; ++k) bI[k] = v6[k];
+            }
+        }
+    }
+    if (gact) {
         float gm = 0.f;
         V3 gc = v3(0, 0, 0);
-        for (int i = 0; i < nl; ++i) {
-            const int l = M::group_links[g][i];
-            gm += LM[l][0];
-            gc = gc + LM[l][0] * v3(LM[l][1], LM[l][2], LM[l][3]);
-        }
-        gc = (gm > 0.f ? 1.0f / gm : 0.f) * gc;
         float gI[6] = {0, 0, 0, 0, 0, 0};
-        for (int i = 0; i < nl; ++i) {
-            const int l = M::group_links[g][i];
-            const float ml = LM[l][0];
-            const V3 dd = v3(LM[l][1], LM[l][2], LM[l][3]) - gc;
-            const float d2 = dot(dd, dd);
-            gI[0] += LM[l][4] + ml * (d2 - dd.x * dd.x);
-            gI[1] += LM[l][5] + ml * (d2 - dd.y * dd.y);
-            gI[2] += LM[l][6] + ml * (d2 - dd.z * dd.z);
-            gI[3] += LM[l][7] - ml * dd.x * dd.y;
-            gI[4] += LM[l][8] - ml * dd.x * dd.z;
-            gI[5] += LM[l][9] - ml * dd.y * dd.z;
+        constexpr int SM = max_small_group<M>();
+        if (gnl > COMPOSE_SERIAL_MAX) {
+            gm = bm;
+            gc = bc;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) gI[k] = bI[k];
+        } else {
+#pragma unroll
+            for (int i = 0; i < SM; ++i) {   // unrolled and branch-free (padding = the zero row)
+                const int k = GL[g][i];
+                gm += LM[k][0];
+                gc = gc + LM[k][0] * v3(LM[k][1], LM[k][2], LM[k][3]);
+            }
+            gc = (gm > 0.f ? 1.0f / gm : 0.f) * gc;
+#pragma unroll
+            for (int i = 0; i < SM; ++i) {
+                const int k = GL[g][i];
+                const float ml = LM[k][0];
+                const V3 dd = v3(LM[k][1], LM[k][2], LM[k][3]) - gc;
+                const float d2 = dot(dd, dd);
+                gI[0] += LM[k][4] + ml * (d2 - dd.x * dd.x);
+                gI[1] += LM[k][5] + ml * (d2 - dd.y * dd.y);
+                gI[2] += LM[k][6] + ml * (d2 - dd.z * dd.z);
+                gI[3] += LM[k][7] - ml * dd.x * dd.y;
+                gI[4] += LM[k][8] - ml * dd.x * dd.z;
+                gI[5] += LM[k][9] - ml * dd.y * dd.z;
+            }
         }
-        const M3 Qg = gq(g);
         const V3 gcq = mulT(Qg, gc);
         float gIq[6];
         sym_from(gIq, mul(mul(transpose(Qg), sym_to(gI)), Qg));
@@ -149,36 +271,31 @@ template <class M> __global__ __launch_bounds__(64) void compose_kernel(StepArgs
 #pragma unroll
         for (int k = 0; k < 6; ++k) ci[(4 + k) * N] = gIq[k];
         if (g > 0) {
-            const int r = M::group_root[g];
-            const float *o = M::link_origin[r];
-            const M3 Ro{{o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7], o[8]}};
             M3 Rp;
             V3 Pp;
-            ldT(M::link_parent[r], Rp, Pp);
-            const M3 Qp = gq(M::parent[g]);
-            const M3 R = mul(mul(transpose(Qp), mul(Rp, Ro)), Qg);
-            const V3 t = mulT(Qp, Pp + mul(Rp, v3(o[9], o[10], o[11])));
+            ldT(gpl, Rp, Pp);
+            const M3 Rx = mul(mul(transpose(Qp), mul(Rp, Rgo)), Qg);
+            const V3 t = mulT(Qp, Pp + mul(Rp, tgo));
             float *cx = c + CL::xtree(g) * N + e;
 #pragma unroll
-            for (int k = 0; k < 9; ++k) cx[k * N] = R.a[k];
+            for (int k = 0; k < 9; ++k) cx[k * N] = Rx.a[k];
             cx[9 * N] = t.x; cx[10 * N] = t.y; cx[11 * N] = t.z;
         }
     }
-    for (int sh = lane; sh < M::NS; sh += 64) {
-        const float *o = M::shape_pose[sh];
-        const M3 Ro{{o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7], o[8]}};
-        M3 Rl;
-        V3 Pl;
-        ldT(M::shape_link[sh], Rl, Pl);
-        const M3 Qg = gq(M::shape_group[sh]);
-        const M3 R = mul(transpose(Qg), mul(Rl, Ro));
-        const V3 t = mulT(Qg, Pl + mul(Rl, v3(o[9], o[10], o[11])));
+    TG_CPROF(2)
+    if (sact) {   // shape poses in their group frame
+        M3 Rsl;
+        V3 Psl;
+        ldT(sl, Rsl, Psl);
+        const M3 Rx = mul(transpose(Qs), mul(Rsl, Rso));
+        const V3 t = mulT(Qs, Psl + mul(Rsl, tso));
         float *cs = c + CL::shape(sh) * N + e;
 #pragma unroll
-        for (int k = 0; k < 9; ++k) cs[k * N] = R.a[k];
+        for (int k = 0; k < 9; ++k) cs[k * N] = Rx.a[k];
         cs[9 * N] = t.x; cs[10 * N] = t.y; cs[11 * N] = t.z;
     }
     if (lane == 0) a.dirty[e] = 0;
+    TG_CPROF(3)
 }
 
 // ---------------------------------------------------------------- rigid-body states
@@ -353,6 +470,11 @@ int launch_compose(uint64_t hash, const StepArgs &a, hipStream_t stream) {
 }
 
 #ifdef TG_SECTION_PROF
+extern "C" int tg_cprof_read(unsigned long long *out, int n) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tg_cprof_acc), sizeof(unsigned long long) * (n < 8 ? n : 8)) != hipSuccess)
+        return -1;
+    return 0;
+}
 extern "C" int tg_prof_read(unsigned long long *out, int n) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tg_prof_acc), sizeof(unsigned long long) * (n < 16 ? n : 16)) != hipSuccess)
         return -1;
