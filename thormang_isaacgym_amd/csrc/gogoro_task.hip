@@ -99,7 +99,8 @@ __device__ void reset_env(const tg_gogoro_params &p, const tg_gogoro_buffers &b,
 #pragma unroll
     for (int k = 7; k < 13; ++k) root[k] = 0.0f;
     float *dof = b.dof_state + 2 * (size_t)e * D;
-    for (int d = 0; d < D; ++d) {
+#pragma unroll 8
+    for (int d = 0; d < D; ++d) {   // unrolled: 8 pose loads in flight instead of one per store
         dof[2 * d] = b.thormang_pose[d];
         dof[2 * d + 1] = 0.0f;
     }
