@@ -52,7 +52,7 @@ __device__ unsigned long long tg_cprof_acc[8];   // compose sections, lane 0 of 
 #define TG_CPROF(k)                                                              \
     {                                                                            \
         const unsigned long long t1 = clock64();                                \
-        if (threadIdx.x == 0) atomicAdd(&tg_cprof_acc[k], t1 - tg_c0);           \
+        if (threadIdx.x % 64 == 0) atomicAdd(&tg_cprof_acc[k], t1 - tg_c0);      \
         tg_c0 = t1;                                                              \
     }
 #else
@@ -75,16 +75,24 @@ template <int NV> __device__ __forceinline__ void wave_sum_n(float *v) {
         for (int k = 0; k < NV; ++k) v[k] += __shfl_xor(v[k], m, 64);
 }
 
-template <class M> __global__ __launch_bounds__(64) void compose_kernel(StepArgs a) {
-    const int e = blockIdx.x;
+// COMPOSE_WPB wavefronts per workgroup, one env each: a launch over all envs
+// is N / COMPOSE_WPB workgroups (most waves exit at once), not N
+constexpr int COMPOSE_WPB = 8;
+
+template <class M> __global__ __launch_bounds__(64 * COMPOSE_WPB) void compose_kernel(StepArgs a) {
+    const int wv = threadIdx.x / 64;
+    const int e = blockIdx.x * COMPOSE_WPB + wv;
     if (e >= a.N || !a.dirty[e]) return;
     TG_CPROF_INIT
     using CL = CompLayout<M>;
     static_assert(M::NL <= 64 && M::NG <= 64 && M::NS <= 64, "compose: one lane per link / group / shape");
-    __shared__ float T[M::NL][12];    // link pose in its group-root frame: R (9), p (3)
-    __shared__ float LM[M::NL + 1][10];   // link mass, com (group frame), inertia about com (group axes, 6); row NL = 0
-    __shared__ int GL[M::NG][M::MAXGL];   // group links, padded with NL (the zero row) so the sums run branch-free
-    const int lane = threadIdx.x;
+    __shared__ float Ts[COMPOSE_WPB][M::NL][12];    // link pose in its group-root frame: R (9), p (3)
+    __shared__ float LMs[COMPOSE_WPB][M::NL + 1][10];   // link mass, com (group frame), inertia about com; row NL = 0
+    __shared__ int GLs[COMPOSE_WPB][M::NG][M::MAXGL];   // group links, padded with NL (the zero row): branch-free sums
+    float(&T)[M::NL][12] = Ts[wv];
+    float(&LM)[M::NL + 1][10] = LMs[wv];
+    int(&GL)[M::NG][M::MAXGL] = GLs[wv];
+    const int lane = threadIdx.x % 64;
     auto wsync = [] {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -443,7 +451,8 @@ template <class M, bool HF> int launch_par(const StepArgs &a, hipStream_t stream
 }
 
 template <class M> int launch_model(const StepArgs &a, hipStream_t stream, hipEvent_t ev_begin, hipEvent_t ev_end) {
-    hipLaunchKernelGGL(compose_kernel<M>, dim3(a.N), dim3(64), 0, stream, a);
+    hipLaunchKernelGGL(compose_kernel<M>, dim3((a.N + COMPOSE_WPB - 1) / COMPOSE_WPB), dim3(64 * COMPOSE_WPB), 0, stream,
+                       a);
     if (ev_begin && hipEventRecord(ev_begin, stream) != hipSuccess) return TG_ERR_HIP;
     if (int rc = a.hf ? launch_par<M, true>(a, stream) : launch_par<M, false>(a, stream)) return rc;
     if (ev_end && hipEventRecord(ev_end, stream) != hipSuccess) return TG_ERR_HIP;
