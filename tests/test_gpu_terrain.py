@@ -144,9 +144,27 @@ def test_gpu_gogoro_terrain_step_matches_oracle_along_300_steps():
 
 
 def test_gpu_gogoro_terrain_free_running_matches_oracle():
+    """Free-running fp32 GPU vs fp64 oracle on the Perlin terrain.  The
+    heightfield is piecewise planar, so a ~1e-4 state difference can put a
+    tyre's support point on the other side of a triangle edge for one step
+    (the contact normal jumps) and the difference spikes before the two
+    trajectories re-converge: seed 6 shows one env at one step at 1.26e-3
+    (scripts/terrain_free_drift.py), while the teacher-forced one-step errors
+    along the same start stay below 1.1e-4 (next test).  Hence the free-running
+    bound is 2e-3 and resets must agree exactly."""
     _cuda()
     from tests.gpu_harness import gogoro_terrain
     err = gogoro_terrain(num_envs=64, steps=60, seed=6, forced=False)
     print(err)
-    assert err["obs"] < 1e-3 and err["rew"] < 1e-3, err
+    assert err["obs"] < 2e-3 and err["rew"] < 2e-3, err
     assert err["reset_equal"], err
+
+
+def test_gpu_gogoro_terrain_forced_on_the_free_running_seed():
+    """Teacher-forced (1e-3, north_star) on the seed of the free-running test."""
+    _cuda()
+    from tests.gpu_harness import gogoro_terrain
+    err = gogoro_terrain(num_envs=64, steps=60, seed=6)
+    print(err)
+    assert err["obs"] < 1e-3 and err["rew"] < 1e-3, err
+    assert err["reset_equal"] and err["timeout_equal"], err

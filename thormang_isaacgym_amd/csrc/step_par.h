@@ -1,20 +1,32 @@
 // step_par.h -- tree-parallel, LDS-resident articulation step (included by
-// articulation.hip after the shared helpers; the algorithm of
-// oracle/physics_ref.c, operation for operation per group).
+// articulation.hip after the shared helpers).  The algorithm of
+// oracle/physics_ref.c (Featherstone ABA with a floating base, implicit drives,
+// patch-friction PGS contact), evaluated in the ROOT-BODY FRAME: every spatial
+// quantity of every group (pose, velocity, inertia, articulated inertia, bias
+// force, acceleration, contact Jacobian) is expressed at the root-body origin
+// in the root body's coordinates frozen at the start of the substep (an
+// inertial frame).  The oracle works in group frames with a spatial transform
+// per tree edge; here pass 1 places each group in the root frame once, and the
+// backward pass, the forward pass, the Delassus columns and the impulse
+// application become transform-free: a child's articulated inertia and bias
+// force add into its parent's as they are, and a parent's acceleration is its
+// child's before the joint term.  The motion subspace of a group is
+// S = (a, P x a) (revolute) or (0, a) (prismatic), a = the group's joint axis
+// (its frame's e_z, joint-aligned frames from model/codegen.py), P its origin.
 //
 // Layout: EPB envs per workgroup, LPE lanes per env (LPE consecutive lanes of
-// one wavefront).  Each env's articulated state (per group: X, v, I^A, p^A, U,
-// D^-1, u, q, qd, qds, gravity-in-frame) lives in LDS at
-// lds[env * ES + group * GF + field] with 16-byte aligned field blocks.  At 16 envs x 2370 floats the
+// one wavefront).  Each env's articulated state (per group: pose R,P; v, I^A,
+// p^A, U, D^-1, u, q, qd, qds) lives in LDS at lds[env * ES + group * GF +
+// field] with 16-byte aligned field blocks.  At 16 envs x 2370 floats the
 // Thormang block uses 148 KB of the 160 KB LDS of a CU; 4096 envs = 256
 // workgroups = one per CU.
 //
 // Parallelism inside an env: model/codegen.py list-schedules the non-root
 // groups onto the LPE lanes (M::sched[step][lane], parents at earlier steps).
-//   pass 1 (kinematics, velocities, bias)      -- schedule forward
+//   pass 1 (root-frame poses, velocities, inertias, bias forces) -- schedule forward
 //   pass 2 (articulated inertias)               -- schedule backward; a group
-//          gathers its children's contributions (each child leaves
-//          X^T I^a X and X^T p^a in its own I^A / p^A slots), so lanes never
+//          gathers its children's contributions (each child leaves its
+//          I^a and p^a in its own I^A / p^A slots), so lanes never
 //          accumulate into the same address
 //   pass 3 (accelerations), impulse application -- forward / backward again
 //   Delassus columns                            -- one column per lane, the
@@ -52,11 +64,14 @@ struct LE {
 };
 
 // per-group field offsets (GF floats per group)
-// (16-byte aligned blocks: X = E,r [0,12), v [12,18), I^A [20,41), p^A [44,50),
-// so the compiler can move them with ds_read/write_b128)
+// (16-byte aligned blocks: pose [0,12), v [12,18), I^A [20,41), p^A [44,50),
+// so the compiler can move them with ds_read/write_b128).  F_RT holds the
+// group->root rotation R column-major (= R^T row-major), so the joint axis
+// (column 2) and the origin P are the 6 contiguous floats [6,12).
+// F_CL: drive-clamp scratch (te, K, effort) between the two solves.
 enum : int {
-    F_E = 0, F_R = 9, F_V = 12, F_Q = 18, F_QD = 19, F_IA = 20, F_DINV = 41, F_UU = 42, F_QDS = 43, F_PA = 44,
-    F_U = 50, F_GL = 56, GF = 60
+    F_RT = 0, F_AX = 6, F_P = 9, F_V = 12, F_Q = 18, F_QD = 19, F_IA = 20, F_DINV = 41, F_UU = 42, F_QDS = 43,
+    F_PA = 44, F_U = 50, F_CL = 56, GF = 60
 };
 
 __device__ __forceinline__ V3 ldv3(const LE &s, int o) { return v3(s(o), s(o + 1), s(o + 2)); }
@@ -89,7 +104,9 @@ __device__ __forceinline__ void stsi(const LE &s, int o, const SI &I) {
 }
 // scratch float x of the contact phase, laid over the groups' I^A slots
 __device__ __forceinline__ int scr(int x) { return (x / 21) * GF + F_IA + x % 21; }
-__device__ __forceinline__ Xf ldx(const LE &s, int g) { return Xf{ldm3(s, g * GF + F_E), ldv3(s, g * GF + F_R)}; }
+// group g's pose in the root frame: rotation (group -> root) and origin
+__device__ __forceinline__ M3 ldR(const LE &s, int g) { return transpose(ldm3(s, g * GF + F_RT)); }
+__device__ __forceinline__ void stR(const LE &s, int g, const M3 &R) { stm3(s, g * GF + F_RT, transpose(R)); }
 
 // per-group model table in LDS (ints; axis as float bits), built once per block
 enum : int { GI_PARENT = 0, GI_DOF = 1, GI_JT = 2, GI_NCH = 3, GI_CH = 4 };
@@ -108,9 +125,11 @@ template <class M> struct ParLayout {
     static constexpr int FLG = CGV + 6 * M::NCG;     // a drive exceeded its effort limit
     // per-block ints after the env area
     static constexpr int T_GI = 0;
-    static constexpr int T_SCHED = M::NG * GIW;
-    static constexpr int T_CPATH = T_SCHED + M::NSTEP * M::LPE;   // [NCG][MAXD]
-    static constexpr int T_TOTAL = T_CPATH + M::NCG * M::MAXD;
+    static constexpr int T_CPATH = T_GI + M::NG * GIW;                 // [NCG][MAXD]
+    // per (schedule step, lane) descriptor, one int4 (see step_desc)
+    static constexpr int T_DESC = (T_CPATH + M::NCG * M::MAXD + 3) & ~3;
+    static constexpr int T_ZERO = T_DESC + 4 * M::NSTEP * M::LPE;     // 32 zero floats
+    static constexpr int T_TOTAL = T_ZERO + 32;
     // SEPC (when the LDS has room): pass 2 writes each group's contribution to
     // its parent (I^a 21 at +0, p^a 6 at +24) and pass 3 its acceleration (+0)
     // into a separate 32-float block, so pass 1's rigid inertias and bias
@@ -122,9 +141,6 @@ template <class M> struct ParLayout {
     template <int EPB> static constexpr size_t bytes() { return ((size_t)EPB * ES + T_TOTAL) * 4; }
 };
 
-// Group frames are joint-aligned (model/codegen.py gq, applied by
-// compose_kernel): every motion subspace is S = (e_z, 0) (revolute) or
-// (0, e_z) (prismatic), so S-products are component selects.
 struct GInfo {
     int parent, dof, jt;
 };
@@ -134,34 +150,55 @@ template <class M> __device__ __forceinline__ GInfo ginfo(const int *gi, int g) 
     return GInfo{p[GI_PARENT], p[GI_DOF], p[GI_JT]};
 }
 
-__device__ __forceinline__ float dotS(int jt, const SV &x) { return jt == TG_JOINT_REVOLUTE ? x.w.z : x.v.z; }
-__device__ __forceinline__ SV addS(int jt, SV x, float a) {   // x + a S
-    if (jt == TG_JOINT_REVOLUTE) x.w.z += a;
-    else x.v.z += a;
-    return x;
+// Schedule descriptor of (step t, lane): everything a lane needs about the
+// group it handles, in one ds_read_b128 (prefetched a step ahead):
+//   x = group (0: idle), y = parent, z = dof | jt << 16,
+//   w = nch | smax << 4 | child_c << (8 + 8c)  (smax: the step's max nch over lanes)
+struct alignas(16) I4 {
+    int x, y, z, w;
+};
+template <class M> constexpr I4 step_desc(int t, int lane) {
+    const int g = M::sched[t][lane];
+    if (g <= 0) return I4{0, 0, 0, 0};
+    int smax = 0;
+    for (int l = 0; l < M::LPE; ++l)
+        if (M::sched[t][l] > 0 && M::nchild[M::sched[t][l]] > smax) smax = M::nchild[M::sched[t][l]];
+    int w = M::nchild[g] | smax << 4;
+    for (int c = 0; c < M::nchild[g]; ++c) w |= M::child[g][c] << (8 + 8 * c);
+    return I4{g, M::parent[g], M::gdof[g] | M::jtype[g] << 16, w};
 }
-__device__ __forceinline__ SV colS(int jt, const SI &I) {   // I S
-    return jt == TG_JOINT_REVOLUTE ? SV{v3(I.A[4], I.A[5], I.A[2]), v3(I.B[6], I.B[7], I.B[8])}
-                                   : SV{v3(I.B[2], I.B[5], I.B[8]), v3(I.C[4], I.C[5], I.C[2])};
+template <class M> constexpr int max_nonroot_children() {
+    int m = 0;
+    for (int g = 1; g < M::NG; ++g) m = M::nchild[g] > m ? M::nchild[g] : m;
+    return m;
 }
-__device__ __forceinline__ SV crmS(int jt, const SV &v, float qd) {   // v x (qd S)
-    const V3 wz = v3(v.w.y * qd, -v.w.x * qd, 0.f);
-    return jt == TG_JOINT_REVOLUTE ? SV{wz, v3(v.v.y * qd, -v.v.x * qd, 0.f)} : SV{v3(0, 0, 0), wz};
-}
-
-// world pose of group g by walking up to the root: R_g = R_0 E_a1^T ... E_g^T
-__device__ __forceinline__ void world_pose(const LE &s, const int *gi, int giw, int g, const M3 &R0, V3 p0, M3 &Rg,
-                                           V3 &pg) {
-    M3 Mr = eye3();
-    V3 t = v3(0, 0, 0);
-    while (g > 0) {
-        const M3 Et = transpose(ldm3(s, g * GF + F_E));
-        t = ldv3(s, g * GF + F_R) + mul(Et, t);
-        Mr = mul(Et, Mr);
-        g = gi[g * giw + GI_PARENT];
+template <class M> struct DescTab {
+    static_assert(max_nonroot_children<M>() <= 3 && M::NG <= 255, "descriptor packs 3 children of 8 bits");
+    struct Arr {
+        I4 d[M::NSTEP * M::LPE];
+    };
+    static constexpr Arr make() {
+        Arr a{};
+        for (int i = 0; i < M::NSTEP * M::LPE; ++i) a.d[i] = step_desc<M>(i / M::LPE, i % M::LPE);
+        return a;
     }
-    Rg = mul(R0, Mr);
-    pg = p0 + mul(R0, t);
+    static constexpr Arr tab = make();
+};
+__device__ __forceinline__ int d_dof(const I4 &d) { return d.z & 0xFFFF; }
+__device__ __forceinline__ int d_jt(const I4 &d) { return d.z >> 16; }
+__device__ __forceinline__ int d_nch(const I4 &d) { return d.w & 15; }
+__device__ __forceinline__ int d_smax(const I4 &d) { return (d.w >> 4) & 15; }
+__device__ __forceinline__ int d_child(const I4 &d, int c) { return (d.w >> (8 + 8 * c)) & 255; }
+
+// motion subspace of a joint in the root frame from its axis a and origin P:
+// (a, P x a) for a revolute joint, (0, a) for a prismatic one
+__device__ __forceinline__ SV motion_S(int jt, V3 ax, V3 P) {
+    const bool rev = jt == TG_JOINT_REVOLUTE;
+    const V3 pa = cross(P, ax);
+    return SV{rev ? ax : v3(0, 0, 0), rev ? pa : ax};
+}
+__device__ __forceinline__ SV ldS(const LE &s, int g, int jt) {
+    return motion_S(jt, ldv3(s, g * GF + F_AX), ldv3(s, g * GF + F_P));
 }
 
 // The LPE lanes of an env are consecutive lanes of one wavefront, whose LDS
@@ -236,10 +273,12 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
     extern __shared__ __attribute__((aligned(16))) float lds_raw[];
     int *tab = reinterpret_cast<int *>(lds_raw + EPB * PL::ES);
     const int *gi = tab + PL::T_GI;
-    const int *sched = tab + PL::T_SCHED;
+    const I4 *desc = reinterpret_cast<const I4 *>(tab + PL::T_DESC);   // [NSTEP][LPE]
+    const float *zeros = reinterpret_cast<const float *>(tab + PL::T_ZERO);
     const int *cpath = tab + PL::T_CPATH;
     const int tid = threadIdx.x;
     const int le = tid / LPE, sub = tid % LPE;
+    auto dsc = [&](int t) { return desc[t * LPE + sub]; };
     // XCD-aware chunk order: workgroups are dispatched round-robin over the 8
     // XCDs, so workgroup b takes env chunk (b % 8) * (nb / 8) + b / 8 and each
     // XCD's L2 sees a contiguous env range (the [KC][N] composite cache rows
@@ -258,7 +297,12 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
         p[GI_NCH] = M::nchild[i];
         for (int c = 0; c < M::MAXC; ++c) p[GI_CH + c] = M::child[i][c];
     }
-    for (int i = tid; i < M::NSTEP * LPE; i += EPB * LPE) tab[PL::T_SCHED + i] = M::sched[i / LPE][i % LPE];
+    for (int i = tid; i < M::NSTEP * LPE; i += EPB * LPE) {
+        const I4 d = DescTab<M>::tab.d[i];
+        int *p = tab + PL::T_DESC + 4 * i;
+        p[0] = d.x; p[1] = d.y; p[2] = d.z; p[3] = d.w;
+    }
+    for (int i = tid; i < 32; i += EPB * LPE) tab[PL::T_ZERO + i] = 0;
     for (int i = tid; i < M::NCG * M::MAXD; i += EPB * LPE) tab[PL::T_CPATH + i] = M::cpath[i / M::MAXD][i % M::MAXD];
 
     const LE s{lds_raw + le * PL::ES};
@@ -267,8 +311,13 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
     const float h = a.h;
     const bool fix_base = a.fix_base != 0;
     const float *comp = a.comp;
-    auto CP = [&](int k) { return comp[(size_t)k * N + e]; };
-    auto PR = [&](int f, int d) { return a.props[((size_t)f * N + e) * D + d]; };
+#ifdef TG_EXP_HOT   // developer experiment: every env reads env (e % 64)'s inputs (cache-resident)
+    const int ein = e % 64;
+#else
+    const int ein = e;
+#endif
+    auto CP = [&](int k) { return comp[(size_t)k * N + ein]; };
+    auto PR = [&](int f, int d) { return a.props[((size_t)f * N + ein) * D + d]; };
     const bool lead = sub == 0;
 
     float *root = a.root + (size_t)e * 13;
@@ -278,6 +327,10 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
         const int d = gi[g * GIW + GI_DOF];
         s(g * GF + F_Q) = dofs[2 * d];
         s(g * GF + F_QD) = dofs[2 * d + 1];
+    }
+    if (sub == 0) {   // the root group's pose in its own frame (never rewritten)
+        stR(s, 0, eye3());
+        stv3(s, F_P, v3(0, 0, 0));
     }
     V3 pos = v3(root[0], root[1], root[2]);
     float qx = root[3], qy = root[4], qz = root[5], qw = root[6];
@@ -292,31 +345,34 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
     SV v0 = fix_base ? sv0() : SV{mulT(R, ww), mulT(R, vo)};
     const V3 grav = v3(a.gx, a.gy, a.gz);
 
-    // rigid inertia + bias force of group g (pass 1 body), v and gl already known
-    // cin: the group's composite inertia (m, c, Ic) from the per-env cache
-    auto body_bias = [&](int g, const SV &vg, V3 gl, const float *cin) {
+    // rigid inertia + bias force of group g (pass 1 body) in the root frame;
+    // v, the group's root-frame pose (Rg, Pg) and gravity in the root frame gr
+    // already known.  cin: the group's composite inertia (m, com, Ic about the
+    // com) in its own frame, from the per-env cache.
+    //   c = P + R c_l, Ic_w = R Ic R^T, I = rb_inertia(m, c, Ic_w)
+    //   h = m (v + w x c) (momentum), L = Ic_w w + c x h
+    //   p = v x* (L, h) - (n, F),  F = m g - k_lin h + f_ext,
+    //   n = c x F - k_ang Ic_w w + t_ext
+    auto body_bias = [&](int g, const SV &vg, const M3 &Rg, V3 Pg, V3 gr, const float *cin) {
         const int o = g * GF;
         const float m = cin[0];
-        const V3 cg = v3(cin[1], cin[2], cin[3]);
-        float Ic[6];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) Ic[k] = cin[4 + k];
-        const SI I = rb_inertia(m, cg, Ic);
-        stsi(s, o + F_IA, I);
-        const SV b = crf(vg, mul(I, vg));
-        V3 F = m * gl;
-        F = F - (a.lin_damp * m) * (vg.v + cross(vg.w, cg));
-        V3 n = cross(cg, F) - a.ang_damp * symmul(Ic, vg.w);
+        const V3 c = Pg + mul(Rg, v3(cin[1], cin[2], cin[3]));
+        float Icw[6];
+        sym_rot(cin + 4, transpose(Rg), Icw);
+        stsi(s, o + F_IA, rb_inertia(m, c, Icw));
+        const V3 hm = m * (vg.v + cross(vg.w, c));
+        const V3 Iw = symmul(Icw, vg.w);
+        const V3 L = Iw + cross(c, hm);
+        V3 F = m * gr - a.lin_damp * hm;
+        V3 n = -a.ang_damp * Iw;
         if (a.force) {
             const float *fw = a.force + ((size_t)e * M::NG + g) * 6;
-            M3 Rw;
-            V3 pw;
-            world_pose(s, gi, GIW, g, R, pos, Rw, pw);
-            const V3 fl = mulT(Rw, v3(fw[0], fw[1], fw[2])), tl = mulT(Rw, v3(fw[3], fw[4], fw[5]));
-            F = F + fl;
-            n = n + tl + cross(cg, fl);
+            F = F + mulT(R, v3(fw[0], fw[1], fw[2]));
+            n = n + mulT(R, v3(fw[3], fw[4], fw[5]));
         }
-        stsv(s, o + F_PA, SV{b.w - n, b.v - F});
+        n = n + cross(c, F);
+        const V3 bw = cross(vg.w, L) + cross(vg.v, hm), bv = cross(vg.w, hm);
+        stsv(s, o + F_PA, SV{bw - n, bv - F});
     };
     // per-group per-env inputs, prefetched one schedule step ahead
     auto load_kin = [&](int g, float *x) {   // joint placement (12) + inertia (10)
@@ -325,8 +381,7 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
 #pragma unroll
         for (int k = 0; k < 10; ++k) x[12 + k] = CP(CL::inertia(g) + k);
     };
-    auto load_drv = [&](int g, float *x) {   // drive / limit inputs of the group's dof
-        const int d = gi[g * GIW + GI_DOF];
+    auto load_drv = [&](int d, float *x) {   // drive / limit inputs of dof d
         x[0] = PR(TG_PROP_ARMATURE, d);
         x[1] = PR(TG_PROP_DRIVE_MODE, d);
         x[2] = PR(TG_PROP_STIFFNESS, d);
@@ -337,6 +392,27 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
         x[7] = a.pos_tgt[(size_t)e * D + d];
         x[8] = a.vel_tgt[(size_t)e * D + d];
         x[9] = a.act ? a.act[(size_t)e * D + d] : 0.f;
+    };
+    // pass 2: the children's contributions of the lane's group, n = the step's
+    // largest child count: absent children read the zero block, so every load
+    // is issued before the first add (one LDS round trip)
+    auto gather = [&](auto NCc, const I4 &dc, SI &IA, SV &pA) {
+        constexpr int n = decltype(NCc)::value;
+        SI ci[n];
+        SV cv[n];
+#pragma unroll
+        for (int c = 0; c < n; ++c) {
+            const bool has = c < d_nch(dc);
+            const int ch = d_child(dc, c);
+            const float *pi = has ? s.b + ia_c(ch) : zeros, *pp = has ? s.b + pa_c(ch) : zeros;
+            ci[c] = ldsi(LE{(float *)__builtin_assume_aligned(pi, 16)}, 0);
+            cv[c] = ldsv(LE{(float *)__builtin_assume_aligned(pp, 16)}, 0);
+        }
+#pragma unroll
+        for (int c = 0; c < n; ++c) {
+            si_add(IA, ci[c]);
+            pA = pA + cv[c];
+        }
     };
     float rin[10];
 #pragma unroll
@@ -349,8 +425,10 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
         // unclamped; if some drive's implicit end-of-substep torque te - K*qdd
         // exceeds its effort, they run once more with those drives as the
         // explicit torque +-effort ("implicit, then clamp", as
-        // oracle/physics_ref.c aba()).  Between the two runs the F_GL slots of
+        // oracle/physics_ref.c aba()).  Between the two runs the F_CL slots of
         // a drive group hold (te, K, effort) and F_UU holds qdd.
+        // Every schedule step below issues all its LDS loads before its first
+        // LDS store (the compiler keeps LDS loads and stores in program order).
         LDL6 rootf{};
         SV a0 = sv0();
 #pragma unroll 1
@@ -363,36 +441,39 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
         if (tid % 64 == 0) atomicAdd(&tg_prof_acc[14 + cp], 1ull);
 #endif
         // ---- pass 1: root, then the schedule forward (SEPC: not rerun, its
-        // results are intact)
-        int gn;
+        // results are intact).  Descriptors run two steps ahead, the cache
+        // inputs one step ahead.
         if (!SEPC || cp == 0) {
+        const V3 gr = mulT(R, grav);   // gravity in the root frame
         if (lead) {
-            const V3 gl = mulT(R, grav);
             stsv(s, F_V, v0);
-            stv3(s, F_GL, gl);
-            body_bias(0, v0, gl, rin);
+            body_bias(0, v0, eye3(), v3(0, 0, 0), gr, rin);
         }
         TG_SYNC();
         float nk[22];
-        gn = sched[sub];
-        if (gn > 0) load_kin(gn, nk);
+        I4 d1 = dsc(0), d2 = M::NSTEP > 1 ? dsc(1) : I4{0, 0, 0, 0};
+        if (d1.x > 0) load_kin(d1.x, nk);
 #pragma unroll 1
         for (int t = 0; t < M::NSTEP; ++t) {
-            const int g = gn;
+            const I4 dc = d1;
             float ck[22];
 #pragma unroll
             for (int k = 0; k < 22; ++k) ck[k] = nk[k];
-            gn = t + 1 < M::NSTEP ? sched[(t + 1) * LPE + sub] : -1;
-            if (gn > 0) load_kin(gn, nk);
+            d1 = d2;
+            d2 = t + 2 < M::NSTEP ? dsc(t + 2) : I4{0, 0, 0, 0};
+            if (d1.x > 0) load_kin(d1.x, nk);
+            const int g = dc.x;
             if (g > 0) {
-                const int o = g * GF;
-                const GInfo G = ginfo<M>(gi, g);
-                M3 Rpc;
+                const int o = g * GF, par = dc.y, jt = d_jt(dc);
+                const M3 Rp = ldR(s, par);
+                const V3 Pp = ldv3(s, par * GF + F_P);
+                const SV vp = ldsv(s, par * GF + F_V);
+                const float qg = s(o + F_Q), qdg = s(o + F_QD);
+                M3 Rpc;   // child -> parent rotation at q, then the root-frame pose
 #pragma unroll
                 for (int k = 0; k < 9; ++k) Rpc.a[k] = ck[k];
                 V3 tr = v3(ck[9], ck[10], ck[11]);
-                const float qg = s(o + F_Q);
-                if (G.jt == TG_JOINT_REVOLUTE) {   // Rpc * Rz(q)
+                if (jt == TG_JOINT_REVOLUTE) {   // Rpc * Rz(q)
                     float sq, cq;
                     __sincosf(qg, &sq, &cq);
 #pragma unroll
@@ -404,59 +485,60 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
                 } else {
                     tr = tr + qg * v3(Rpc.a[2], Rpc.a[5], Rpc.a[8]);
                 }
-                const Xf X{transpose(Rpc), tr};
-                stm3(s, o + F_E, X.E);
-                stv3(s, o + F_R, tr);
-                const SV vg = addS(G.jt, xmotion(X, ldsv(s, G.parent * GF + F_V)), s(o + F_QD));
-                const V3 gl = mul(X.E, ldv3(s, G.parent * GF + F_GL));
+                const M3 Rg = mul(Rp, Rpc);
+                const V3 Pg = Pp + mul(Rp, tr);
+                stR(s, g, Rg);
+                stv3(s, o + F_P, Pg);
+                const SV Sg = motion_S(jt, v3(Rg.a[2], Rg.a[5], Rg.a[8]), Pg);
+                const SV vg = vp + qdg * Sg;
                 stsv(s, o + F_V, vg);
-                stv3(s, o + F_GL, gl);
-                body_bias(g, vg, gl, ck + 12);
+                body_bias(g, vg, Rg, Pg, gr, ck + 12);
             }
             TG_SYNC();
         }
         }   // pass 1
         TG_PROF(1)
         // ---- pass 2: schedule backward, children contributions gathered
+        {
         float nd[10];
-        gn = sched[(M::NSTEP - 1) * LPE + sub];
-        if (gn > 0) load_drv(gn, nd);
+        I4 d1 = dsc(M::NSTEP - 1), d2 = M::NSTEP > 1 ? dsc(M::NSTEP - 2) : I4{0, 0, 0, 0};
+        if (d1.x > 0) load_drv(d_dof(d1), nd);
 #pragma unroll 1
         for (int t = M::NSTEP - 1; t >= 0; --t) {
-            const int g = gn;
+            const I4 dc = d1;
             float cd[10];
 #pragma unroll
             for (int k = 0; k < 10; ++k) cd[k] = nd[k];
-            gn = t > 0 ? sched[(t - 1) * LPE + sub] : -1;
-            if (gn > 0) load_drv(gn, nd);
+            d1 = d2;
+            d2 = t >= 2 ? dsc(t - 2) : I4{0, 0, 0, 0};
+            if (d1.x > 0) load_drv(d_dof(d1), nd);
+            const int g = dc.x;
             if (g > 0) {
                 const int o = g * GF;
-                const GInfo G = ginfo<M>(gi, g);
                 SI IA = ldsi(s, o + F_IA);
                 SV pA = ldsv(s, o + F_PA);
-                const int nch = gi[g * GIW + GI_NCH];
-                for (int c = 0; c < nch; ++c) {
-                    const int ch = gi[g * GIW + GI_CH + c];
-                    si_add(IA, ldsi(s, ia_c(ch)));
-                    pA = pA + ldsv(s, pa_c(ch));
-                }
-                const SV U = colS(G.jt, IA);
-                const float q = s(o + F_Q), qd = s(o + F_QD);
-                const float D0 = dotS(G.jt, U) + cd[0];
+                const SV Sg = ldS(s, g, d_jt(dc));
+                const SV vg = ldsv(s, o + F_V);
+                const float q = s(o + F_Q), qd = s(o + F_QD), qdd0 = s(o + F_UU);
+                const int smax = d_smax(dc);
+                if (smax == 1) gather(std::integral_constant<int, 1>{}, dc, IA, pA);
+                else if (smax == 2) gather(std::integral_constant<int, 2>{}, dc, IA, pA);
+                else if (smax >= 3) gather(std::integral_constant<int, 3>{}, dc, IA, pA);
+                const SV U = mul(IA, Sg);
+                const float D0 = dot(Sg, U) + cd[0];
                 float Dimp = 0.f, tau = 0.f;
                 const int mode = (int)rintf(cd[1]);
                 const float kp = cd[2], kd = cd[3];
                 const float eff = cd[4];
+                float cl0 = 0.f, cl1 = -1.f;   // clamp scratch (te, K) of the first solve
                 if (mode == TG_DOF_MODE_POS || mode == TG_DOF_MODE_VEL) {
                     const float te = kp * (cd[7] - q - h * qd) + kd * (cd[8] - qd);
                     const float K = h * kd + h * h * kp;
                     bool implicit = true;
-                    if (cp == 0) {
-                        s(o + F_GL) = te;
-                        s(o + F_GL + 1) = K;
-                        s(o + F_GL + 2) = eff;
-                    } else {
-                        const float ti = te - K * s(o + F_UU);   // F_UU: qdd of the first solve
+                    cl0 = te;
+                    cl1 = K;
+                    if (cp == 1) {
+                        const float ti = te - K * qdd0;   // qdd0: qdd of the first solve
                         if (fabsf(ti) > eff) {
                             implicit = false;
                             tau += ti > 0.f ? eff : -eff;
@@ -464,7 +546,6 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
                     }
                     if (implicit) { tau += te; Dimp += K; }
                 } else {
-                    if (cp == 0) s(o + F_GL + 1) = -1.f;
                     if (mode == TG_DOF_MODE_EFFORT && a.act) tau += fminf(fmaxf(cd[9], -eff), eff);
                 }
                 const float lo = cd[5], hi = cd[6];
@@ -481,27 +562,40 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
                     Dimp += r * (h * cl + h * h * kl);
                 }
                 const float Dinv = 1.0f / (D0 + Dimp);
-                const float u = tau - dotS(G.jt, pA);
+                const float u = tau - dot(Sg, pA);
+                SI Ia = IA;
+                si_sub_outer(Ia, U, Dinv);
+                const SV cb = crm(vg, qd * Sg);   // velocity-product acceleration
+                const SV pa = pA + mul(Ia, cb) + (u * Dinv) * U;
+                if (cp == 0) {
+                    s(o + F_CL) = cl0;
+                    s(o + F_CL + 1) = cl1;
+                    s(o + F_CL + 2) = eff;
+                }
                 stsv(s, o + F_U, U);
                 s(o + F_DINV) = Dinv;
                 s(o + F_UU) = u;
-                SI Ia = IA;
-                si_sub_outer(Ia, U, Dinv);
-                const SV cb = crmS(G.jt, ldsv(s, o + F_V), qd);
-                const SV pa = pA + mul(Ia, cb) + (u * Dinv) * U;
-                const Xf X = ldx(s, g);
-                stsi(s, ia_c(g), si_to_parent(Ia, X));     // contribution to the parent
-                stsv(s, pa_c(g), xTforce(X, pa));
+                stsi(s, ia_c(g), Ia);     // contribution to the parent (same frame: no transform)
+                stsv(s, pa_c(g), pa);
             }
             TG_SYNC();
+        }
         }
         // root: every lane factors the root articulated inertia itself
         {
             SI IA0 = ldsi(s, F_IA);
             SV pA0 = ldsv(s, F_PA);
+            SI ci[M::nchild[0] > 0 ? M::nchild[0] : 1];
+            SV cv[M::nchild[0] > 0 ? M::nchild[0] : 1];
+#pragma unroll
             for (int c = 0; c < M::nchild[0]; ++c) {
-                si_add(IA0, ldsi(s, ia_c(M::child[0][c])));
-                pA0 = pA0 + ldsv(s, pa_c(M::child[0][c]));
+                ci[c] = ldsi(s, ia_c(M::child[0][c]));
+                cv[c] = ldsv(s, pa_c(M::child[0][c]));
+            }
+#pragma unroll
+            for (int c = 0; c < M::nchild[0]; ++c) {
+                si_add(IA0, ci[c]);
+                pA0 = pA0 + cv[c];
             }
             if (!fix_base) {
                 rootf = ldl6(IA0);
@@ -516,25 +610,31 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
             s(PL::FLG) = 0.f;
         }
         TG_SYNC();
+        {
+        I4 d1 = dsc(0);
 #pragma unroll 1
         for (int t = 0; t < M::NSTEP; ++t) {
-            const int g = sched[t * LPE + sub];
+            const I4 dc = d1;
+            d1 = t + 1 < M::NSTEP ? dsc(t + 1) : I4{0, 0, 0, 0};
+            const int g = dc.x;
             if (g > 0) {
                 const int o = g * GF;
-                const GInfo G = ginfo<M>(gi, g);
-                const float qd = s(o + F_QD);
-                const SV cb = crmS(G.jt, ldsv(s, o + F_V), qd);
-                const SV ap = xmotion(ldx(s, g), ldsv(s, ac_s(G.parent))) + cb;
-                const float qdd = (s(o + F_UU) - dot(ldsv(s, o + F_U), ap)) * s(o + F_DINV);
-                stsv(s, ac_s(g), addS(G.jt, ap, qdd));
+                const SV apar = ldsv(s, ac_s(dc.y));
+                const SV vg = ldsv(s, o + F_V), Ug = ldsv(s, o + F_U);
+                const SV Sg = ldS(s, g, d_jt(dc));
+                const float qd = s(o + F_QD), uu = s(o + F_UU), dinv = s(o + F_DINV);
+                const float te = s(o + F_CL), K = s(o + F_CL + 1), eff = s(o + F_CL + 2);
+                const SV ap = apar + crm(vg, qd * Sg);
+                const float qdd = (uu - dot(Ug, ap)) * dinv;
+                stsv(s, ac_s(g), ap + qdd * Sg);
                 s(o + F_QDS) = qd + h * qdd;
                 if (cp == 0) {
                     s(o + F_UU) = qdd;
-                    const float K = s(o + F_GL + 1);
-                    if (K >= 0.f && fabsf(s(o + F_GL) - K * qdd) > s(o + F_GL + 2)) s(PL::FLG) = 1.f;
+                    if (K >= 0.f && fabsf(te - K * qdd) > eff) s(PL::FLG) = 1.f;
                 }
             }
             TG_SYNC();
+        }
         }
         if (cp == 0 && s(PL::FLG) == 0.f) break;
         }   // clamp pass
@@ -547,15 +647,13 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
         if constexpr (M::NS > 0) {
             // contact-group world poses and free velocities (one lane per contact group)
             for (int c = sub; c < M::NCG; c += LPE) {
-                M3 Rc;
-                V3 pc;
-                world_pose(s, gi, GIW, M::cgroup[c], R, pos, Rc, pc);
-                stm3(s, PL::CGP + 12 * c, Rc);
-                stv3(s, PL::CGP + 12 * c + 9, pc);
-                SV v = v0s;
+                const int cg = M::cgroup[c];
+                stm3(s, PL::CGP + 12 * c, mul(R, ldR(s, cg)));
+                stv3(s, PL::CGP + 12 * c + 9, pos + mul(R, ldv3(s, cg * GF + F_P)));
+                SV v = v0s;   // root frame: the root velocity plus the path's joint terms
                 for (int i = 0; i < M::cpath_len[c]; ++i) {
                     const int hg = cpath[c * M::MAXD + i];
-                    v = addS(ginfo<M>(gi, hg).jt, xmotion(ldx(s, hg), v), s(hg * GF + F_QDS));
+                    v = v + s(hg * GF + F_QDS) * ldS(s, hg, ginfo<M>(gi, hg).jt);
                 }
                 stsv(s, PL::CGV + 6 * c, v);
             }
@@ -616,7 +714,7 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
                 support(n);
                 // every point carries a speculative normal row along n; the friction
                 // patch is anchored at the centroid weighted by clamp((margin-phi)/margin)
-                const V3 dl = mulT(Rwg, n);
+                const V3 dl = mulT(R, n);   // root frame
                 V3 cen = v3(0, 0, 0), cen0 = v3(0, 0, 0);
                 float wk[4], wsum = 0.f;
 #pragma unroll
@@ -630,8 +728,8 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
                         const float gz = ground_at(a, pts[k].x, pts[k].y, nk, th);
                         phi = (pts[k].z - gz) * nk.z;
                     }
-                    // row Jacobian in the group frame: (r x d, d), d = Rwg^T n
-                    stsv(s, ro, SV{cross(mulT(Rwg, pts[k] - pwg), dl), dl});
+                    // row Jacobian in the root frame: (r x d, d), r = the point about the root origin
+                    stsv(s, ro, SV{cross(mulT(R, pts[k] - pos), dl), dl});
                     s(ro + 6) = phi > a.rest ? -(phi - a.rest) / h : fminf(a.baumgarte * (a.rest - phi) / h, a.max_depen);
                     s(ro + 7) = 1.f;
                     wk[k] = fminf(fmaxf((a.margin - phi) / a.margin, 0.f), 1.f);
@@ -659,18 +757,18 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
                     if (nx > 1e-6f) t1 = (1.f / nx) * x;
                 }
                 const V3 t2 = cross(n, t1);
-                const V3 rl = mulT(Rwg, cen - pwg);
+                const V3 rl = mulT(R, cen - pos);
                 const float fon = 1.f;
                 for (int t = 0; t < 3; ++t) {
                     const int ro = PL::ROW + (rb + nr + t) * 8;
-                    const V3 dt = mulT(Rwg, t == 0 ? t1 : (t == 1 ? t2 : n));
+                    const V3 dt = mulT(R, t == 0 ? t1 : (t == 1 ? t2 : n));
                     stsv(s, ro, t == 2 ? SV{dt, v3(0, 0, 0)} : SV{cross(rl, dt), dt});   // torsion row: angular
                     s(ro + 6) = 0.f;
                     s(ro + 7) = fon;
                 }
             }
             TG_SYNC();
-            // row i: group-frame Jacobian J_i (6) -> velocity J_i . v, impulse lam J_i
+            // row i: root-frame Jacobian J_i (6) -> velocity J_i . v, impulse lam J_i
             auto rvel = [&](int i, const SV &vg) { return dot(ldsv(s, PL::ROW + i * 8), vg); };
             auto rforce = [&](int i, float lam) { return lam * ldsv(s, PL::ROW + i * 8); };
             for (int i = sub; i < K; i += LPE) {
@@ -693,10 +791,9 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
                     du[i] = 0.f;
                     if (i < lk) {
                         const int g = pk[i];
-                        const float u = -dotS(ginfo<M>(gi, g).jt, p);
+                        const float u = -dot(ldS(s, g, ginfo<M>(gi, g).jt), p);
                         du[i] = u;
-                        const SV pa = p + (u * s(g * GF + F_DINV)) * ldsv(s, g * GF + F_U);
-                        p = xTforce(ldx(s, g), pa);
+                        p = p + (u * s(g * GF + F_DINV)) * ldsv(s, g * GF + F_U);
                     }
                 }
                 const SV aj = fix_base ? sv0() : ldl6_solve(rootf, -1.0f * p);
@@ -716,10 +813,9 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
                     for (int i = 0; i < M::MAXD; ++i) {
                         if (i < M::cpath_len[c]) {
                             const int hg = M::cpath[c][i];
-                            const SV ap = xmotion(ldx(s, hg), av);
                             const float dui = (i < lk && pk[i] == hg) ? du[i] : 0.0f;
-                            const float x = (dui - dot(ldsv(s, hg * GF + F_U), ap)) * s(hg * GF + F_DINV);
-                            av = addS(M::jtype[hg], ap, x);
+                            const float x = (dui - dot(ldsv(s, hg * GF + F_U), av)) * s(hg * GF + F_DINV);
+                            av = av + x * ldS(s, hg, M::jtype[hg]);
                         }
                     }
                     dvc[c] = av;
@@ -850,16 +946,15 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
                 // impulse application: bottom-up gather, root solve, top-down
 #pragma unroll 1
                 for (int t = M::NSTEP - 1; t >= 0; --t) {
-                    const int g = sched[t * LPE + sub];
+                    const I4 dc = dsc(t);
+                    const int g = dc.x;
                     if (g > 0) {
                         const int o = g * GF;
                         SV p = ldsv(s, o + F_PA);
-                        const int nch = gi[g * GIW + GI_NCH];
-                        for (int c = 0; c < nch; ++c) p = p + ldsv(s, gi[g * GIW + GI_CH + c] * GF + F_PA);
-                        const float u = -dotS(ginfo<M>(gi, g).jt, p);
+                        for (int c = 0; c < d_nch(dc); ++c) p = p + ldsv(s, d_child(dc, c) * GF + F_PA);
+                        const float u = -dot(ldS(s, g, d_jt(dc)), p);
                         s(o + F_UU) = u;
-                        const SV pa = p + (u * s(o + F_DINV)) * ldsv(s, o + F_U);
-                        stsv(s, o + F_PA, xTforce(ldx(s, g), pa));
+                        stsv(s, o + F_PA, p + (u * s(o + F_DINV)) * ldsv(s, o + F_U));
                     }
                     TG_SYNC();
                 }
@@ -870,18 +965,24 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
             TG_SYNC();
             if (lead) stsv(s, F_PA, da0);
             TG_SYNC();
+            {
+            I4 d1 = dsc(0);
 #pragma unroll 1
             for (int t = 0; t < M::NSTEP; ++t) {
-                const int g = sched[t * LPE + sub];
+                const I4 dc = d1;
+                d1 = t + 1 < M::NSTEP ? dsc(t + 1) : I4{0, 0, 0, 0};
+                const int g = dc.x;
                 if (g > 0) {
                     const int o = g * GF;
-                    const GInfo G = ginfo<M>(gi, g);
-                    const SV ap = xmotion(ldx(s, g), ldsv(s, G.parent * GF + F_PA));
-                    const float x = (s(o + F_UU) - dot(ldsv(s, o + F_U), ap)) * s(o + F_DINV);
-                    stsv(s, o + F_PA, addS(G.jt, ap, x));
-                    s(o + F_QDS) += x;
+                    const SV ap = ldsv(s, dc.y * GF + F_PA), Ug = ldsv(s, o + F_U);
+                    const SV Sg = ldS(s, g, d_jt(dc));
+                    const float uu = s(o + F_UU), dinv = s(o + F_DINV), qds = s(o + F_QDS);
+                    const float x = (uu - dot(Ug, ap)) * dinv;
+                    stsv(s, o + F_PA, ap + x * Sg);
+                    s(o + F_QDS) = qds + x;
                 }
                 TG_SYNC();
+            }
             }
             if (!fix_base) v0s = v0s + da0;
             TG_PROF(7)
