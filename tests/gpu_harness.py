@@ -204,16 +204,33 @@ def gogoro_terrain(num_envs=64, steps=300, seed=0, max_steps=300, terrain_seed=5
         if forced:
             err = forced_step_errors(env, orc, balance_policy, steps, act_to_orc=lambda a: a[:, 0])
         else:
-            err = {"obs": 0.0, "rew": 0.0, "root": 0.0, "reset_equal": True}
+            # Free running until the first step whose reset masks differ.  Such a
+            # step is accepted only as a threshold tie: every env that disagrees
+            # has its clean roll within `tie` of the 0.30 fall threshold
+            # (gogoro_new.py:671-676), i.e. inside the fp32-vs-fp64 tolerance.
+            # The reset draws are consumed in env order, so after a tie the two
+            # random streams desynchronise and the comparison stops there.
+            tie = 1e-3
+            err = {"obs": 0.0, "rew": 0.0, "root": 0.0, "reset_equal": True, "compared_steps": steps,
+                   "tie_envs": [], "ties_within_tol": True}
             obs = orc.a["obs_buf"].copy()
-            for _ in range(steps):
+            for k in range(steps):
                 act = balance_policy(obs)
                 obs_d, rew, reset, _ = env.step(torch.from_numpy(act).to("cuda:0"))
                 o_obs, o_rew, o_reset, _ = orc.step(act[:, 0])
+                r_g = reset.cpu().numpy()
+                if not np.array_equal(r_g, o_reset):
+                    bad = np.nonzero(r_g != o_reset)[0]
+                    roll = np.abs(orc.a["buffer_obs"][bad, -1, 0])
+                    err["reset_equal"] = False
+                    err["tie_envs"] = bad.tolist()
+                    err["tie_roll"] = roll.tolist()
+                    err["ties_within_tol"] = bool(np.all(np.abs(roll - 0.30) < tie))
+                    err["compared_steps"] = k
+                    break
                 err["obs"] = max(err["obs"], float(np.abs(obs_d["obs"].cpu().numpy() - o_obs).max()))
                 err["rew"] = max(err["rew"], float(np.abs(rew.cpu().numpy() - o_rew).max()))
                 err["root"] = max(err["root"], float(np.abs(env.root_tensor.cpu().numpy() - orc.a["root"]).max()))
-                err["reset_equal"] &= bool(np.array_equal(reset.cpu().numpy(), o_reset))
                 obs = o_obs.copy()
         err["spawn_z_max"] = float(env.root_reset_tensor[:, 2].max())
         return err

