@@ -29,10 +29,16 @@
 namespace tg {
 
 // per-env composite cache layout (SoA, [KC][N])
+// Per-env composite cache, env-major ([N][KC] floats): group g's block of 24
+// floats (joint placement R (9) + t (3), then mass, com (3), inertia about the
+// com (6), 2 pad) at 24 g, then 12 floats (R, t) per contact shape.  A lane
+// takes a group's 22 inputs with 6 16-byte loads from one base address.
 template <class M> struct CompLayout {
-    static constexpr int inertia(int g) { return 10 * g; }
-    static constexpr int xtree(int g) { return 10 * M::NG + 12 * (g - 1); }
-    static constexpr int shape(int s) { return 10 * M::NG + 12 * (M::NG - 1) + 12 * s; }
+    static constexpr int GB = 24;
+    static constexpr int xtree(int g) { return GB * g; }
+    static constexpr int inertia(int g) { return GB * g + 12; }
+    static constexpr int shape(int s) { return GB * M::NG + 12 * s; }
+    static_assert(M::KC == GB * M::NG + 12 * M::NS, "codegen KC");
 };
 
 __device__ __forceinline__ float prop(const StepArgs &a, int f, int e, int d) {
@@ -200,8 +206,7 @@ template <class M> __global__ __launch_bounds__(64 * COMPOSE_WPB) void compose_k
     // oracle/physics_ref.c), written to the cache in joint-aligned group
     // frames (axis e_z, codegen gq): v' = Q^T v, I' = Q^T I Q, placements
     // R' = Q_p^T R Q_g, t' = Q_p^T t
-    float *c = a.comp;
-    const size_t N = a.N;
+    float *c = a.comp + (size_t)e * M::KC;
     // large groups (the scooter's root group holds the locked rider: 55 links)
     // by wave reductions over lane = link, in tree order; the others by their
     // own lane in link order
@@ -273,21 +278,23 @@ template <class M> __global__ __launch_bounds__(64 * COMPOSE_WPB) void compose_k
         const V3 gcq = mulT(Qg, gc);
         float gIq[6];
         sym_from(gIq, mul(mul(transpose(Qg), sym_to(gI)), Qg));
-        float *ci = c + CL::inertia(g) * N + e;
+        float *ci = c + CL::inertia(g);
         ci[0] = gm;
-        ci[N] = gcq.x; ci[2 * N] = gcq.y; ci[3 * N] = gcq.z;
+        ci[1] = gcq.x; ci[2] = gcq.y; ci[3] = gcq.z;
 #pragma unroll
-        for (int k = 0; k < 6; ++k) ci[(4 + k) * N] = gIq[k];
+        for (int k = 0; k < 6; ++k) ci[4 + k] = gIq[k];
+        ci[10] = 0.f;
+        ci[11] = 0.f;
         if (g > 0) {
             M3 Rp;
             V3 Pp;
             ldT(gpl, Rp, Pp);
             const M3 Rx = mul(mul(transpose(Qp), mul(Rp, Rgo)), Qg);
             const V3 t = mulT(Qp, Pp + mul(Rp, tgo));
-            float *cx = c + CL::xtree(g) * N + e;
+            float *cx = c + CL::xtree(g);
 #pragma unroll
-            for (int k = 0; k < 9; ++k) cx[k * N] = Rx.a[k];
-            cx[9 * N] = t.x; cx[10 * N] = t.y; cx[11 * N] = t.z;
+            for (int k = 0; k < 9; ++k) cx[k] = Rx.a[k];
+            cx[9] = t.x; cx[10] = t.y; cx[11] = t.z;
         }
     }
     TG_CPROF(2)
@@ -297,10 +304,10 @@ template <class M> __global__ __launch_bounds__(64 * COMPOSE_WPB) void compose_k
         ldT(sl, Rsl, Psl);
         const M3 Rx = mul(transpose(Qs), mul(Rsl, Rso));
         const V3 t = mulT(Qs, Psl + mul(Rsl, tso));
-        float *cs = c + CL::shape(sh) * N + e;
+        float *cs = c + CL::shape(sh);
 #pragma unroll
-        for (int k = 0; k < 9; ++k) cs[k * N] = Rx.a[k];
-        cs[9 * N] = t.x; cs[10 * N] = t.y; cs[11 * N] = t.z;
+        for (int k = 0; k < 9; ++k) cs[k] = Rx.a[k];
+        cs[9] = t.x; cs[10] = t.y; cs[11] = t.z;
     }
     if (lane == 0) a.dirty[e] = 0;
     TG_CPROF(3)

@@ -158,10 +158,12 @@ struct alignas(16) I4 {
     int x, y, z, w;
 };
 template <class M> constexpr I4 step_desc(int t, int lane) {
-    const int g = M::sched[t][lane];
+    // lane pairs (M::PAIR): lanes sub and sub + SL run schedule slot sub
+    const int slot = lane % M::SL;
+    const int g = (lane < M::SL || M::PAIR) ? M::sched[t][slot] : -1;
     if (g <= 0) return I4{0, 0, 0, 0};
     int smax = 0;
-    for (int l = 0; l < M::LPE; ++l)
+    for (int l = 0; l < M::SL; ++l)
         if (M::sched[t][l] > 0 && M::nchild[M::sched[t][l]] > smax) smax = M::nchild[M::sched[t][l]];
     int w = M::nchild[g] | smax << 4;
     for (int c = 0; c < M::nchild[g]; ++c) w |= M::child[g][c] << (8 + 8 * c);
@@ -216,6 +218,18 @@ __device__ __forceinline__ float sum8(float v) {
     v += dpp<0xB1>(v);    // quad_perm [1,0,3,2]
     return v;
 }
+// over the 16 lanes of a DPP row: the two 8-lane halves, then row_ror:8
+__device__ __forceinline__ float sum16(float v) {
+    v = sum8(v);
+    return v + dpp<0x128>(v);
+}
+template <int L> __device__ __forceinline__ float sum_lanes(float v) {
+    static_assert(L == 8 || L == 16, "env lanes: 8 or 16");
+    if constexpr (L == 8) return sum8(v);
+    else return sum16(v);
+}
+// the partner lane's value (lane pairs sub, sub + 8 of a 16-lane row)
+__device__ __forceinline__ float pair_swap(float v) { return dpp<0x128>(v); }
 
 #define TG_SYNC()                                          \
     do {                                                   \
@@ -316,8 +330,13 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
 #else
     const int ein = e;
 #endif
-    auto CP = [&](int k) { return comp[(size_t)k * N + ein]; };
-    auto PR = [&](int f, int d) { return a.props[((size_t)f * N + ein) * D + d]; };
+    // per-env inputs through 32-bit element offsets from the uniform base
+    // pointers (scalar base + vector offset addressing, no 64-bit address math)
+    const unsigned cbase = (unsigned)ein * M::KC;
+    auto CP = [&](int k) { return comp[cbase + (unsigned)k]; };
+    auto CP4 = [&](int k) { return *reinterpret_cast<const float4 *>(comp + (cbase + (unsigned)k)); };
+    const unsigned ND = (unsigned)N * (unsigned)D, pbase = (unsigned)ein * (unsigned)D;
+    auto PR = [&](int f, int d) { return a.props[(unsigned)f * ND + pbase + (unsigned)d]; };
     const bool lead = sub == 0;
 
     float *root = a.root + (size_t)e * 13;
@@ -375,11 +394,13 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
         stsv(s, o + F_PA, SV{bw - n, bv - F});
     };
     // per-group per-env inputs, prefetched one schedule step ahead
-    auto load_kin = [&](int g, float *x) {   // joint placement (12) + inertia (10)
+    auto load_kin = [&](int g, float *x) {   // joint placement (12) + inertia (10): one 24-float block
 #pragma unroll
-        for (int k = 0; k < 12; ++k) x[k] = CP(CL::xtree(g) + k);
-#pragma unroll
-        for (int k = 0; k < 10; ++k) x[12 + k] = CP(CL::inertia(g) + k);
+        for (int k = 0; k < 6; ++k) {
+            const float4 v = CP4(CL::xtree(g) + 4 * k);
+            x[4 * k] = v.x; x[4 * k + 1] = v.y;
+            if (k < 5) { x[4 * k + 2] = v.z; x[4 * k + 3] = v.w; }
+        }
     };
     auto load_drv = [&](int d, float *x) {   // drive / limit inputs of dof d
         x[0] = PR(TG_PROP_ARMATURE, d);
@@ -389,9 +410,10 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
         x[4] = PR(TG_PROP_EFFORT, d);
         x[5] = PR(TG_PROP_LOWER, d);
         x[6] = PR(TG_PROP_UPPER, d);
-        x[7] = a.pos_tgt[(size_t)e * D + d];
-        x[8] = a.vel_tgt[(size_t)e * D + d];
-        x[9] = a.act ? a.act[(size_t)e * D + d] : 0.f;
+        const unsigned ed = (unsigned)e * (unsigned)D + (unsigned)d;
+        x[7] = a.pos_tgt[ed];
+        x[8] = a.vel_tgt[ed];
+        x[9] = a.act ? a.act[ed] : 0.f;
     };
     // pass 2: the children's contributions of the lane's group, n = the step's
     // largest child count: absent children read the zero block, so every load
@@ -450,18 +472,7 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
             body_bias(0, v0, eye3(), v3(0, 0, 0), gr, rin);
         }
         TG_SYNC();
-        float nk[22];
-        I4 d1 = dsc(0), d2 = M::NSTEP > 1 ? dsc(1) : I4{0, 0, 0, 0};
-        if (d1.x > 0) load_kin(d1.x, nk);
-#pragma unroll 1
-        for (int t = 0; t < M::NSTEP; ++t) {
-            const I4 dc = d1;
-            float ck[22];
-#pragma unroll
-            for (int k = 0; k < 22; ++k) ck[k] = nk[k];
-            d1 = d2;
-            d2 = t + 2 < M::NSTEP ? dsc(t + 2) : I4{0, 0, 0, 0};
-            if (d1.x > 0) load_kin(d1.x, nk);
+        auto body1 = [&](const I4 &dc, const float *ck) {
             const int g = dc.x;
             if (g > 0) {
                 const int o = g * GF, par = dc.y, jt = d_jt(dc);
@@ -495,6 +506,24 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
                 body_bias(g, vg, Rg, Pg, gr, ck + 12);
             }
             TG_SYNC();
+        };
+        // two schedule steps per iteration with ping-pong input buffers (no
+        // register copies); step t + 1's inputs are in flight during step t
+        constexpr I4 Z4{0, 0, 0, 0};
+        float kA[22], kB[22];
+        I4 dA = dsc(0), dB = M::NSTEP > 1 ? dsc(1) : Z4;
+        if (dA.x > 0) load_kin(dA.x, kA);
+#pragma unroll 1
+        for (int t = 0; t < M::NSTEP; t += 2) {
+            if (dB.x > 0) load_kin(dB.x, kB);
+            const I4 dC = t + 2 < M::NSTEP ? dsc(t + 2) : Z4;
+            body1(dA, kA);
+            if (t + 1 >= M::NSTEP) break;
+            if (dC.x > 0) load_kin(dC.x, kA);
+            const I4 dD = t + 3 < M::NSTEP ? dsc(t + 3) : Z4;
+            body1(dB, kB);
+            dA = dC;
+            dB = dD;
         }
         }   // pass 1
         TG_PROF(1)
@@ -834,7 +863,6 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
             // vector in registers; a row's W*lambda is an 8-lane reduction, so
             // every lane computes the same update (no LDS traffic in the sweeps)
             {
-                static_assert(LPE == 8, "sum8 reduces over 8 lanes");
                 constexpr int JL = (K + LPE - 1) / LPE;
                 float wc[K][JL], vf[K], tg[K], onr[K], wd[K], lam[K], my[JL];
 #pragma unroll
@@ -856,7 +884,7 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
                     float part = 0.f;
 #pragma unroll
                     for (int jj = 0; jj < JL; ++jj) part += wc[i][jj] * my[jj];
-                    return vf[i] + sum8(part);
+                    return vf[i] + sum_lanes<LPE>(part);
                 };
                 auto set_lam = [&](int i, float v) {
                     lam[i] = v;

@@ -38,7 +38,8 @@ def shape_rows(kind: int) -> int:
     return BOX_NORMALS if kind == 1 else 1
 
 
-LANES_PER_ENV = 8   # lanes per env of the tree-parallel step kernel (csrc/step_par.h)
+LANES_PER_ENV = 8   # schedule lanes per env of the tree-parallel step kernel (csrc/step_par.h)
+PAIR_MIN_GROUPS = 16   # trees with at least this many groups run on lane pairs (16 lanes per env)
 
 
 def lane_schedule(parent, lanes):
@@ -110,11 +111,16 @@ def emit(m: Model, cname: str) -> str:
         p = [g for g in range(1, G) if anc[c][g]]
         cpaths.append(p + [0] * (maxd - len(p)))
     shape_cg = [cgroups.index(g) for g in sgroup]
-    # 8 lanes x 16 envs per workgroup for every model: Thormang fills a CU's
-    # LDS with 16 envs; for the scooter 8 lanes also beat 2/4 (more Delassus
-    # columns in parallel) and 16 envs beat 8 (measured)
-    LPE, EPB = LANES_PER_ENV, 16
-    sched = lane_schedule(gpar, LPE)
+    # 8 schedule lanes x 16 envs per workgroup for every model: Thormang fills a
+    # CU's LDS with 16 envs; for the scooter 8 lanes also beat 2/4 (more
+    # Delassus columns in parallel) and 16 envs beat 8 (measured).
+    # Large trees (PAIR) run every schedule slot on a lane pair (sub, sub + 8)
+    # that splits each group's update: 16 lanes per env, 4 wavefronts per
+    # workgroup, so 4096 envs put one wavefront on every SIMD.
+    SL, EPB = LANES_PER_ENV, 16
+    PAIR = 1 if G >= PAIR_MIN_GROUPS else 0
+    LPE = SL * (1 + PAIR)
+    sched = lane_schedule(gpar, SL)
     children = [[c for c in range(G) if gpar[c] == g] for g in range(G)]
     # compose: link level below its group root (FK level by level), links per group
     lpar = [int(x) for x in a["link_parent"]]
@@ -136,7 +142,7 @@ def emit(m: Model, cname: str) -> str:
         f"struct {cname} {{",
         f"  static constexpr unsigned long long hash = 0x{d.hash:016x}ULL;",
         f"  static constexpr int NG = {G}, NL = {L}, ND = {D}, NS = {S > 0 and S or 0}, NSA = {max(S, 1)};",
-        f"  static constexpr int KC = {10 * G + 12 * (G - 1) + 12 * S};  // per-env composite floats",
+        f"  static constexpr int KC = {24 * G + 12 * S};  // per-env composite floats (env-major, csrc CompLayout)",
         f"  static constexpr int NROWS = {sum(n + 3 for n in nrows_n)};  // contact rows (normals + 3 friction per shape)",
         f"  static constexpr int parent[{G}] = {_arr(a['group_parent'])};",
         f"  static constexpr int gdof[{G}] = {_arr(gdof)};",
@@ -170,8 +176,8 @@ def emit(m: Model, cname: str) -> str:
         f"  static constexpr int cpath[{max(len(cgroups), 1)}][{maxd}] = "
         f"{_arr([_arr(p) for p in cpaths] or [_arr([0] * maxd)])};",
         f"  static constexpr int shape_cg[{max(S, 1)}] = {_arr(shape_cg or [0])};",
-        f"  static constexpr int LPE = {LPE}, EPB = {EPB}, NSTEP = {len(sched)}, MAXC = {maxc};",
-        f"  static constexpr int sched[{len(sched)}][{LPE}] = {_arr([_arr(r) for r in sched])};",
+        f"  static constexpr int SL = {SL}, PAIR = {PAIR}, LPE = {LPE}, EPB = {EPB}, NSTEP = {len(sched)}, MAXC = {maxc};",
+        f"  static constexpr int sched[{len(sched)}][{SL}] = {_arr([_arr(r) for r in sched])};",
         f"  static constexpr int nchild[{G}] = {_arr([len(c) for c in children])};",
         f"  static constexpr int child[{G}][{maxc}] = {_arr([_arr(c + [-1] * (maxc - len(c))) for c in children])};",
         f"  static constexpr int dof_locked[{D}] = {_arr(a['dof_locked'])};",
