@@ -394,12 +394,26 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
         stsv(s, o + F_PA, SV{bw - n, bv - F});
     };
     // per-group per-env inputs, prefetched one schedule step ahead
-    auto load_kin = [&](int g, float *x) {   // joint placement (12) + inertia (10): one 24-float block
+    auto load_kin = [&](int g, float *x) {   // joint placement (12)
 #pragma unroll
-        for (int k = 0; k < 6; ++k) {
+        for (int k = 0; k < 3; ++k) {
             const float4 v = CP4(CL::xtree(g) + 4 * k);
-            x[4 * k] = v.x; x[4 * k + 1] = v.y;
-            if (k < 5) { x[4 * k + 2] = v.z; x[4 * k + 3] = v.w; }
+            x[4 * k] = v.x; x[4 * k + 1] = v.y; x[4 * k + 2] = v.z; x[4 * k + 3] = v.w;
+        }
+    };
+    // pass 1b: groups sub, sub + LPE, ... of the env (all lanes, no schedule)
+    constexpr int NR1 = (M::NG + LPE - 1) / LPE;
+    auto load_inertia = [&](float (*x)[12]) {   // mass, com, inertia (10 + 2 pad) of the lane's groups
+#pragma unroll
+        for (int r = 0; r < NR1; ++r) {
+            const int g = sub + r * LPE;
+            if (g < M::NG) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const float4 v = CP4(CL::inertia(g) + 4 * k);
+                    x[r][4 * k] = v.x; x[r][4 * k + 1] = v.y; x[r][4 * k + 2] = v.z; x[r][4 * k + 3] = v.w;
+                }
+            }
         }
     };
     auto load_drv = [&](int d, float *x) {   // drive / limit inputs of dof d
@@ -436,9 +450,6 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
             pA = pA + cv[c];
         }
     };
-    float rin[10];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) rin[k] = CP(CL::inertia(0) + k);
     TG_SYNC();
     TG_PROF(0)
 
@@ -466,11 +477,13 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
         // results are intact).  Descriptors run two steps ahead, the cache
         // inputs one step ahead.
         if (!SEPC || cp == 0) {
+        // 1a (schedule forward): root-frame poses and velocities; 1b (every
+        // group at once, LPE lanes wide): rigid inertias and bias forces,
+        // which depend on the group's own pose and velocity only
         const V3 gr = mulT(R, grav);   // gravity in the root frame
-        if (lead) {
-            stsv(s, F_V, v0);
-            body_bias(0, v0, eye3(), v3(0, 0, 0), gr, rin);
-        }
+        float cin[NR1][12];
+        load_inertia(cin);
+        if (lead) stsv(s, F_V, v0);
         TG_SYNC();
         auto body1 = [&](const I4 &dc, const float *ck) {
             const int g = dc.x;
@@ -503,14 +516,13 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
                 const SV Sg = motion_S(jt, v3(Rg.a[2], Rg.a[5], Rg.a[8]), Pg);
                 const SV vg = vp + qdg * Sg;
                 stsv(s, o + F_V, vg);
-                body_bias(g, vg, Rg, Pg, gr, ck + 12);
             }
             TG_SYNC();
         };
         // two schedule steps per iteration with ping-pong input buffers (no
         // register copies); step t + 1's inputs are in flight during step t
         constexpr I4 Z4{0, 0, 0, 0};
-        float kA[22], kB[22];
+        float kA[12], kB[12];
         I4 dA = dsc(0), dB = M::NSTEP > 1 ? dsc(1) : Z4;
         if (dA.x > 0) load_kin(dA.x, kA);
 #pragma unroll 1
@@ -525,6 +537,12 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
             dA = dC;
             dB = dD;
         }
+#pragma unroll
+        for (int r = 0; r < NR1; ++r) {
+            const int g = sub + r * LPE;
+            if (g < M::NG) body_bias(g, ldsv(s, g * GF + F_V), ldR(s, g), ldv3(s, g * GF + F_P), gr, cin[r]);
+        }
+        TG_SYNC();
         }   // pass 1
         TG_PROF(1)
         // ---- pass 2: schedule backward, children contributions gathered
