@@ -71,7 +71,7 @@ struct LE {
 // F_CL: drive-clamp scratch (te, K, effort) between the two solves.
 enum : int {
     F_RT = 0, F_AX = 6, F_P = 9, F_V = 12, F_Q = 18, F_QD = 19, F_IA = 20, F_DINV = 41, F_UU = 42, F_QDS = 43,
-    F_PA = 44, F_U = 50, F_CL = 56, GF = 60
+    F_PA = 44, F_U = 50, F_CL = 56, F_C1 = 59, GF = 60
 };
 
 __device__ __forceinline__ V3 ldv3(const LE &s, int o) { return v3(s(o), s(o + 1), s(o + 2)); }
@@ -545,34 +545,24 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
         TG_SYNC();
         }   // pass 1
         TG_PROF(1)
-        // ---- pass 2: schedule backward, children contributions gathered
-        {
-        float nd[10];
-        I4 d1 = dsc(M::NSTEP - 1), d2 = M::NSTEP > 1 ? dsc(M::NSTEP - 2) : I4{0, 0, 0, 0};
-        if (d1.x > 0) load_drv(d_dof(d1), nd);
-#pragma unroll 1
-        for (int t = M::NSTEP - 1; t >= 0; --t) {
-            const I4 dc = d1;
-            float cd[10];
+        // ---- pass 2a (every group at once, LPE lanes wide): the joint-space
+        // terms that need no articulated inertia -- drive torque and implicit
+        // gain (implicit, or clamped to +-effort on the rerun), effort torque,
+        // limit spring/damper as multiples of D0 = S.I^A.S, velocity-product
+        // acceleration cb -- parked in the group's own pass-2 output slots
+        // (F_U: cb, F_DINV: c0, F_UU: tau, F_QDS: limit torque per D0, F_C1: 1 +
+        // limit gain per D0)
 #pragma unroll
-            for (int k = 0; k < 10; ++k) cd[k] = nd[k];
-            d1 = d2;
-            d2 = t >= 2 ? dsc(t - 2) : I4{0, 0, 0, 0};
-            if (d1.x > 0) load_drv(d_dof(d1), nd);
-            const int g = dc.x;
-            if (g > 0) {
+        for (int r = 0; r < NR1; ++r) {
+            const int g = sub + r * LPE;
+            if (g > 0 && g < M::NG) {
                 const int o = g * GF;
-                SI IA = ldsi(s, o + F_IA);
-                SV pA = ldsv(s, o + F_PA);
-                const SV Sg = ldS(s, g, d_jt(dc));
+                const int d = gi[g * GIW + GI_DOF];
+                float cd[10];
+                load_drv(d, cd);
+                const SV Sg = ldS(s, g, gi[g * GIW + GI_JT]);
                 const SV vg = ldsv(s, o + F_V);
                 const float q = s(o + F_Q), qd = s(o + F_QD), qdd0 = s(o + F_UU);
-                const int smax = d_smax(dc);
-                if (smax == 1) gather(std::integral_constant<int, 1>{}, dc, IA, pA);
-                else if (smax == 2) gather(std::integral_constant<int, 2>{}, dc, IA, pA);
-                else if (smax >= 3) gather(std::integral_constant<int, 3>{}, dc, IA, pA);
-                const SV U = mul(IA, Sg);
-                const float D0 = dot(Sg, U) + cd[0];
                 float Dimp = 0.f, tau = 0.f;
                 const int mode = (int)rintf(cd[1]);
                 const float kp = cd[2], kd = cd[3];
@@ -595,30 +585,58 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
                 } else {
                     if (mode == TG_DOF_MODE_EFFORT && a.act) tau += fminf(fmaxf(cd[9], -eff), eff);
                 }
+                // limit spring + damping (kl = lim_k D0 / h^2, cl = lim_c D0 / h),
+                // damping/implicit terms ramped in past the limit
                 const float lo = cd[5], hi = cd[6];
                 const float qp = q + h * qd;
-                const float kl = a.lim_k * D0 / (h * h), cl = a.lim_c * D0 / h;
-                // limit spring + damping, damping/implicit terms ramped in past the limit
+                float al = 0.f, be = 0.f;
                 if (qp < lo && lo > -1e30f) {
-                    const float r = fminf((lo - qp) * (1.0f / TG_LIMIT_RAMP), 1.0f);
-                    tau += kl * (lo - qp) - r * cl * qd;
-                    Dimp += r * (h * cl + h * h * kl);
+                    const float rr = fminf((lo - qp) * (1.0f / TG_LIMIT_RAMP), 1.0f);
+                    al = a.lim_k / (h * h) * (lo - qp) - rr * a.lim_c / h * qd;
+                    be = rr * (a.lim_c + a.lim_k);
                 } else if (qp > hi && hi < 1e30f) {
-                    const float r = fminf((qp - hi) * (1.0f / TG_LIMIT_RAMP), 1.0f);
-                    tau += kl * (hi - qp) - r * cl * qd;
-                    Dimp += r * (h * cl + h * h * kl);
+                    const float rr = fminf((qp - hi) * (1.0f / TG_LIMIT_RAMP), 1.0f);
+                    al = a.lim_k / (h * h) * (hi - qp) - rr * a.lim_c / h * qd;
+                    be = rr * (a.lim_c + a.lim_k);
                 }
-                const float Dinv = 1.0f / (D0 + Dimp);
-                const float u = tau - dot(Sg, pA);
-                SI Ia = IA;
-                si_sub_outer(Ia, U, Dinv);
-                const SV cb = crm(vg, qd * Sg);   // velocity-product acceleration
-                const SV pa = pA + mul(Ia, cb) + (u * Dinv) * U;
                 if (cp == 0) {
                     s(o + F_CL) = cl0;
                     s(o + F_CL + 1) = cl1;
                     s(o + F_CL + 2) = eff;
                 }
+                // with D0 = S.I^A.S + armature: D = (1 + be) D0 + Dimp, tau + al D0
+                stsv(s, o + F_U, crm(vg, qd * Sg));
+                s(o + F_DINV) = (1.f + be) * cd[0] + Dimp;
+                s(o + F_UU) = tau + al * cd[0];
+                s(o + F_QDS) = al;
+                s(o + F_C1) = 1.f + be;
+            }
+        }
+        TG_SYNC();
+        // ---- pass 2b: schedule backward, children contributions gathered
+        {
+#pragma unroll 1
+        for (int t = M::NSTEP - 1; t >= 0; --t) {
+            const I4 dc = dsc(t);
+            const int g = dc.x;
+            if (g > 0) {
+                const int o = g * GF;
+                SI IA = ldsi(s, o + F_IA);
+                SV pA = ldsv(s, o + F_PA);
+                const SV Sg = ldS(s, g, d_jt(dc));
+                const SV cb = ldsv(s, o + F_U);
+                const float c0 = s(o + F_DINV), tau = s(o + F_UU), al = s(o + F_QDS), c1 = s(o + F_C1);
+                const int smax = d_smax(dc);
+                if (smax == 1) gather(std::integral_constant<int, 1>{}, dc, IA, pA);
+                else if (smax == 2) gather(std::integral_constant<int, 2>{}, dc, IA, pA);
+                else if (smax >= 3) gather(std::integral_constant<int, 3>{}, dc, IA, pA);
+                const SV U = mul(IA, Sg);
+                const float D0 = dot(Sg, U);   // without the armature (folded into c0, tau)
+                const float Dinv = 1.0f / (c1 * D0 + c0);
+                const float u = tau + al * D0 - dot(Sg, pA);
+                SI Ia = IA;
+                si_sub_outer(Ia, U, Dinv);
+                const SV pa = pA + mul(Ia, cb) + (u * Dinv) * U;
                 stsv(s, o + F_U, U);
                 s(o + F_DINV) = Dinv;
                 s(o + F_UU) = u;
