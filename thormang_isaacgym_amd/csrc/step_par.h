@@ -549,8 +549,8 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
         // terms that need no articulated inertia -- drive torque and implicit
         // gain (implicit, or clamped to +-effort on the rerun), effort torque,
         // limit spring/damper as multiples of D0 = S.I^A.S, velocity-product
-        // acceleration cb -- parked in the group's own pass-2 output slots
-        // (F_U: cb, F_DINV: c0, F_UU: tau, F_QDS: limit torque per D0, F_C1: 1 +
+        // acceleration cb -- parked in the group's own slots (F_V: cb, which
+        // pass 3 reads too; F_DINV: c0, F_UU: tau, F_QDS: limit torque per D0, F_C1: 1 +
         // limit gain per D0)
 #pragma unroll
         for (int r = 0; r < NR1; ++r) {
@@ -560,8 +560,6 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
                 const int d = gi[g * GIW + GI_DOF];
                 float cd[10];
                 load_drv(d, cd);
-                const SV Sg = ldS(s, g, gi[g * GIW + GI_JT]);
-                const SV vg = ldsv(s, o + F_V);
                 const float q = s(o + F_Q), qd = s(o + F_QD), qdd0 = s(o + F_UU);
                 float Dimp = 0.f, tau = 0.f;
                 const int mode = (int)rintf(cd[1]);
@@ -605,7 +603,9 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
                     s(o + F_CL + 2) = eff;
                 }
                 // with D0 = S.I^A.S + armature: D = (1 + be) D0 + Dimp, tau + al D0
-                stsv(s, o + F_U, crm(vg, qd * Sg));
+                // cb replaces v (dead after pass 1b) in F_V; on a SEPC rerun pass 1
+                // was not rerun and F_V already holds cb
+                if (!SEPC || cp == 0) stsv(s, o + F_V, crm(ldsv(s, o + F_V), qd * ldS(s, g, gi[g * GIW + GI_JT])));
                 s(o + F_DINV) = (1.f + be) * cd[0] + Dimp;
                 s(o + F_UU) = tau + al * cd[0];
                 s(o + F_QDS) = al;
@@ -624,7 +624,7 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
                 SI IA = ldsi(s, o + F_IA);
                 SV pA = ldsv(s, o + F_PA);
                 const SV Sg = ldS(s, g, d_jt(dc));
-                const SV cb = ldsv(s, o + F_U);
+                const SV cb = ldsv(s, o + F_V);
                 const float c0 = s(o + F_DINV), tau = s(o + F_UU), al = s(o + F_QDS), c1 = s(o + F_C1);
                 const int smax = d_smax(dc);
                 if (smax == 1) gather(std::integral_constant<int, 1>{}, dc, IA, pA);
@@ -684,12 +684,11 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
             const int g = dc.x;
             if (g > 0) {
                 const int o = g * GF;
-                const SV apar = ldsv(s, ac_s(dc.y));
-                const SV vg = ldsv(s, o + F_V), Ug = ldsv(s, o + F_U);
+                const SV apar = ldsv(s, ac_s(dc.y)), cb = ldsv(s, o + F_V), Ug = ldsv(s, o + F_U);
                 const SV Sg = ldS(s, g, d_jt(dc));
                 const float qd = s(o + F_QD), uu = s(o + F_UU), dinv = s(o + F_DINV);
                 const float te = s(o + F_CL), K = s(o + F_CL + 1), eff = s(o + F_CL + 2);
-                const SV ap = apar + crm(vg, qd * Sg);
+                const SV ap = apar + cb;   // cb: pass 2a
                 const float qdd = (uu - dot(Ug, ap)) * dinv;
                 stsv(s, ac_s(g), ap + qdd * Sg);
                 s(o + F_QDS) = qd + h * qdd;
