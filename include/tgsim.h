@@ -195,11 +195,13 @@ int tg_sync(tg_sim *sim);
 const char *tg_last_error(void);
 uint64_t tg_compiled_model_hashes(uint64_t *out, int32_t cap); /* returns count */
 
-/* Benchmark instrumentation (no reference counterpart): while enabled,
- * tg_simulate brackets the articulation step kernel launch with HIP events on
- * the sim stream; tg_read_kernel_timing waits for the recorded launches and
- * returns (and resets) the summed kernel time and the launch count. */
-int tg_set_kernel_timing(tg_sim *sim, int32_t enable);
+/* Benchmark instrumentation (no reference counterpart): with period > 0,
+ * tg_simulate brackets every period-th articulation step kernel launch with HIP
+ * events on the sim stream (an event pair serialises the queue for ~5 us each
+ * side, so sampling keeps the instrumented run's throughput honest); 0 turns
+ * timing off.  tg_read_kernel_timing waits for the recorded launches and
+ * returns (and resets) the summed kernel time and the timed launch count. */
+int tg_set_kernel_timing(tg_sim *sim, int32_t period);
 int tg_read_kernel_timing(tg_sim *sim, double *total_ms, int64_t *launches);
 
 #ifdef __cplusplus

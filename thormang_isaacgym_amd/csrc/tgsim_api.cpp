@@ -58,7 +58,8 @@ struct tg_sim {
     float hf_hs = 0.f, hf_vs = 0.f, hf_ox = 0.f, hf_oy = 0.f, hf_mu = 0.f;
     std::vector<void *> allocs;
     // kernel timing (tg_set_kernel_timing): event pairs recorded, not yet read
-    bool timing = false;
+    int timing = 0;          // period (0: off)
+    int64_t timing_count = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending, ev_free;
     double timed_ms = 0.0;
     int64_t timed_launches = 0;
@@ -392,7 +393,7 @@ int tg_simulate(tg_sim *s) {
     if (int rc = check_sim(s)) return rc;
     tg::StepArgs a = step_args(s);
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
-    if (s->timing) {
+    if (s->timing > 0 && s->timing_count++ % s->timing == 0) {
         if (!s->ev_free.empty()) {
             ev = s->ev_free.back();
             s->ev_free.pop_back();
@@ -416,9 +417,11 @@ int tg_rigid_body_states(tg_sim *s, float *out) {
     return TG_OK;
 }
 
-int tg_set_kernel_timing(tg_sim *s, int32_t enable) {
+int tg_set_kernel_timing(tg_sim *s, int32_t period) {
     if (int rc = check_sim(s)) return rc;
-    s->timing = enable != 0;
+    if (period < 0) return fail(TG_ERR_ARG, "tg_set_kernel_timing: negative period");
+    s->timing = period;
+    s->timing_count = 0;
     return TG_OK;
 }
 

@@ -156,9 +156,10 @@ class Sim:
     def sync(self):
         check(lib().tg_sync(self._h), "sync")
 
-    def set_kernel_timing(self, enable: bool):
-        """Bracket every articulation step kernel with HIP events on the sim stream."""
-        check(lib().tg_set_kernel_timing(self._h, int(bool(enable))), "set_kernel_timing")
+    def set_kernel_timing(self, period: int):
+        """Bracket every ``period``-th articulation step kernel launch with HIP
+        events on the sim stream (``True``/1: every launch, 0/``False``: off)."""
+        check(lib().tg_set_kernel_timing(self._h, int(period)), "set_kernel_timing")
 
     def read_kernel_timing(self):
         """(total kernel ms, launches) since the last read; waits for the recorded launches."""
