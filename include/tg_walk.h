@@ -81,6 +81,14 @@ typedef struct tg_walk_buffers {
 
 /* actions [N,D] -> clamp -> PD position targets default + scale*a */
 int tg_walk_pre_physics(tg_sim *sim, const tg_walk_params *p, const tg_walk_buffers *b, const float *actions);
+/* One VecTask.step of the task (tasks/base/vec_task.py:313-359 with
+ * pre_physics_step, control_freq_inv = n_simulate simulate calls and
+ * post_physics_step): the same results as tg_walk_pre_physics +
+ * [tg_apply_body_forces(body_force) when b->body_force] + n_simulate x
+ * tg_simulate + tg_walk_post_physics, with the pre-physics work fused into the
+ * first simulate's compose launch (one launch fewer per step). */
+int tg_walk_step(tg_sim *sim, const tg_walk_params *p, const tg_walk_buffers *b, const float *actions,
+                 int32_t n_simulate, const float *reset_draws, const float *push_draws, uint64_t counter);
 /* progress, masked resets, observation, reward, termination, timeouts, pushes */
 int tg_walk_post_physics(tg_sim *sim, const tg_walk_params *p, const tg_walk_buffers *b, const float *reset_draws,
                          const float *push_draws, uint64_t counter);

@@ -91,3 +91,28 @@ def test_gpu_walk_dr_16384_envs():
         resets += int(reset.sum())
     assert torch.isfinite(obs["obs"]).all() and torch.isfinite(rew).all() and torch.isfinite(env.root_tensor).all()
     assert resets > 0
+
+
+def test_gpu_walk_fused_step_equals_separate_calls():
+    """tg_walk_step (pre-physics fused into the compose launch) gives the
+    bit-identical results of tg_walk_pre_physics + tg_simulate +
+    tg_walk_post_physics (the VecTask.step sequence), resets and pushes
+    included."""
+    _cuda()
+    import thormang_isaacgym_amd as tia
+    from thormang_isaacgym_amd.tasks.base.vec_task import VecTask
+    for task in ("ThormangWalk", "ThormangWalkDR"):
+        envs = [tia.make(seed=11, task=task, num_envs=256, sim_device="cuda:0", rl_device="cuda:0")
+                for _ in range(2)]
+        g = torch.Generator(device="cuda:0").manual_seed(5)
+        for _ in range(120):
+            a = torch.rand(256, 33, device="cuda:0", generator=g) * 2.4 - 1.2   # some beyond the clip
+            envs[0].step(a)
+            VecTask.step(envs[1], a)
+            torch.cuda.synchronize()
+            for name in ("obs_buf", "rew_buf", "reset_buf", "progress_buf", "actions", "root_tensor"):
+                x, y = getattr(envs[0], name), getattr(envs[1], name)
+                assert torch.equal(x, y), (task, name)
+            assert torch.equal(envs[0].sim.dof_state, envs[1].sim.dof_state), task
+            assert torch.equal(envs[0].sim.dof_pos_target, envs[1].sim.dof_pos_target), task
+        assert int(envs[0].reset_buf.sum()) >= 0

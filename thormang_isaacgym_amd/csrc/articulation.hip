@@ -85,9 +85,23 @@ template <int NV> __device__ __forceinline__ void wave_sum_n(float *v) {
 // is N / COMPOSE_WPB workgroups (most waves exit at once), not N
 constexpr int COMPOSE_WPB = 8;
 
+// Prologue (tg_walk_step): the walk task's pre_physics_step fused into the
+// compose launch that precedes every step kernel -- the same fp32 operations
+// as walk_task.hip walk_pre_kernel (no contraction: default + scale * a).
+__device__ __forceinline__ void target_prologue(const StepArgs &a, int e, int lane) {
+#pragma clang fp contract(off)
+    if (lane >= a.D) return;
+    const unsigned i = (unsigned)e * (unsigned)a.D + (unsigned)lane;
+    const float x = a.pm_actions[i];
+    const float c = x < -a.pm_clip ? -a.pm_clip : (x > a.pm_clip ? a.pm_clip : x);
+    a.pm_act_out[i] = c;
+    a.pm_tgt_out[i] = a.pm_default[lane] + a.pm_scale * c;
+}
+
 template <class M> __global__ __launch_bounds__(64 * COMPOSE_WPB) void compose_kernel(StepArgs a) {
     const int wv = threadIdx.x / 64;
     const int e = blockIdx.x * COMPOSE_WPB + wv;
+    if (a.pm_actions && e < a.N) target_prologue(a, e, threadIdx.x % 64);
     if (e >= a.N || !a.dirty[e]) return;
     TG_CPROF_INIT
     using CL = CompLayout<M>;
@@ -492,7 +506,7 @@ extern "C" int tg_cprof_read(unsigned long long *out, int n) {
     return 0;
 }
 extern "C" int tg_prof_read(unsigned long long *out, int n) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tg_prof_acc), sizeof(unsigned long long) * (n < 16 ? n : 16)) != hipSuccess)
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tg_prof_acc), sizeof(unsigned long long) * (n < 24 ? n : 24)) != hipSuccess)
         return -1;
     return 0;
 }

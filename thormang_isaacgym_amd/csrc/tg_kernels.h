@@ -11,6 +11,8 @@
 
 namespace tg {
 
+constexpr int TG_PM_MAX_DOF = 64;   // prologue lanes: one wavefront per env, lane = dof
+
 struct StepArgs {
     int N, D;
     float h;
@@ -32,6 +34,14 @@ struct StepArgs {
     const float *hf;          // terrain heights [rows, cols] or null (z = 0 plane)
     int hf_rows, hf_cols;
     float hf_hs, hf_vs, hf_ox, hf_oy, hf_mu;
+    // optional prologue of the compose launch (tg_walk_step): the task's
+    // actions -> clamp(+-pm_clip) -> PD position targets pm_default + pm_scale*a
+    // (null pm_actions: none)
+    const float *pm_actions;  // [N,D]
+    float *pm_act_out;        // [N,D] clamped actions
+    float *pm_tgt_out;        // [N,D] position targets
+    float pm_scale, pm_clip;
+    float pm_default[TG_PM_MAX_DOF];
 };
 
 // ev_begin / ev_end (optional) are recorded around the step kernel itself

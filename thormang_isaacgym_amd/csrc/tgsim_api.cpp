@@ -389,9 +389,8 @@ int tg_set_heightfield(tg_sim *s, const float *heights, int32_t rows, int32_t co
     return TG_OK;
 }
 
-int tg_simulate(tg_sim *s) {
-    if (int rc = check_sim(s)) return rc;
-    tg::StepArgs a = step_args(s);
+// compose (+ optional prologue in a) and the step kernel of one simulate call
+static int simulate_args(tg_sim *s, const tg::StepArgs &a) {
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     if (s->timing > 0 && s->timing_count++ % s->timing == 0) {
         if (!s->ev_free.empty()) {
@@ -407,6 +406,11 @@ int tg_simulate(tg_sim *s) {
     s->forces_pending = false;   // apply_rigid_body_force_tensors acts for one simulate call
     if (rc) return fail(rc, "step launch failed: %s", hipGetErrorString(hipGetLastError()));
     return TG_OK;
+}
+
+int tg_simulate(tg_sim *s) {
+    if (int rc = check_sim(s)) return rc;
+    return simulate_args(s, step_args(s));
 }
 
 int tg_rigid_body_states(tg_sim *s, float *out) {
@@ -497,6 +501,33 @@ int tg_walk_pre_physics(tg_sim *s, const tg_walk_params *p, const tg_walk_buffer
     if (int rc = check_walk(s, p, b)) return rc;
     if (!actions) return fail(TG_ERR_ARG, "walk: null actions");
     if (int rc = tg::launch_walk_pre(*p, *b, actions, s->stream)) return fail(rc, "launch failed");
+    return TG_OK;
+}
+
+int tg_walk_step(tg_sim *s, const tg_walk_params *p, const tg_walk_buffers *b, const float *actions,
+                 int32_t n_simulate, const float *reset_draws, const float *push_draws, uint64_t counter) {
+    if (int rc = check_walk(s, p, b)) return rc;
+    if (!actions || !b->actions || !b->pos_target) return fail(TG_ERR_ARG, "walk step: null actions / targets");
+    if (n_simulate < 1) return fail(TG_ERR_ARG, "walk step: n_simulate %d < 1", n_simulate);
+    if (p->num_dof > tg::TG_PM_MAX_DOF) return fail(TG_ERR_ARG, "walk step: num_dof %d > %d", p->num_dof, tg::TG_PM_MAX_DOF);
+    if (b->body_force) {   // pre_physics_step: apply_rigid_body_force_tensors(body_force)
+        if (int rc = copy_full(s, s->force, b->body_force, (size_t)s->N * s->G * 6)) return rc;
+        s->forces_pending = true;
+    }
+    for (int i = 0; i < n_simulate; ++i) {
+        tg::StepArgs a = step_args(s);
+        if (i == 0) {   // pre_physics_step fused into the first compose launch
+            a.pm_actions = actions;
+            a.pm_act_out = b->actions;
+            a.pm_tgt_out = b->pos_target;
+            a.pm_scale = p->action_scale;
+            a.pm_clip = p->clip_actions;
+            for (int d = 0; d < p->num_dof; ++d) a.pm_default[d] = p->default_pos[d];
+        }
+        if (int rc = simulate_args(s, a)) return rc;
+    }
+    if (int rc = tg::launch_walk_post(*p, *b, reset_draws, push_draws, counter, s->stream))
+        return fail(rc, "launch failed");
     return TG_OK;
 }
 

@@ -126,12 +126,17 @@ class ThormangWalk(VecTask):
             out[i] = self.draw_source.uniform(4 + 2 * D)
         return out
 
+    def _post_draws(self):
+        """Replay draws of the coming post_physics_step (None: in-kernel Philox)."""
+        if self.draw_source is None:
+            return None, None
+        ids = self.reset_buf.nonzero(as_tuple=False).squeeze(-1).cpu().numpy()
+        rd = self._dev(self._reset_draws(ids))
+        pd = self._dev(self.draw_source.uniform(3 * self.num_envs).reshape(self.num_envs, 3))
+        return rd, pd
+
     def post_physics_step(self):
-        rd = pd = None
-        if self.draw_source is not None:
-            ids = self.reset_buf.nonzero(as_tuple=False).squeeze(-1).cpu().numpy()
-            rd = self._dev(self._reset_draws(ids))
-            pd = self._dev(self.draw_source.uniform(3 * self.num_envs).reshape(self.num_envs, 3))
+        rd, pd = self._post_draws()
         check(lib().tg_walk_post_physics(self.sim.handle, C.byref(self.params), C.byref(self._bufs), _p(rd), _p(pd),
                                          self._counter()), "tg_walk_post_physics")
         self._keep_post = (rd, pd)
@@ -139,10 +144,16 @@ class ThormangWalk(VecTask):
     def step(self, actions):
         if self.dr_randomizations.get("actions", None) or self.dr_randomizations.get("observations", None):
             return super().step(actions)
-        self.pre_physics_step(actions)
-        for _ in range(self.control_freq_inv):
-            self.simulate()
-        self.post_physics_step()
+        # pre_physics_step + control_freq_inv x simulate + post_physics_step in
+        # one library call (tg_walk_step: the pre-physics work rides in the
+        # first simulate's compose launch); reset_buf is unchanged until the
+        # post kernel, so the replay draws are taken first
+        a = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        rd, pd = self._post_draws()
+        check(lib().tg_walk_step(self.sim.handle, C.byref(self.params), C.byref(self._bufs), _p(a),
+                                 self.control_freq_inv, _p(rd), _p(pd), self._counter()), "tg_walk_step")
+        self.frame_count += self.control_freq_inv
+        self._keep, self._keep_post = a, (rd, pd)
         self.extras["time_outs"] = self.timeout_buf
         self.obs_dict["obs"] = self.obs_buf
         return self.obs_dict, self.rew_buf, self.reset_buf, self.extras
