@@ -35,99 +35,130 @@ __device__ __forceinline__ float walk_draw(const tg_walk_params &p, const float 
     return u01(c);
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
-    return v;
+// sum over the wavefront, returned to every lane: DPP within each 16-lane row
+// (half-mirror, quad swaps, row rotate by 8), then the four row totals
+template <int CTRL> __device__ __forceinline__ float dppw(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_total(float v) {
+    v += dppw<0x141>(v);
+    v += dppw<0x4E>(v);
+    v += dppw<0xB1>(v);
+    v += dppw<0x128>(v);
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return (r0 + r1) + (r2 + r3);
 }
 
 // One wavefront per env: lane d handles dof d (reset, dof observations, the
 // per-dof reward sums); lane 0 the root, commands, reward and termination.
+// Every input of the env (the lane's dof, the root, the commands) is read in
+// one batch with the progress / reset flags, so the wave pays one memory
+// latency; a reset env then replaces them with the freshly drawn values.
 __device__ void walk_env(const tg_walk_params &p, const tg_walk_buffers &b, int e, bool reset, int64_t prog,
                          const float *reset_draws, uint32_t c_lo, uint32_t c_hi) {
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x;   // blockDim.x == 64 >= num_dof (TG_WALK_MAX_DOF)
     const int D = p.num_dof;
     float *root = b.root + 13 * (size_t)e;
     float *o = b.obs_buf + (size_t)p.num_obs * e;
     const float co = p.clip_obs;
+    const bool dl = lane < D;
+    const size_t i = (size_t)e * D + lane;
+    float q = 0.0f, qd = 0.0f, a = 0.0f, la = 0.0f, pt = 0.0f;
+    float rt[13], cmd[3];
+    if (dl) {   // issued before the reset flag is known (a reset env overwrites them)
+        pt = b.pos_target[i];
+        q = b.dof_state[2 * i];
+        qd = b.dof_state[2 * i + 1];
+        a = b.actions[i];
+        la = b.last_actions[i];
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 13; ++k) rt[k] = root[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) cmd[k] = b.commands[3 * (size_t)e + k];
+    }
     if (reset) {
-        for (int d = lane; d < D; d += 64) {
-            const size_t i = (size_t)e * D + d;
-            b.dof_state[2 * i] = p.default_pos[d] + (walk_draw(p, reset_draws, e, 4 + d, c_lo, c_hi) * 2.0f - 1.0f) * p.joint_noise;
-            b.dof_state[2 * i + 1] = 0.1f * (walk_draw(p, reset_draws, e, 4 + D + d, c_lo, c_hi) * 2.0f - 1.0f);
-            b.last_actions[i] = 0.0f;
+        if (dl) {
+            q = p.default_pos[lane] + (walk_draw(p, reset_draws, e, 4 + lane, c_lo, c_hi) * 2.0f - 1.0f) * p.joint_noise;
+            qd = 0.1f * (walk_draw(p, reset_draws, e, 4 + D + lane, c_lo, c_hi) * 2.0f - 1.0f);
+            b.dof_state[2 * i] = q;
+            b.dof_state[2 * i + 1] = qd;
             b.actions[i] = 0.0f;
+            a = la = 0.0f;
         }
         if (lane == 0) {
             float r[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) r[k] = walk_draw(p, reset_draws, e, k, c_lo, c_hi);
-            b.commands[3 * (size_t)e + 0] = p.cmd_vx[0] + r[0] * (p.cmd_vx[1] - p.cmd_vx[0]);
-            b.commands[3 * (size_t)e + 1] = p.cmd_vy[0] + r[1] * (p.cmd_vy[1] - p.cmd_vy[0]);
-            b.commands[3 * (size_t)e + 2] = p.cmd_wz[0] + r[2] * (p.cmd_wz[1] - p.cmd_wz[0]);
+            cmd[0] = p.cmd_vx[0] + r[0] * (p.cmd_vx[1] - p.cmd_vx[0]);
+            cmd[1] = p.cmd_vy[0] + r[1] * (p.cmd_vy[1] - p.cmd_vy[0]);
+            cmd[2] = p.cmd_wz[0] + r[2] * (p.cmd_wz[1] - p.cmd_wz[0]);
             const float yaw = (r[3] * 2.0f - 1.0f) * W_PI;
             const float *tpl = b.root_reset + 13 * (size_t)e;
-            root[0] = tpl[0];
-            root[1] = tpl[1];
-            root[2] = p.spawn_height;
-            root[3] = 0.0f;
-            root[4] = 0.0f;
-            root[5] = sinf(0.5f * yaw);
-            root[6] = cosf(0.5f * yaw);
+            rt[0] = tpl[0];
+            rt[1] = tpl[1];
+            rt[2] = p.spawn_height;
+            rt[3] = 0.0f;
+            rt[4] = 0.0f;
+            rt[5] = sinf(0.5f * yaw);
+            rt[6] = cosf(0.5f * yaw);
 #pragma unroll
-            for (int k = 7; k < 13; ++k) root[k] = 0.0f;
+            for (int k = 7; k < 13; ++k) rt[k] = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) b.commands[3 * (size_t)e + k] = cmd[k];
+#pragma unroll
+            for (int k = 0; k < 13; ++k) root[k] = rt[k];
             b.progress_buf[e] = 0;
         }
     }
     // dof observations and the per-dof reward terms
     float rate = 0.0f, vel2 = 0.0f, tq = 0.0f;
-    const float *ds = b.dof_state + 2 * (size_t)e * D;
-    for (int d = lane; d < D; d += 64) {
-        const size_t i = (size_t)e * D + d;
-        const float q = ds[2 * d], qd = ds[2 * d + 1];
-        const float a = b.actions[i], la = b.last_actions[i];
-        o[13 + d] = clampw((q - p.default_pos[d]) * p.dof_pos_scale, -co, co);
-        o[13 + D + d] = clampw(qd * p.dof_vel_scale, -co, co);
-        o[13 + 2 * D + d] = clampw(a, -co, co);
-        rate += (a - la) * (a - la);
-        vel2 += qd * qd;
-        const float t = p.stiffness[d] * (b.pos_target[i] - q);
-        tq += t * t;
+    if (dl) {
+        o[13 + lane] = clampw((q - p.default_pos[lane]) * p.dof_pos_scale, -co, co);
+        o[13 + D + lane] = clampw(qd * p.dof_vel_scale, -co, co);
+        o[13 + 2 * D + lane] = clampw(a, -co, co);
+        rate = (a - la) * (a - la);
+        vel2 = qd * qd;
+        const float tt = p.stiffness[lane] * (pt - q);
+        tq = tt * tt;
         b.last_actions[i] = a;
     }
-    rate = wave_sum(rate);
-    vel2 = wave_sum(vel2);
-    tq = wave_sum(tq);
+    rate = wave_total(rate);
+    vel2 = wave_total(vel2);
+    tq = wave_total(tq);
     if (lane != 0) return;
-    const float x = root[3], y = root[4], z = root[5], w = root[6];
+    const float x = rt[3], y = rt[4], z = rt[5], w = rt[6];
     const float R[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w),
                         2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w),
                         2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)};
     float vb[3], wb[3], gb[3];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        vb[i] = R[i] * root[7] + R[3 + i] * root[8] + R[6 + i] * root[9];
-        wb[i] = R[i] * root[10] + R[3 + i] * root[11] + R[6 + i] * root[12];
-        gb[i] = -R[6 + i];
+    for (int k = 0; k < 3; ++k) {
+        vb[k] = R[k] * rt[7] + R[3 + k] * rt[8] + R[6 + k] * rt[9];
+        wb[k] = R[k] * rt[10] + R[3 + k] * rt[11] + R[6 + k] * rt[12];
+        gb[k] = -R[6 + k];
     }
-    const float *cmd = b.commands + 3 * (size_t)e;
-    o[0] = clampw(root[2], -co, co);
+    o[0] = clampw(rt[2], -co, co);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        o[1 + i] = clampw(vb[i] * p.lin_vel_scale, -co, co);
-        o[4 + i] = clampw(wb[i] * p.ang_vel_scale, -co, co);
-        o[7 + i] = clampw(gb[i], -co, co);
+    for (int k = 0; k < 3; ++k) {
+        o[1 + k] = clampw(vb[k] * p.lin_vel_scale, -co, co);
+        o[4 + k] = clampw(wb[k] * p.ang_vel_scale, -co, co);
+        o[7 + k] = clampw(gb[k], -co, co);
     }
     o[10] = clampw(cmd[0] * p.lin_vel_scale, -co, co);
     o[11] = clampw(cmd[1] * p.lin_vel_scale, -co, co);
     o[12] = clampw(cmd[2] * p.ang_vel_scale, -co, co);
     const float lin_err = (cmd[0] - vb[0]) * (cmd[0] - vb[0]) + (cmd[1] - vb[1]) * (cmd[1] - vb[1]);
     const float ang_err = (cmd[2] - wb[2]) * (cmd[2] - wb[2]);
-    const float dz = root[2] - p.target_height;
+    const float dz = rt[2] - p.target_height;
     float rew = p.rew_lin_vel_xy * expf(-lin_err / 0.25f) + p.rew_ang_vel_z * expf(-ang_err / 0.25f) +
                 p.rew_upright * (-gb[2]) + p.rew_alive + p.rew_height * expf(-dz * dz / 0.01f) +
                 p.rew_action_rate * rate + p.rew_dof_vel * vel2 + p.rew_torque * tq;
-    const bool fall = (root[2] < p.termination_height) || (-gb[2] < p.termination_up);
+    const bool fall = (rt[2] < p.termination_height) || (-gb[2] < p.termination_up);
     if (fall) rew += p.rew_termination;
     const bool rs = fall || prog >= p.max_episode_length - 1;
     b.rew_buf[e] = rew;
