@@ -28,11 +28,20 @@ def main():
     for _ in range(20):
         env.step(torch.rand(4096, env.num_actions, device="cuda:0", generator=g) * 2 - 1)
     torch.cuda.synchronize()
-    buf = (C.c_ulonglong * 16)()
-    L.tg_prof_read(buf, 16)
-    tot = sum(buf[:len(NAMES)])
-    for n, v in zip(NAMES, buf):
+    buf = (C.c_ulonglong * 24)()
+    L.tg_prof_read(buf, 24)
+    # sub-sections [16..] are cut out of the section that follows them
+    sec = list(buf[:len(NAMES)])
+    sec[1] += buf[16]
+    sec[2] += buf[17] + buf[18]
+    tot = sum(sec)
+    subs = {1: [("1a schedule fwd", 16), ("1b all groups", None)],
+            2: [("2a all groups", 17), ("2b schedule bwd", 18), ("root solve", None)]}
+    for i, (n, v) in enumerate(zip(NAMES, sec)):
         print(f"{n:14s} {v / tot * 100:6.2f} %  {v:14d}")
+        for sn, k in subs.get(i, []):
+            sv = buf[k] if k is not None else buf[i]
+            print(f"   {sn:16s} {sv / tot * 100:6.2f} %")
     L.tg_cprof_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
     cb = (C.c_ulonglong * 8)()
     L.tg_cprof_read(cb, 8)

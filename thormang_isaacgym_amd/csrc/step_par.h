@@ -476,27 +476,11 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
         // ---- pass 1: root, then the schedule forward (SEPC: not rerun, its
         // results are intact).  Descriptors run two steps ahead, the cache
         // inputs one step ahead.
-#ifdef TG_AB_DRV
-        float cdall[NR1][10];
-#pragma unroll
-        for (int r = 0; r < NR1; ++r) {
-            const int g = min(max(sub + r * LPE, 1), M::NG - 1);
-            load_drv(gi[g * GIW + GI_DOF], cdall[r]);
-        }
-#endif
         if (!SEPC || cp == 0) {
         // 1a (schedule forward): root-frame poses and velocities; 1b (every
         // group at once, LPE lanes wide): rigid inertias and bias forces,
         // which depend on the group's own pose and velocity only
         const V3 gr = mulT(R, grav);   // gravity in the root frame
-#ifdef TG_AB_KALL
-        float kall[M::NSTEP][12];
-#pragma unroll
-        for (int t = 0; t < M::NSTEP; ++t) {
-            const I4 d = dsc(t);
-            if (d.x > 0) load_kin(d.x, kall[t]);
-        }
-#endif
         float cin[NR1][12];
         load_inertia(cin);
         if (lead) stsv(s, F_V, v0);
@@ -535,10 +519,6 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
             }
             TG_SYNC();
         };
-#ifdef TG_AB_KALL
-#pragma unroll
-        for (int t = 0; t < M::NSTEP; ++t) body1(dsc(t), kall[t]);
-#else
         // two schedule steps per iteration with ping-pong input buffers (no
         // register copies); step t + 1's inputs are in flight during step t
         constexpr I4 Z4{0, 0, 0, 0};
@@ -557,7 +537,6 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
             dA = dC;
             dB = dD;
         }
-#endif
         TG_PROF(16)
 #pragma unroll
         for (int r = 0; r < NR1; ++r) {
@@ -580,12 +559,8 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
             if (g > 0 && g < M::NG) {
                 const int o = g * GF;
                 const int d = gi[g * GIW + GI_DOF];
-#ifdef TG_AB_DRV
-                const float *cd = cdall[r];
-#else
                 float cd[10];
                 load_drv(d, cd);
-#endif
                 const float q = s(o + F_Q), qd = s(o + F_QD), qdd0 = s(o + F_UU);
                 float Dimp = 0.f, tau = 0.f;
                 const int mode = (int)rintf(cd[1]);

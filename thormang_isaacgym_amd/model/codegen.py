@@ -39,7 +39,8 @@ def shape_rows(kind: int) -> int:
 
 
 LANES_PER_ENV = 8   # schedule lanes per env of the tree-parallel step kernel (csrc/step_par.h)
-PAIR_MIN_GROUPS = 16   # trees with at least this many groups run on lane pairs (16 lanes per env)
+# trees with at least this many groups run on lane pairs (16 lanes per env)
+PAIR_MIN_GROUPS = int(os.environ.get("TG_PAIR_MIN_GROUPS", "16"))
 
 
 def lane_schedule(parent, lanes):
