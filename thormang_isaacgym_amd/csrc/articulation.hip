@@ -101,8 +101,9 @@ __device__ __forceinline__ void target_prologue(const StepArgs &a, int e, int la
 template <class M> __global__ __launch_bounds__(64 * COMPOSE_WPB) void compose_kernel(StepArgs a) {
     const int wv = threadIdx.x / 64;
     const int e = blockIdx.x * COMPOSE_WPB + wv;
+    const bool dirty = e < a.N && a.dirty[e] != 0;   // read before the prologue: one memory latency
     if (a.pm_actions && e < a.N) target_prologue(a, e, threadIdx.x % 64);
-    if (e >= a.N || !a.dirty[e]) return;
+    if (!dirty) return;
     TG_CPROF_INIT
     using CL = CompLayout<M>;
     static_assert(M::NL <= 64 && M::NG <= 64 && M::NS <= 64, "compose: one lane per link / group / shape");

@@ -519,23 +519,23 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
             }
             TG_SYNC();
         };
-        // two schedule steps per iteration with ping-pong input buffers (no
-        // register copies); step t + 1's inputs are in flight during step t
-        constexpr I4 Z4{0, 0, 0, 0};
-        float kA[12], kB[12];
-        I4 dA = dsc(0), dB = M::NSTEP > 1 ? dsc(1) : Z4;
-        if (dA.x > 0) load_kin(dA.x, kA);
+        // one schedule step per iteration; step t + 1's inputs are loaded
+        // before step t runs and reach it through the loop back-edge, so the
+        // compiler cannot sink the load into the step that consumes it (which
+        // exposed the full L2 latency on every step).  The loads are
+        // unconditional (idle lanes read group 0's row).
+        float kc[12], kn[12];
+        I4 dA = dsc(0), dB = M::NSTEP > 1 ? dsc(1) : I4{0, 0, 0, 0};
+        load_kin(dA.x, kc);
 #pragma unroll 1
-        for (int t = 0; t < M::NSTEP; t += 2) {
-            if (dB.x > 0) load_kin(dB.x, kB);
-            const I4 dC = t + 2 < M::NSTEP ? dsc(t + 2) : Z4;
-            body1(dA, kA);
-            if (t + 1 >= M::NSTEP) break;
-            if (dC.x > 0) load_kin(dC.x, kA);
-            const I4 dD = t + 3 < M::NSTEP ? dsc(t + 3) : Z4;
-            body1(dB, kB);
-            dA = dC;
-            dB = dD;
+        for (int t = 0; t < M::NSTEP; ++t) {
+            load_kin(dB.x, kn);
+            const I4 dC = t + 2 < M::NSTEP ? dsc(t + 2) : I4{0, 0, 0, 0};
+            body1(dA, kc);
+#pragma unroll
+            for (int k = 0; k < 12; ++k) kc[k] = kn[k];
+            dA = dB;
+            dB = dC;
         }
         TG_PROF(16)
 #pragma unroll
