@@ -52,6 +52,14 @@ def kernel_bytes_per_env(task_name: str, env) -> int:
     kc = 10 * G + 12 * (G - 1) + 12 * S
     read = 13 * 4 + na * 2 * 4 + na * 2 * 4 + na * 8 * 4 + nl * 2 * 4 + kc * 4 + S * 4 + 1
     write = 13 * 4 + D * 2 * 4
+    if task_name.startswith("ThormangWalk"):
+        # post-physics fused into the kernel (tg_walk_step): progress, reset flag,
+        # actions, last actions, commands in; observations, last actions, reward,
+        # reset, timeout, progress out (+ the push wrench row for the DR variant)
+        read += 8 + 8 + D * 4 * 2 + 3 * 4
+        write += env.num_obs * 4 + D * 4 + 4 + 8 + 1 + 8
+        if getattr(env, "push_enabled", False):
+            write += 6 * 4
     return read + write
 
 

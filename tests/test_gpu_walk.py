@@ -94,25 +94,42 @@ def test_gpu_walk_dr_16384_envs():
 
 
 def test_gpu_walk_fused_step_equals_separate_calls():
-    """tg_walk_step (pre-physics fused into the compose launch) gives the
-    bit-identical results of tg_walk_pre_physics + tg_simulate +
-    tg_walk_post_physics (the VecTask.step sequence), resets and pushes
-    included."""
+    """tg_walk_step (pre-physics fused into the compose launch, post-physics
+    fused into the step kernel's epilogue) against tg_walk_pre_physics +
+    tg_simulate + tg_walk_post_physics (the VecTask.step sequence), resets and
+    pushes included, teacher-forced: before every step the separate-call env is
+    re-synced from the fused one, so each step is compared from identical
+    inputs.  The two step-kernel instantiations are separately optimised
+    fast-math code, so they agree to the last bits (1e-5 here), not bit for bit;
+    resets, progress, actions and targets must be identical."""
     _cuda()
     import thormang_isaacgym_amd as tia
     from thormang_isaacgym_amd.tasks.base.vec_task import VecTask
     for task in ("ThormangWalk", "ThormangWalkDR"):
         envs = [tia.make(seed=11, task=task, num_envs=256, sim_device="cuda:0", rl_device="cuda:0")
                 for _ in range(2)]
+        f, u = envs
         g = torch.Generator(device="cuda:0").manual_seed(5)
+        n_reset = 0
+        worst = 0.0
         for _ in range(120):
+            for name in ("obs_buf", "rew_buf", "reset_buf", "progress_buf", "actions", "last_actions", "commands"):
+                getattr(u, name).copy_(getattr(f, name))
+            for name in ("root_state", "dof_state", "body_force"):
+                if getattr(u.sim, name, None) is not None:
+                    getattr(u.sim, name).copy_(getattr(f.sim, name))
             a = torch.rand(256, 33, device="cuda:0", generator=g) * 2.4 - 1.2   # some beyond the clip
-            envs[0].step(a)
-            VecTask.step(envs[1], a)
+            f.step(a)
+            VecTask.step(u, a)
             torch.cuda.synchronize()
-            for name in ("obs_buf", "rew_buf", "reset_buf", "progress_buf", "actions", "root_tensor"):
-                x, y = getattr(envs[0], name), getattr(envs[1], name)
-                assert torch.equal(x, y), (task, name)
-            assert torch.equal(envs[0].sim.dof_state, envs[1].sim.dof_state), task
-            assert torch.equal(envs[0].sim.dof_pos_target, envs[1].sim.dof_pos_target), task
-        assert int(envs[0].reset_buf.sum()) >= 0
+            for name in ("reset_buf", "progress_buf", "actions"):
+                assert torch.equal(getattr(f, name), getattr(u, name)), (task, name)
+            assert torch.equal(f.sim.dof_pos_target, u.sim.dof_pos_target), task
+            for x, y, what in ((f.obs_buf, u.obs_buf, "obs"), (f.rew_buf, u.rew_buf, "rew"),
+                               (f.sim.root_state, u.sim.root_state, "root"), (f.sim.dof_state, u.sim.dof_state, "dof")):
+                d = float((x - y).abs().max())
+                worst = max(worst, d)
+                assert d <= 1e-5, (task, what, d)
+            n_reset += int(f.reset_buf.sum())
+        print(task, "max |fused - separate|", worst, "resets", n_reset)
+        assert n_reset > 0, task   # the comparison covered resets

@@ -451,24 +451,202 @@ template <class M> __device__ __forceinline__ constexpr int row_base(int s) {
 
 namespace tg {
 
+// ---------------------------------------------------------------- fused walk post-physics
+// tg_walk_step's last simulate: the ThormangWalk post-physics step
+// (walk_task.hip walk_post_kernel: progress, masked resets, observations,
+// reward, termination, timeouts, pushes) as the step kernel's epilogue, LPE
+// lanes per env (lane = dof mod LPE) on the final state the kernel holds, so
+// the state is stored once (reset values for a reset env) and the separate
+// launch disappears.  Same operations as walk_env; the fp contraction and
+// reassociation are off here as in walk_task.hip, the transcendentals are this
+// translation unit's (fast-math) ones.
+struct WalkPost {
+    static constexpr bool on = true;
+    using Args = WalkPostArgs;
+    static __device__ __forceinline__ float clampw(float x, float lo, float hi) {
+        return x < lo ? lo : (x > hi ? hi : x);
+    }
+    template <class M, int LPE>
+    static __device__ __forceinline__ void epilogue(const Args &pa, const StepArgs &a, const LE &s, int e, bool owner,
+                                                    int sub, const float *rt0, float *root, float *dofs) {
+#pragma clang fp contract(off) reassociate(off)
+        constexpr int D = M::ND;
+        constexpr int NR = (D + LPE - 1) / LPE;
+        const tg_walk_params &p = pa.p;
+        const tg_walk_buffers &b = pa.b;
+        const uint32_t c_lo = pa.c_lo, c_hi = pa.c_hi;
+        const bool lead = sub == 0;
+        const size_t eD = (size_t)e * D;
+        // every input of the env in one batch
+        const int64_t prog1 = b.progress_buf[e] + 1;
+        const bool reset = b.reset_buf[e] != 0;
+        float q[NR], qd[NR], act[NR], la[NR], pt[NR], cmd[3], rt[13];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const int d = sub + LPE * r;
+            q[r] = qd[r] = act[r] = la[r] = pt[r] = 0.f;
+            if (d < D) {
+                const int g = DofGroup<M>::tab.g[d];
+                if (g > 0) {
+                    q[r] = s(g * GF + F_Q);
+                    qd[r] = s(g * GF + F_QD);
+                } else {
+                    q[r] = 0.5f * (prop(a, TG_PROP_LOWER, e, d) + prop(a, TG_PROP_UPPER, e, d));
+                }
+                act[r] = b.actions[eD + d];
+                la[r] = b.last_actions[eD + d];
+                pt[r] = b.pos_target[eD + d];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) cmd[k] = b.commands[3 * (size_t)e + k];
+#pragma unroll
+        for (int k = 0; k < 13; ++k) rt[k] = rt0[k];
+        const int64_t prog = reset ? 0 : prog1;
+        if (reset) {
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const int d = sub + LPE * r;
+                if (d < D) {
+                    q[r] = p.default_pos[d] +
+                           (walk_draw(p, pa.reset_draws, e, 4 + d, c_lo, c_hi) * 2.0f - 1.0f) * p.joint_noise;
+                    qd[r] = 0.1f * (walk_draw(p, pa.reset_draws, e, 4 + D + d, c_lo, c_hi) * 2.0f - 1.0f);
+                    act[r] = la[r] = 0.f;
+                    if (owner) b.actions[eD + d] = 0.f;
+                }
+            }
+            if (lead) {
+                float r4[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) r4[k] = walk_draw(p, pa.reset_draws, e, k, c_lo, c_hi);
+                cmd[0] = p.cmd_vx[0] + r4[0] * (p.cmd_vx[1] - p.cmd_vx[0]);
+                cmd[1] = p.cmd_vy[0] + r4[1] * (p.cmd_vy[1] - p.cmd_vy[0]);
+                cmd[2] = p.cmd_wz[0] + r4[2] * (p.cmd_wz[1] - p.cmd_wz[0]);
+                const float yaw = (r4[3] * 2.0f - 1.0f) * 3.14159265358979323846f;
+                const float *tpl = b.root_reset + 13 * (size_t)e;
+                rt[0] = tpl[0];
+                rt[1] = tpl[1];
+                rt[2] = p.spawn_height;
+                rt[3] = 0.0f;
+                rt[4] = 0.0f;
+                rt[5] = sinf(0.5f * yaw);
+                rt[6] = cosf(0.5f * yaw);
+#pragma unroll
+                for (int k = 7; k < 13; ++k) rt[k] = 0.0f;
+                if (owner) {
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) b.commands[3 * (size_t)e + k] = cmd[k];
+                }
+            }
+        }
+        // dof observations and the per-dof reward terms
+        float *o = b.obs_buf + (size_t)p.num_obs * e;
+        const float co = p.clip_obs;
+        float rate = 0.0f, vel2 = 0.0f, tq = 0.0f;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const int d = sub + LPE * r;
+            if (d < D) {
+                if (owner) {
+                    o[13 + d] = clampw((q[r] - p.default_pos[d]) * p.dof_pos_scale, -co, co);
+                    o[13 + D + d] = clampw(qd[r] * p.dof_vel_scale, -co, co);
+                    o[13 + 2 * D + d] = clampw(act[r], -co, co);
+                    b.last_actions[eD + d] = act[r];
+                }
+                rate += (act[r] - la[r]) * (act[r] - la[r]);
+                vel2 += qd[r] * qd[r];
+                const float tt = p.stiffness[d] * (pt[r] - q[r]);
+                tq += tt * tt;
+            }
+        }
+        rate = sum_lanes<LPE>(rate);
+        vel2 = sum_lanes<LPE>(vel2);
+        tq = sum_lanes<LPE>(tq);
+        if (owner) {
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const int d = sub + LPE * r;
+                if (d < D) {
+                    dofs[2 * d] = q[r];
+                    dofs[2 * d + 1] = qd[r];
+                }
+            }
+        }
+        if (!lead || !owner) return;
+#pragma unroll
+        for (int k = 0; k < 13; ++k) root[k] = rt[k];
+        b.progress_buf[e] = prog;
+        const float x = rt[3], y = rt[4], z = rt[5], w = rt[6];
+        const float Rw[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w),
+                             2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w),
+                             2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)};
+        float vb[3], wb[3], gb[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            vb[k] = Rw[k] * rt[7] + Rw[3 + k] * rt[8] + Rw[6 + k] * rt[9];
+            wb[k] = Rw[k] * rt[10] + Rw[3 + k] * rt[11] + Rw[6 + k] * rt[12];
+            gb[k] = -Rw[6 + k];
+        }
+        o[0] = clampw(rt[2], -co, co);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            o[1 + k] = clampw(vb[k] * p.lin_vel_scale, -co, co);
+            o[4 + k] = clampw(wb[k] * p.ang_vel_scale, -co, co);
+            o[7 + k] = clampw(gb[k], -co, co);
+        }
+        o[10] = clampw(cmd[0] * p.lin_vel_scale, -co, co);
+        o[11] = clampw(cmd[1] * p.lin_vel_scale, -co, co);
+        o[12] = clampw(cmd[2] * p.ang_vel_scale, -co, co);
+        const float lin_err = (cmd[0] - vb[0]) * (cmd[0] - vb[0]) + (cmd[1] - vb[1]) * (cmd[1] - vb[1]);
+        const float ang_err = (cmd[2] - wb[2]) * (cmd[2] - wb[2]);
+        const float dz = rt[2] - p.target_height;
+        float rew = p.rew_lin_vel_xy * expf(-lin_err / 0.25f) + p.rew_ang_vel_z * expf(-ang_err / 0.25f) +
+                    p.rew_upright * (-gb[2]) + p.rew_alive + p.rew_height * expf(-dz * dz / 0.01f) +
+                    p.rew_action_rate * rate + p.rew_dof_vel * vel2 + p.rew_torque * tq;
+        const bool fall = (rt[2] < p.termination_height) || (-gb[2] < p.termination_up);
+        if (fall) rew += p.rew_termination;
+        const bool rs = fall || prog >= p.max_episode_length - 1;
+        b.rew_buf[e] = rew;
+        b.reset_buf[e] = rs ? 1 : 0;
+        b.timeout_buf[e] = (prog >= p.max_episode_length - 1) && rs;
+        if (!b.body_force) return;
+        // push wrench for the next simulate (walk_post_kernel)
+        float *f = b.body_force + (size_t)6 * p.num_groups * e;
+        const bool push = p.push_force > 0.0f && p.push_interval > 0 && prog > 0 && (prog % p.push_interval) == 0;
+        float u[3];
+        if (pa.push_draws) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) u[k] = pa.push_draws[3 * (size_t)e + k];
+        } else {
+            const U4 xx = philox(U4{(uint32_t)e, c_lo, c_hi, 0x50555348u}, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+            u[0] = u01(xx.x); u[1] = u01(xx.y); u[2] = u01(xx.z);
+        }
+        f[0] = push ? p.push_force * (u[0] * 2.0f - 1.0f) : 0.0f;
+        f[1] = push ? p.push_force * (u[1] * 2.0f - 1.0f) : 0.0f;
+        f[2] = push ? 0.25f * p.push_force * (u[2] * 2.0f - 1.0f) : 0.0f;
+        f[3] = 0.0f; f[4] = 0.0f; f[5] = 0.0f;
+    }
+};
+
 // ---------------------------------------------------------------- dispatch
 // compose (dirty envs only), then the tree-parallel LDS-resident step,
 // M::EPB envs x M::LPE lanes per workgroup (Thormang: 16 envs, 151 KB of LDS).
 
 // HF: terrain heightfield present (tg_set_heightfield); the flat-ground
 // instantiation keeps the contact normal a compile-time e_z.
-template <class M, bool HF> int launch_par(const StepArgs &a, hipStream_t stream) {
+template <class M, bool HF, class P = NoPost>
+int launch_par(const StepArgs &a, hipStream_t stream, const typename P::Args &pa = {}) {
     constexpr size_t bytes = ParLayout<M>::template bytes<M::EPB>();
     static_assert(bytes <= 160 * 1024, "LDS budget");
     static bool attr = false;
     if (!attr) {
-        if (hipFuncSetAttribute((const void *)step_par_kernel<M, M::EPB, HF>,
+        if (hipFuncSetAttribute((const void *)step_par_kernel<M, M::EPB, HF, P>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess)
             return TG_ERR_HIP;
         attr = true;
     }
-    hipLaunchKernelGGL((step_par_kernel<M, M::EPB, HF>), dim3((a.N + M::EPB - 1) / M::EPB), dim3(M::EPB * M::LPE),
-                       bytes, stream, a);
+    hipLaunchKernelGGL((step_par_kernel<M, M::EPB, HF, P>), dim3((a.N + M::EPB - 1) / M::EPB), dim3(M::EPB * M::LPE),
+                       bytes, stream, a, pa);
     return 0;
 }
 
@@ -486,6 +664,33 @@ template <class M> int launch_model(const StepArgs &a, hipStream_t stream, hipEv
 
 int launch_step(uint64_t hash, const StepArgs &a, hipStream_t stream, hipEvent_t ev_begin, hipEvent_t ev_end) {
     TG_FOR_EACH_MODEL(TG_LAUNCH)
+    return TG_ERR_MODEL;
+}
+
+// the fused walk epilogue is instantiated for the lane-pair (humanoid-size)
+// trees on flat ground only
+template <class M>
+int launch_model_walk(const StepArgs &a, const WalkPostArgs &pa, hipStream_t stream, hipEvent_t ev_begin,
+                      hipEvent_t ev_end) {
+    if constexpr (M::PAIR == 0 || M::ND > 64) {
+        return 1;
+    } else {
+        if (a.hf || pa.p.num_dof != M::ND) return 1;
+        hipLaunchKernelGGL(compose_kernel<M>, dim3((a.N + COMPOSE_WPB - 1) / COMPOSE_WPB), dim3(64 * COMPOSE_WPB), 0,
+                           stream, a);
+        if (ev_begin && hipEventRecord(ev_begin, stream) != hipSuccess) return TG_ERR_HIP;
+        if (int rc = launch_par<M, false, WalkPost>(a, stream, pa)) return rc;
+        if (ev_end && hipEventRecord(ev_end, stream) != hipSuccess) return TG_ERR_HIP;
+        return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
+    }
+}
+
+#define TG_LAUNCH_WALK(MODEL) \
+    if (hash == MODEL::hash) return launch_model_walk<MODEL>(a, pa, stream, ev_begin, ev_end);
+
+int launch_step_walk(uint64_t hash, const StepArgs &a, const WalkPostArgs &pa, hipStream_t stream,
+                     hipEvent_t ev_begin, hipEvent_t ev_end) {
+    TG_FOR_EACH_MODEL(TG_LAUNCH_WALK)
     return TG_ERR_MODEL;
 }
 

@@ -265,7 +265,31 @@ __device__ __forceinline__ float ground_at(const StepArgs &a, float x, float y, 
     return H;
 }
 
-template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a) {
+// Optional fused epilogue P: a task's post-physics step run by the step
+// kernel on the final state (still in registers / LDS) instead of a separate
+// launch that re-reads it; P::epilogue then also stores the state.  NoPost:
+// plain store.
+struct NoPost {
+    struct Args {};
+    static constexpr bool on = false;
+};
+
+// inverse of the group -> dof map: group of dof d, -1 for a locked dof
+template <class M> struct DofGroup {
+    struct Arr {
+        int g[M::ND > 0 ? M::ND : 1];
+    };
+    static constexpr Arr make() {
+        Arr x{};
+        for (int d = 0; d < M::ND; ++d) x.g[d] = -1;
+        for (int g = 1; g < M::NG; ++g) x.g[M::gdof[g]] = g;
+        return x;
+    }
+    static constexpr Arr tab = make();
+};
+
+template <class M, int EPB, bool HF, class P = NoPost>
+__global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, typename P::Args pa) {
     constexpr int LPE = M::LPE;
     static_assert(64 % LPE == 0, "an env's lanes must share a wavefront");
     using CL = CompLayout<M>;
@@ -1088,7 +1112,13 @@ template <class M, int EPB, bool HF> __global__ __launch_bounds__(EPB * M::LPE) 
         TG_SYNC();
         TG_PROF(8)
     }
-    if (owner) {
+    if constexpr (P::on) {
+        // final root state in the world frame (every lane of the env holds it)
+        const V3 wwo = mul(R, v0.w);
+        const V3 vco = mul(R, v0.v) + cross(wwo, mul(R, c0));
+        const float rt[13] = {pos.x, pos.y, pos.z, qx, qy, qz, qw, vco.x, vco.y, vco.z, wwo.x, wwo.y, wwo.z};
+        P::template epilogue<M, LPE>(pa, a, s, e, owner, sub, rt, root, dofs);
+    } else if (owner) {
         if (lead) {
             const V3 wwo = mul(R, v0.w);
             const V3 vco = mul(R, v0.v) + cross(wwo, mul(R, c0));

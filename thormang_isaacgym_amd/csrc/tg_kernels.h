@@ -44,6 +44,18 @@ struct StepArgs {
     float pm_default[TG_PM_MAX_DOF];
 };
 
+// tg_walk_step's fused post-physics epilogue (articulation.hip WalkPost)
+struct WalkPostArgs {
+    tg_walk_params p;
+    tg_walk_buffers b;
+    const float *reset_draws, *push_draws;
+    uint32_t c_lo, c_hi;
+};
+// compose + step kernel with the walk post-physics fused in; returns 1 (nothing
+// launched) when the model / ground has no fused instantiation
+int launch_step_walk(uint64_t hash, const StepArgs &a, const WalkPostArgs &pa, hipStream_t stream,
+                     hipEvent_t ev_begin = nullptr, hipEvent_t ev_end = nullptr);
+
 // ev_begin / ev_end (optional) are recorded around the step kernel itself
 int launch_step(uint64_t hash, const StepArgs &a, hipStream_t stream, hipEvent_t ev_begin = nullptr,
                 hipEvent_t ev_end = nullptr);
@@ -99,6 +111,17 @@ __device__ __forceinline__ float gauss(uint32_t a, uint32_t b) {
     float u1 = ((float)(a >> 8) + 1.0f) * (1.0f / 16777217.0f);
     float u2 = u01(b);
     return sqrtf(-2.0f * __logf(u1)) * __cosf(6.28318530718f * u2);
+}
+
+// ThormangWalk reset draw k of env e (replay array or in-kernel Philox, 4 draws per counter)
+__device__ __forceinline__ float walk_draw(const tg_walk_params &p, const float *reset_draws, int e, int k,
+                                           uint32_t c_lo, uint32_t c_hi) {
+    const int n = 4 + 2 * p.num_dof;
+    if (reset_draws) return reset_draws[(size_t)n * e + k];
+    const U4 x = philox(U4{(uint32_t)e, c_lo, c_hi, 0x57524530u + (uint32_t)(k >> 2)}, (uint32_t)p.seed,
+                        (uint32_t)(p.seed >> 32));
+    const uint32_t c = (k & 3) == 0 ? x.x : (k & 3) == 1 ? x.y : (k & 3) == 2 ? x.z : x.w;
+    return u01(c);
 }
 
 }  // namespace tg

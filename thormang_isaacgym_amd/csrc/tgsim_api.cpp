@@ -12,6 +12,7 @@
 #include <cstring>
 #include <string>
 #include <utility>
+#include <cstdlib>
 #include <vector>
 
 #include "../../include/tg_gogoro.h"
@@ -58,6 +59,7 @@ struct tg_sim {
     float hf_hs = 0.f, hf_vs = 0.f, hf_ox = 0.f, hf_oy = 0.f, hf_mu = 0.f;
     std::vector<void *> allocs;
     // kernel timing (tg_set_kernel_timing): event pairs recorded, not yet read
+    bool walk_unfused = false;   // tg_walk_step: separate post-physics launch (TG_WALK_UNFUSED=1)
     int timing = 0;          // period (0: off)
     int64_t timing_count = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending, ev_free;
@@ -156,6 +158,7 @@ int tg_sim_create(const tg_model_desc *m, const tg_sim_params *params, int32_t n
     if (device < 0 || device >= ndev) return fail(TG_ERR_ARG, "device %d not present (%d visible)", device, ndev);
     HIPCHK(hipSetDevice(device));
     tg_sim *s = new tg_sim();
+    if (const char *u = getenv("TG_WALK_UNFUSED")) s->walk_unfused = u[0] == '1';
     s->device = device;
     s->N = num_envs;
     s->D = m->num_dofs;
@@ -389,8 +392,10 @@ int tg_set_heightfield(tg_sim *s, const float *heights, int32_t rows, int32_t co
     return TG_OK;
 }
 
-// compose (+ optional prologue in a) and the step kernel of one simulate call
-static int simulate_args(tg_sim *s, const tg::StepArgs &a) {
+// compose (+ optional prologue in a) and the step kernel of one simulate call;
+// with wp, the step kernel carrying the walk post-physics epilogue (returns 1,
+// nothing launched, when the model has no such instantiation)
+static int simulate_args(tg_sim *s, const tg::StepArgs &a, const tg::WalkPostArgs *wp = nullptr) {
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     if (s->timing > 0 && s->timing_count++ % s->timing == 0) {
         if (!s->ev_free.empty()) {
@@ -402,7 +407,16 @@ static int simulate_args(tg_sim *s, const tg::StepArgs &a) {
         }
         s->ev_pending.push_back(ev);
     }
-    int rc = tg::launch_step(s->hash, a, s->stream, ev.first, ev.second);
+    int rc = wp ? tg::launch_step_walk(s->hash, a, *wp, s->stream, ev.first, ev.second)
+                : tg::launch_step(s->hash, a, s->stream, ev.first, ev.second);
+    if (rc == 1) {   // not launched: hand the event pair back
+        if (ev.first) {
+            s->ev_pending.pop_back();
+            s->ev_free.push_back(ev);
+        }
+        if (s->timing > 0) s->timing_count--;
+        return 1;
+    }
     s->forces_pending = false;   // apply_rigid_body_force_tensors acts for one simulate call
     if (rc) return fail(rc, "step launch failed: %s", hipGetErrorString(hipGetLastError()));
     return TG_OK;
@@ -523,6 +537,12 @@ int tg_walk_step(tg_sim *s, const tg_walk_params *p, const tg_walk_buffers *b, c
             a.pm_scale = p->action_scale;
             a.pm_clip = p->clip_actions;
             for (int d = 0; d < p->num_dof; ++d) a.pm_default[d] = p->default_pos[d];
+        }
+        if (i == n_simulate - 1 && !s->walk_unfused) {   // post-physics fused into the last step kernel
+            const tg::WalkPostArgs wp{*p, *b, reset_draws, push_draws, (uint32_t)counter, (uint32_t)(counter >> 32)};
+            const int rc = simulate_args(s, a, &wp);
+            if (rc == 0) return TG_OK;
+            if (rc < 0) return rc;
         }
         if (int rc = simulate_args(s, a)) return rc;
     }

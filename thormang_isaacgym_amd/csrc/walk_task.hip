@@ -24,17 +24,6 @@ __global__ __launch_bounds__(256) void walk_pre_kernel(tg_walk_params p, tg_walk
     b.pos_target[t] = p.default_pos[d] + p.action_scale * a;
 }
 
-// reset draw k of env e (replay array or in-kernel Philox, 4 draws per counter)
-__device__ __forceinline__ float walk_draw(const tg_walk_params &p, const float *reset_draws, int e, int k,
-                                           uint32_t c_lo, uint32_t c_hi) {
-    const int n = 4 + 2 * p.num_dof;
-    if (reset_draws) return reset_draws[(size_t)n * e + k];
-    const U4 x = philox(U4{(uint32_t)e, c_lo, c_hi, 0x57524530u + (uint32_t)(k >> 2)}, (uint32_t)p.seed,
-                        (uint32_t)(p.seed >> 32));
-    const uint32_t c = (k & 3) == 0 ? x.x : (k & 3) == 1 ? x.y : (k & 3) == 2 ? x.z : x.w;
-    return u01(c);
-}
-
 // sum over the wavefront, returned to every lane: DPP within each 16-lane row
 // (half-mirror, quad swaps, row rotate by 8), then the four row totals
 template <int CTRL> __device__ __forceinline__ float dppw(float v) {
@@ -59,7 +48,7 @@ __device__ __forceinline__ float wave_total(float v) {
 // latency; a reset env then replaces them with the freshly drawn values.
 __device__ void walk_env(const tg_walk_params &p, const tg_walk_buffers &b, int e, bool reset, int64_t prog,
                          const float *reset_draws, uint32_t c_lo, uint32_t c_hi) {
-    const int lane = threadIdx.x;   // blockDim.x == 64 >= num_dof (TG_WALK_MAX_DOF)
+    const int lane = threadIdx.x % 64;   // one wavefront per env, 64 >= num_dof (TG_WALK_MAX_DOF)
     const int D = p.num_dof;
     float *root = b.root + 13 * (size_t)e;
     float *o = b.obs_buf + (size_t)p.num_obs * e;
@@ -166,15 +155,23 @@ __device__ void walk_env(const tg_walk_params &p, const tg_walk_buffers &b, int 
     b.timeout_buf[e] = (prog >= p.max_episode_length - 1) && rs;
 }
 
-__global__ __launch_bounds__(64) void walk_post_kernel(tg_walk_params p, tg_walk_buffers b, const float *reset_draws,
-                                                       const float *push_draws, uint32_t c_lo, uint32_t c_hi) {
-    const int e = blockIdx.x;
+#ifndef TG_WALK_POST_WPB
+#define TG_WALK_POST_WPB 16
+#endif
+// WALK_POST_WPB wavefronts (envs) per workgroup
+constexpr int WALK_POST_WPB = TG_WALK_POST_WPB;
+__global__ __launch_bounds__(64 * WALK_POST_WPB) void walk_post_kernel(tg_walk_params p, tg_walk_buffers b,
+                                                                       const float *reset_draws, const float *push_draws,
+                                                                       uint32_t c_lo, uint32_t c_hi) {
+    const int e = blockIdx.x * WALK_POST_WPB + threadIdx.x / 64;
+    if (e >= p.num_envs) return;
+    const int lane = threadIdx.x % 64;
     int64_t prog = b.progress_buf[e] + 1;
     const bool reset = b.reset_buf[e] != 0;
-    if (threadIdx.x == 0) b.progress_buf[e] = prog;
+    if (lane == 0) b.progress_buf[e] = prog;
     if (reset) prog = 0;
     walk_env(p, b, e, reset, prog, reset_draws, c_lo, c_hi);
-    if (threadIdx.x != 0 || !b.body_force) return;
+    if (lane != 0 || !b.body_force) return;
     float *f = b.body_force + (size_t)6 * p.num_groups * e;
     const bool push = p.push_force > 0.0f && p.push_interval > 0 && prog > 0 && (prog % p.push_interval) == 0;
     float u[3];
@@ -206,7 +203,8 @@ int launch_walk_pre(const tg_walk_params &p, const tg_walk_buffers &b, const flo
 int launch_walk_post(const tg_walk_params &p, const tg_walk_buffers &b, const float *rd, const float *pd,
                      uint64_t counter, hipStream_t s) {
     if (p.num_dof > TG_WALK_MAX_DOF) return TG_ERR_ARG;
-    hipLaunchKernelGGL(walk_post_kernel, dim3(p.num_envs), dim3(64), 0, s, p, b, rd, pd,
+    hipLaunchKernelGGL(walk_post_kernel, dim3((p.num_envs + WALK_POST_WPB - 1) / WALK_POST_WPB),
+                       dim3(64 * WALK_POST_WPB), 0, s, p, b, rd, pd,
                        (uint32_t)counter, (uint32_t)(counter >> 32));
     return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
 }
