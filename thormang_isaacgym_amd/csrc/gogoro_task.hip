@@ -136,30 +136,130 @@ __device__ void reset_env(const tg_gogoro_params &p, const tg_gogoro_buffers &b,
     for (int k = 0; k < 5; ++k) b.action_history[5 * (size_t)e + k] = 0.0f;
 }
 
-__global__ __launch_bounds__(256) void post_kernel(tg_gogoro_params p, tg_gogoro_buffers b, const float *reset_draws,
-                                                   const float *obs_draws, const float *speed_draws,
-                                                   const float *yaw_draws, uint32_t c_lo, uint32_t c_hi) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= p.num_envs) return;
+// post_physics_step with POST_LPE lanes per env (4 envs per wavefront): the
+// env's 9 Philox blocks (5 reset, 3 sensor noise, 1 command resample) run at
+// once on lanes 0-8 and reach the lead lane through LDS, every input is read
+// in one batch before the reset flag is known, a reset's dof writes are spread
+// over the env's lanes, and the lead lane does the scalar task math on
+// register copies.  Same counters and the same fp32 operations as the
+// lane-per-env formulation (reset_env / philox_reset_draws), so the same values.
+constexpr int POST_LPE = 16;
+constexpr int POST_EPB = 64 / POST_LPE;
+__global__ __launch_bounds__(64) void post_kernel(tg_gogoro_params p, tg_gogoro_buffers b, const float *reset_draws,
+                                                  const float *obs_draws, const float *speed_draws,
+                                                  const float *yaw_draws, uint32_t c_lo, uint32_t c_hi) {
+    __shared__ float xch[POST_EPB][POST_LPE * 3];
+    const int le = threadIdx.x / POST_LPE, l = threadIdx.x % POST_LPE;
+    const int e0 = blockIdx.x * POST_EPB + le;
+    const bool owner = e0 < p.num_envs;
+    const int e = owner ? e0 : p.num_envs - 1;   // tail lanes redo the last env, never store
+    const bool lead = l == 0;
     const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
+    const int D = p.num_dof;
+    // ---- inputs (lead lane), one batch
     int64_t prog = b.progress_buf[e] + 1;
-    b.progress_buf[e] = prog;
-    if (b.reset_buf[e] != 0) {
-        float r[TG_GOGORO_RESET_DRAWS];
+    const bool rflag = b.reset_buf[e] != 0;
+    float rt[13], ah[5], yawc = 0.0f, cmdc = 0.0f, imu = 0.0f;
+    if (lead) {
+        const float *root = b.root + 13 * (size_t)e;
+#pragma unroll
+        for (int k = 0; k < 13; ++k) rt[k] = root[k];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) ah[k] = b.action_history[5 * (size_t)e + k];
+        yawc = b.yaw_command[e];
+        cmdc = b.curent_command[e];
+        imu = b.imu_offsets[e];
+    }
+    // ---- draws: lane k < 9 runs Philox block k and leaves its (up to 3) floats in xch
+    if (l < 9) {
+        const uint32_t key = l < 5 ? 0x52535430u + (uint32_t)l : (l < 8 ? 0x4F425330u + (uint32_t)(l - 5) : 0x434D4430u);
+        const U4 x = philox(U4{(uint32_t)e, c_lo, c_hi, key}, k0, k1);
+        const float A = u01(x.x), B = gauss(x.x, x.y), C = gauss(x.y, x.z), Dd = u01(x.w), E = u01(x.y),
+                    F = gauss(x.z, x.w);
+        xch[le][3 * l] = (l == 0 || l == 1 || l == 4 || l == 8) ? A : B;
+        xch[le][3 * l + 1] = l == 0 ? C : ((l == 1 || l == 8) ? E : F);
+        xch[le][3 * l + 2] = l == 0 ? Dd : F;
+    }
+    __syncthreads();
+    float r[TG_GOGORO_RESET_DRAWS];
+    if (rflag) {
         if (reset_draws) {
 #pragma unroll
             for (int k = 0; k < TG_GOGORO_RESET_DRAWS; ++k) r[k] = reset_draws[(size_t)e * TG_GOGORO_RESET_DRAWS + k];
         } else {
-            philox_reset_draws(e, c_lo, c_hi, k0, k1, r);
+            const int slot[TG_GOGORO_RESET_DRAWS] = {0, 1, 2, 3, 4, 5, 6, 7, 9, 10, 12};
+#pragma unroll
+            for (int k = 0; k < TG_GOGORO_RESET_DRAWS; ++k) r[k] = xch[le][slot[k]];
         }
-        reset_env(p, b, e, r);
+        // reset_env: dof writes over the env's lanes, the rest on the lead lane
+        if (owner) {
+            float *dof = b.dof_state + 2 * (size_t)e * D;
+            for (int d = l; d < D; d += POST_LPE) {
+                dof[2 * d] = b.thormang_pose[d];
+                dof[2 * d + 1] = 0.0f;
+            }
+        }
+        if (lead) {
+            const float target = (r[3] * 2.0f - 1.0f) * F_PI;
+            const float rot = target + u_aff(-1.57f, 1.57f, r[4]);
+            const float hh = rot / 2.0f;
+            const float *tpl = b.root_reset + 13 * (size_t)e;
+            rt[0] = tpl[0];
+            rt[1] = tpl[1];
+            rt[2] = p.terrain_spawn ? tpl[2] : p.spawn_z;
+            rt[3] = 0.0f;
+            rt[4] = 0.0f;
+            rt[5] = sinf(hh);
+            rt[6] = cosf(hh);
+#pragma unroll
+            for (int k = 7; k < 13; ++k) rt[k] = 0.0f;
+            float cv[5];
+            cv[0] = n_aff(p.seat_offset_x_range, r[5]);
+            cv[1] = n_aff(p.seat_offset_y_range, r[6]);
+            cv[2] = n_aff(p.seat_offset_z_range, r[7]);
+            cv[3] = n_aff(p.seat_offset_xr_range, r[8]);
+            cv[4] = n_aff(p.steering_offset, r[9]);
+            imu = cv[3];
+            yawc = target;
+            cmdc = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) ah[k] = 0.0f;
+            if (owner) {
+                b.curent_speed[e] = u_aff(p.speed_range[0], p.speed_range[1], r[0]);
+                b.speed_offset[e] = u_aff(p.speed_sensor_offset[0], p.speed_sensor_offset[1], r[2]);
+                float *root = b.root + 13 * (size_t)e;
+#pragma unroll
+                for (int k = 0; k < 13; ++k) root[k] = rt[k];
+#pragma unroll
+                for (int k = 0; k < 5; ++k) b.config_vector[5 * (size_t)e + k] = cv[k];
+                const size_t ND = (size_t)p.num_envs * D;
+                float *prop = b.dof_props + (size_t)e * D;
+                const int seat[3] = {p.dof_base_x, p.dof_base_y, p.dof_base_z};
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    prop[TG_PROP_DRIVE_MODE * ND + seat[k]] = 0.0f;
+                    prop[TG_PROP_LOWER * ND + seat[k]] = cv[k];
+                    prop[TG_PROP_UPPER * ND + seat[k]] = cv[k] + 0.0001f;
+                }
+                b.imu_offsets[e] = cv[3];
+                b.steer_offsets[e] = cv[4];
+                const int st = p.dof_steer;
+                prop[TG_PROP_DRIVE_MODE * ND + st] = 1.0f;
+                prop[TG_PROP_STIFFNESS * ND + st] = p.steer_stiffness;
+                prop[TG_PROP_DAMPING * ND + st] = u_aff(p.steering_damping_range[0], p.steering_damping_range[1], r[10]);
+                prop[TG_PROP_EFFORT * ND + st] = p.steer_effort;
+                prop[TG_PROP_VELOCITY * ND + st] = p.steer_velocity;
+                b.env_dirty[e] = 1;
+                b.curent_command[e] = 0.0f;
+#pragma unroll
+                for (int k = 0; k < 5; ++k) b.action_history[5 * (size_t)e + k] = 0.0f;
+            }
+        }
         prog = 0;
     }
+    if (!lead) return;
     float o[6];
-    observation(b.root + 13 * (size_t)e, b.yaw_command[e], b.curent_command[e], o);
-    float *bo = b.buffer_obs + 6 * (size_t)e;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) bo[k] = o[k];
+    observation(rt, yawc, cmdc, o);
     // compute_gogoro_reward
     const float max_tilt = 0.30f;
     float tilt_err = t_clamp(o[0] / max_tilt, -1.0f, 1.0f);
@@ -169,7 +269,6 @@ __global__ __launch_bounds__(256) void post_kernel(tg_gogoro_params p, tg_gogoro
     float r1 = 1.0f / (1.0f + y30 * y30);
     float r2 = 1.0f - tilt_err * tilt_err;
     float r4 = 1.0f - dtilt_err * dtilt_err;
-    const float *ah = b.action_history + 5 * (size_t)e;
     float ce = 0.0f;
 #pragma unroll
     for (int k = 0; k < 5; ++k) ce += 1.0f - ah[k] * ah[k];
@@ -177,44 +276,42 @@ __global__ __launch_bounds__(256) void post_kernel(tg_gogoro_params p, tg_gogoro
     const bool felt = fabsf(o[0]) >= max_tilt;
     const bool finished = prog >= p.max_episode_length - 1;
     const int64_t reset = (finished || felt) ? 1 : 0;
-    b.rew_buf[e] = felt ? -100.0f : rew;
-    b.reset_buf[e] = reset;
     // sensor noise (compute_obs_rwd :449-462)
     float nd[5];
     if (obs_draws) {
 #pragma unroll
         for (int k = 0; k < 5; ++k) nd[k] = obs_draws[(size_t)e * 5 + k];
     } else {
-        U4 x0 = philox(U4{(uint32_t)e, c_lo, c_hi, 0x4F425330u}, k0, k1);
-        U4 x1 = philox(U4{(uint32_t)e, c_lo, c_hi, 0x4F425331u}, k0, k1);
-        U4 x2 = philox(U4{(uint32_t)e, c_lo, c_hi, 0x4F425332u}, k0, k1);
-        nd[0] = gauss(x0.x, x0.y); nd[1] = gauss(x0.z, x0.w); nd[2] = gauss(x1.x, x1.y);
-        nd[3] = gauss(x1.z, x1.w); nd[4] = gauss(x2.x, x2.y);
+        nd[0] = xch[le][15]; nd[1] = xch[le][16]; nd[2] = xch[le][18]; nd[3] = xch[le][19]; nd[4] = xch[le][21];
     }
     float rr[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) rr[k] = o[k];
-    rr[0] += n_aff(p.imu_filter_noise, nd[0]) + b.imu_offsets[e];
+    rr[0] += n_aff(p.imu_filter_noise, nd[0]) + imu;
     rr[1] += n_aff(p.imu_noise, nd[1]);
     rr[2] += n_aff(p.imu_noise, nd[2]);
     rr[3] = rintf(rr[4]);                     // quirk :457-458 (speed-sensor value discarded)
     rr[4] += n_aff(p.imu_filter_noise, nd[4]);
-    float *ob = b.obs_buf + 6 * (size_t)e;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) ob[k] = t_clamp(rr[k], -p.clip_obs, p.clip_obs);
     // command resampling (:384-389)
     float su, yu;
     if (speed_draws) { su = speed_draws[e]; yu = yaw_draws[e]; }
-    else {
-        U4 x = philox(U4{(uint32_t)e, c_lo, c_hi, 0x434D4430u}, k0, k1);
-        su = u01(x.x);
-        yu = u01(x.y);
-    }
-    if (prog == p.speed_freq_update) b.curent_speed[e] = u_aff(p.speed_range[0], p.speed_range[1], su);
-    float yc = b.yaw_command[e];
+    else { su = xch[le][24]; yu = xch[le][25]; }
+    float yc = yawc;
     if (prog == p.yaw_freq_update) yc = u_aff(-F_PI, F_PI, yu);
     if (yc > F_PI) yc = yc - F_2PI;
     if (yc < -F_PI) yc = yc + F_2PI;
+    if (!owner) return;
+    b.progress_buf[e] = prog;
+    float *bo = b.buffer_obs + 6 * (size_t)e;
+    float *ob = b.obs_buf + 6 * (size_t)e;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        bo[k] = o[k];
+        ob[k] = t_clamp(rr[k], -p.clip_obs, p.clip_obs);
+    }
+    b.rew_buf[e] = felt ? -100.0f : rew;
+    b.reset_buf[e] = reset;
+    if (prog == p.speed_freq_update) b.curent_speed[e] = u_aff(p.speed_range[0], p.speed_range[1], su);
     b.yaw_command[e] = yc;
     b.timeout_buf[e] = (prog >= p.max_episode_length - 1) && (reset != 0);
 }
@@ -284,8 +381,7 @@ int launch_gogoro_pre(const tg_gogoro_params &p, const tg_gogoro_buffers &b, con
 int launch_gogoro_post(const tg_gogoro_params &p, const tg_gogoro_buffers &b, const float *reset_draws,
                        const float *obs_draws, const float *speed_draws, const float *yaw_draws, uint64_t counter,
                        hipStream_t stream) {
-    const int t = env_threads(p.num_envs);
-    dim3 grid((p.num_envs + t - 1) / t), block(t);
+    dim3 grid((p.num_envs + POST_EPB - 1) / POST_EPB), block(64);
     hipLaunchKernelGGL(post_kernel, grid, block, 0, stream, p, b, reset_draws, obs_draws, speed_draws, yaw_draws,
                        (uint32_t)counter, (uint32_t)(counter >> 32));
     return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
