@@ -117,6 +117,14 @@ int tg_gogoro_post_physics(tg_sim *sim, const tg_gogoro_params *p, const tg_gogo
                            const float *reset_draws, const float *obs_draws, const float *speed_draws,
                            const float *yaw_draws, uint64_t counter);
 
+/* One VecTask.step (vec_task.py:313-359): pre_physics_step + n_simulate x
+ * simulate + post_physics_step with in-kernel Philox draws -- the same results
+ * as tg_gogoro_pre_physics(counter_pre) + n_simulate x tg_simulate +
+ * tg_gogoro_post_physics(counter_post) with NULL draw arrays, the pre-physics
+ * work fused into the first simulate's compose launch. */
+int tg_gogoro_step(tg_sim *sim, const tg_gogoro_params *p, const tg_gogoro_buffers *b, const float *actions,
+                   int32_t n_simulate, uint64_t counter_pre, uint64_t counter_post);
+
 /* Gogoro.reset_idx(env_ids) outside post_physics_step (gogoro_new.py:150,505-591;
  * VecTask.reset_done, vec_task.py:391-406): ids [n] int32 device, reset_draws
  * [N,11] (rows of the listed envs used) or NULL. */

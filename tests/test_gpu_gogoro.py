@@ -127,3 +127,33 @@ def test_gpu_env_step_matches_oracle_along_1000_steps():
     print(err)
     assert err["obs"] < 1e-3 and err["rew"] < 1e-3, err
     assert err["reset_equal"] and err["timeout_equal"], err
+
+
+def test_gpu_gogoro_fused_step_matches_separate_calls():
+    """tg_gogoro_step (pre-physics fused into the compose launch) against
+    tg_gogoro_pre_physics + tg_simulate + tg_gogoro_post_physics (the
+    VecTask.step sequence) with in-kernel Philox draws, resets included.  The
+    fused prologue is compiled in the fast-math physics translation unit
+    (its sqrt in the Box-Muller draw may differ in the last bit), so the
+    comparison is to 1e-4 over a free-running horizon; resets and progress
+    must be identical."""
+    _cuda()
+    import thormang_isaacgym_amd as tia
+    from thormang_isaacgym_amd.tasks.base.vec_task import VecTask
+    envs = [tia.make(seed=21, task="Gogoro", num_envs=512, sim_device="cuda:0", rl_device="cuda:0")
+            for _ in range(2)]
+    f, u = envs
+    g = torch.Generator(device="cuda:0").manual_seed(9)
+    n_reset = 0
+    for _ in range(40):
+        a = torch.rand(512, 1, device="cuda:0", generator=g) * 2 - 1
+        f.step(a)
+        VecTask.step(u, a)
+        torch.cuda.synchronize()
+        assert torch.equal(f.reset_buf, u.reset_buf) and torch.equal(f.progress_buf, u.progress_buf)
+        for x, y, what in ((f.obs_buf, u.obs_buf, "obs"), (f.rew_buf, u.rew_buf, "rew"),
+                           (f.root_tensor, u.root_tensor, "root")):
+            d = float((x - y).abs().max())
+            assert d <= 1e-4, (what, d)
+        n_reset += int(f.reset_buf.sum())
+    assert n_reset > 0

@@ -98,11 +98,34 @@ __device__ __forceinline__ void target_prologue(const StepArgs &a, int e, int la
     a.pm_tgt_out[i] = a.pm_default[lane] + a.pm_scale * c;
 }
 
+// Prologue (tg_gogoro_step): gogoro_task.hip pre_kernel for env e on one lane
+// -- the same fp32 operations (no contraction / reassociation here either)
+// and the same Philox draw.
+__device__ __forceinline__ void gogoro_pre_prologue(const GogoroPre &g, int e, int D) {
+#pragma clang fp contract(off) reassociate(off)
+    const float x = g.actions[e];
+    const float a = x < -g.clip_actions ? -g.clip_actions : (x > g.clip_actions ? g.clip_actions : x);
+    float *ah = g.action_history + 5 * (size_t)e;
+    const float h0 = ah[1], h1 = ah[2], h2 = ah[3], h3 = ah[4];
+    ah[0] = h0; ah[1] = h1; ah[2] = h2; ah[3] = h3; ah[4] = a;
+    const float m = g.max_steering_change, ms = g.max_steering;
+    float da = a * m;
+    da = da < -m ? -m : (da > m ? m : da);
+    float c = g.curent_command[e] + da;
+    c = c < -ms ? -ms : (c > ms ? ms : c);
+    g.curent_command[e] = c;
+    const U4 u = philox(U4{(uint32_t)e, g.c_lo, g.c_hi, 0x50524531u}, g.k0, g.k1);
+    const float noise = g.noise_mean + gauss(u.x, u.y) * g.noise_std;
+    g.pos_target[(size_t)e * D + g.dof_steer] = c + g.steer_offsets[e] + noise;
+    g.vel_target[(size_t)e * D + g.dof_rear] = g.curent_speed[e];
+}
+
 template <class M> __global__ __launch_bounds__(64 * COMPOSE_WPB) void compose_kernel(StepArgs a) {
     const int wv = threadIdx.x / 64;
     const int e = blockIdx.x * COMPOSE_WPB + wv;
     const bool dirty = e < a.N && a.dirty[e] != 0;   // read before the prologue: one memory latency
     if (a.pm_actions && e < a.N) target_prologue(a, e, threadIdx.x % 64);
+    if (a.gp.actions && e < a.N && threadIdx.x % 64 == 0) gogoro_pre_prologue(a.gp, e, a.D);
     if (!dirty) return;
     TG_CPROF_INIT
     using CL = CompLayout<M>;

@@ -13,6 +13,16 @@ namespace tg {
 
 constexpr int TG_PM_MAX_DOF = 64;   // prologue lanes: one wavefront per env, lane = dof
 
+// optional Gogoro pre-physics prologue of the compose launch (tg_gogoro_step)
+struct GogoroPre {
+    const float *actions;     // [N] (null: none)
+    float *action_history, *curent_command, *pos_target, *vel_target;
+    const float *steer_offsets, *curent_speed;
+    float clip_actions, max_steering_change, max_steering, noise_mean, noise_std;
+    int dof_steer, dof_rear;
+    uint32_t k0, k1, c_lo, c_hi;
+};
+
 struct StepArgs {
     int N, D;
     float h;
@@ -42,6 +52,7 @@ struct StepArgs {
     float *pm_tgt_out;        // [N,D] position targets
     float pm_scale, pm_clip;
     float pm_default[TG_PM_MAX_DOF];
+    GogoroPre gp;
 };
 
 // tg_walk_step's fused post-physics epilogue (articulation.hip WalkPost)

@@ -477,6 +477,42 @@ int tg_gogoro_pre_physics(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_
     return TG_OK;
 }
 
+int tg_gogoro_step(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_buffers *b, const float *actions,
+                   int32_t n_simulate, uint64_t counter_pre, uint64_t counter_post) {
+    if (int rc = check_sim(s)) return rc;
+    if (!p || !b || !actions) return fail(TG_ERR_ARG, "tg_gogoro_step: null argument");
+    if (p->num_envs != s->N || p->num_dof != s->D) return fail(TG_ERR_ARG, "gogoro params do not match the sim");
+    if (n_simulate < 1) return fail(TG_ERR_ARG, "tg_gogoro_step: n_simulate %d < 1", n_simulate);
+    for (int i = 0; i < n_simulate; ++i) {
+        tg::StepArgs a = step_args(s);
+        if (i == 0) {   // pre_physics_step fused into the first compose launch
+            tg::GogoroPre &g = a.gp;
+            g.actions = actions;
+            g.action_history = b->action_history;
+            g.curent_command = b->curent_command;
+            g.pos_target = b->pos_target;
+            g.vel_target = b->vel_target;
+            g.steer_offsets = b->steer_offsets;
+            g.curent_speed = b->curent_speed;
+            g.clip_actions = p->clip_actions;
+            g.max_steering_change = p->max_steering_change;
+            g.max_steering = p->max_steering;
+            g.noise_mean = p->steering_action_noise[0];
+            g.noise_std = p->steering_action_noise[1];
+            g.dof_steer = p->dof_steer;
+            g.dof_rear = p->dof_rear;
+            g.k0 = (uint32_t)p->seed;
+            g.k1 = (uint32_t)(p->seed >> 32);
+            g.c_lo = (uint32_t)counter_pre;
+            g.c_hi = (uint32_t)(counter_pre >> 32);
+        }
+        if (int rc = simulate_args(s, a)) return rc;
+    }
+    if (int rc = tg::launch_gogoro_post(*p, *b, nullptr, nullptr, nullptr, nullptr, counter_post, s->stream))
+        return fail(rc, "launch failed");
+    return TG_OK;
+}
+
 int tg_gogoro_post_physics(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_buffers *b, const float *reset_draws,
                            const float *obs_draws, const float *speed_draws, const float *yaw_draws, uint64_t counter) {
     if (int rc = check_sim(s)) return rc;

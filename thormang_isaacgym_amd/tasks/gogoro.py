@@ -226,6 +226,10 @@ class Gogoro(VecTask):
         check(lib().tg_gogoro_post_physics(self.sim.handle, C.byref(self.params), C.byref(self._bufs), _p(rd), _p(od),
                                            _p(sd), _p(yd), self._counter()), "tg_gogoro_post_physics")
         self._keep_post = keep
+        self._post_host()
+
+    def _post_host(self):
+        """Host-side tail of post_physics_step (step count, periodic non-env DR)."""
         self.curent_step += 1
         # non-env DR (gravity every `frequency` frames, gogoro_new.py:476 -> vec_task.py:559)
         freq = self.randomization_params.get("frequency", 1)
@@ -239,10 +243,23 @@ class Gogoro(VecTask):
     def step(self, actions):
         if self.dr_randomizations.get("actions", None) or self.dr_randomizations.get("observations", None):
             return super().step(actions)
-        self.pre_physics_step(actions)
-        for _ in range(self.control_freq_inv):
-            self.simulate()
-        self.post_physics_step()
+        if self.draw_source is None:
+            # pre_physics_step + control_freq_inv x simulate + post_physics_step in
+            # one library call (tg_gogoro_step: the pre-physics work rides in the
+            # first simulate's compose launch); same counters as the separate calls
+            a = actions.to(device=self.device, dtype=torch.float32).contiguous()
+            c_pre = self._counter()
+            c_post = self._counter()
+            check(lib().tg_gogoro_step(self.sim.handle, C.byref(self.params), C.byref(self._bufs), _p(a),
+                                       self.control_freq_inv, c_pre, c_post), "tg_gogoro_step")
+            self._keep = (a, None)
+            self.frame_count += self.control_freq_inv
+            self._post_host()
+        else:
+            self.pre_physics_step(actions)
+            for _ in range(self.control_freq_inv):
+                self.simulate()
+            self.post_physics_step()
         self.extras["time_outs"] = self.timeout_buf
         self.obs_dict["obs"] = self.obs_buf
         if self.num_states > 0:
