@@ -640,7 +640,118 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         TG_SYNC();
         TG_PROF(17)
         // ---- pass 2b: schedule backward, children contributions gathered
-        {
+        if constexpr (M::PAIR) {
+        // Lane pairs split the group's update as the same instructions on
+        // different data: with I = [A B; B^T C] acting on (w, v), lane half 0
+        // computes the angular rows (X = A, Y = B, S1 = S.w, S2 = S.v), half 1
+        // the linear rows (X = C, Y = B^T, S1 = S.v, S2 = S.w).  Dot products
+        // over the 6-vector are completed with the partner's half (DPP swap);
+        // B's update is formed so that both halves compute its entries from the
+        // same two factors, and half 0 stores it.
+        const int hh = sub >= M::SL ? 1 : 0;
+        const bool hb = hh != 0;
+        auto pswap3 = [](const float *v, float *o) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) o[k] = pair_swap(v[k]);
+        };
+#pragma unroll 1
+        for (int t = M::NSTEP - 1; t >= 0; --t) {
+            const I4 dc = dsc(t);
+            const int g = dc.x;
+            if (g > 0) {
+                const int o = g * GF;
+                float X[6], Bm[9], ph[3], cb1[3], cb2[3];
+#pragma unroll
+                for (int k = 0; k < 6; ++k) X[k] = s(o + F_IA + 15 * hh + k);
+#pragma unroll
+                for (int k = 0; k < 9; ++k) Bm[k] = s(o + F_IA + 6 + k);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    ph[k] = s(o + F_PA + 3 * hh + k);
+                    cb1[k] = s(o + F_V + 3 * hh + k);
+                    cb2[k] = s(o + F_V + 3 - 3 * hh + k);
+                }
+                const SV Sg = ldS(s, g, d_jt(dc));
+                const float c0 = s(o + F_DINV), tau = s(o + F_UU), al = s(o + F_QDS), c1 = s(o + F_C1);
+                // children: every load issued before the first add (absent children read the zero block)
+                auto gather2 = [&](auto NCc) {
+                    constexpr int n = decltype(NCc)::value;
+                    float cx[n][6], cbm[n][9], cp[n][3];
+#pragma unroll
+                    for (int c = 0; c < n; ++c) {
+                        const bool has = c < d_nch(dc);
+                        const int ch = d_child(dc, c);
+                        const float *pi = has ? s.b + ia_c(ch) : zeros, *pp = has ? s.b + pa_c(ch) : zeros;
+#pragma unroll
+                        for (int k = 0; k < 6; ++k) cx[c][k] = pi[15 * hh + k];
+#pragma unroll
+                        for (int k = 0; k < 9; ++k) cbm[c][k] = pi[6 + k];
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) cp[c][k] = pp[3 * hh + k];
+                    }
+#pragma unroll
+                    for (int c = 0; c < n; ++c) {
+#pragma unroll
+                        for (int k = 0; k < 6; ++k) X[k] += cx[c][k];
+#pragma unroll
+                        for (int k = 0; k < 9; ++k) Bm[k] += cbm[c][k];
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) ph[k] += cp[c][k];
+                    }
+                };
+                const int smax = d_smax(dc);
+                if (smax == 1) gather2(std::integral_constant<int, 1>{});
+                else if (smax == 2) gather2(std::integral_constant<int, 2>{});
+                else if (smax >= 3) gather2(std::integral_constant<int, 3>{});
+                // the half's orientation of B
+                float Y[9];
+                Y[0] = Bm[0]; Y[4] = Bm[4]; Y[8] = Bm[8];
+                Y[1] = hb ? Bm[3] : Bm[1]; Y[3] = hb ? Bm[1] : Bm[3];
+                Y[2] = hb ? Bm[6] : Bm[2]; Y[6] = hb ? Bm[2] : Bm[6];
+                Y[5] = hb ? Bm[7] : Bm[5]; Y[7] = hb ? Bm[5] : Bm[7];
+                const V3 S1 = hb ? Sg.v : Sg.w, S2 = hb ? Sg.w : Sg.v;
+                const V3 Uv = symmul(X, S1) + bmul(Y, S2);
+                const float Uh[3] = {Uv.x, Uv.y, Uv.z};
+                const float d0 = dot(S1, Uv);
+                const float D0 = d0 + pair_swap(d0);   // S.U, without the armature (folded into c0, tau)
+                const float sp = dot(S1, v3(ph[0], ph[1], ph[2]));
+                const float SpA = sp + pair_swap(sp);
+                const float Dinv = 1.0f / (c1 * D0 + c0);
+                const float u = tau + al * D0 - SpA;
+                float Uo[3], DUh[3], DUo[3], Pf[3], Qf[3];
+                pswap3(Uh, Uo);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    DUh[k] = Dinv * Uh[k];
+                    DUo[k] = Dinv * Uo[k];
+                    Pf[k] = hb ? Uh[k] : DUh[k];   // B entries from the same two factors on both halves
+                    Qf[k] = hb ? DUo[k] : Uo[k];
+                }
+                const int ii[6] = {0, 1, 2, 0, 0, 1}, jj[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+                for (int k = 0; k < 6; ++k) X[k] -= DUh[ii[k]] * Uh[jj[k]];
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) Y[3 * i + j] -= Pf[i] * Qf[j];
+                const float ud = u * Dinv;
+                const V3 pav = v3(ph[0], ph[1], ph[2]) + symmul(X, v3(cb1[0], cb1[1], cb1[2])) +
+                               bmul(Y, v3(cb2[0], cb2[1], cb2[2])) + ud * Uv;
+                stv3(s, o + F_U + 3 * hh, Uv);
+                s(o + F_DINV) = Dinv;
+                s(o + F_UU) = u;
+                // contribution to the parent (same frame: no transform)
+#pragma unroll
+                for (int k = 0; k < 6; ++k) s(ia_c(g) + 15 * hh + k) = X[k];
+                if (!hb) {
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) s(ia_c(g) + 6 + k) = Y[k];
+                }
+                stv3(s, pa_c(g) + 3 * hh, pav);
+            }
+            TG_SYNC();
+        }
+        } else {
 #pragma unroll 1
         for (int t = M::NSTEP - 1; t >= 0; --t) {
             const I4 dc = dsc(t);
