@@ -543,23 +543,24 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
             }
             TG_SYNC();
         };
-        // one schedule step per iteration; step t + 1's inputs are loaded
-        // before step t runs and reach it through the loop back-edge, so the
-        // compiler cannot sink the load into the step that consumes it (which
-        // exposed the full L2 latency on every step).  The loads are
-        // unconditional (idle lanes read group 0's row).
-        float kc[12], kn[12];
-        I4 dA = dsc(0), dB = M::NSTEP > 1 ? dsc(1) : I4{0, 0, 0, 0};
-        load_kin(dA.x, kc);
-#pragma unroll 1
-        for (int t = 0; t < M::NSTEP; ++t) {
-            load_kin(dB.x, kn);
-            const I4 dC = t + 2 < M::NSTEP ? dsc(t + 2) : I4{0, 0, 0, 0};
-            body1(dA, kc);
+        // fully unrolled, inputs two steps ahead in a 3-deep ring (renamed
+        // registers, no copies: the wait for step t's inputs leaves steps
+        // t + 1 and t + 2 in flight)
+        float kr[3][12];
+        I4 dr[3];
+        dr[0] = dsc(0);
+        load_kin(dr[0].x, kr[0]);
+        if constexpr (M::NSTEP > 1) {
+            dr[1] = dsc(1);
+            load_kin(dr[1].x, kr[1]);
+        }
 #pragma unroll
-            for (int k = 0; k < 12; ++k) kc[k] = kn[k];
-            dA = dB;
-            dB = dC;
+        for (int t = 0; t < M::NSTEP; ++t) {
+            if (t + 2 < M::NSTEP) {
+                dr[(t + 2) % 3] = dsc(t + 2);
+                load_kin(dr[(t + 2) % 3].x, kr[(t + 2) % 3]);
+            }
+            body1(dr[t % 3], kr[t % 3]);
         }
         TG_PROF(16)
 #pragma unroll
