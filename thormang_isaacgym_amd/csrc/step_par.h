@@ -578,6 +578,67 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         // acceleration cb -- parked in the group's own slots (F_V: cb, which
         // pass 3 reads too; F_DINV: c0, F_UU: tau, F_QDS: limit torque per D0, F_C1: 1 +
         // limit gain per D0)
+        if constexpr (NR1 > 1) {
+        // Every round's drive inputs are loaded first (clamped group index: the
+        // loads are unconditional) and consumed by branch-free arithmetic with
+        // only the stores predicated, so the compiler cannot sink a load into a
+        // conditional block that uses it: the rounds share one memory latency.
+        float cdr[NR1][10];
+#pragma unroll
+        for (int r = 0; r < NR1; ++r) {
+            const int gc = min(max(sub + r * LPE, 1), M::NG - 1);
+            load_drv(gi[gc * GIW + GI_DOF], cdr[r]);
+        }
+#pragma unroll
+        for (int r = 0; r < NR1; ++r) {
+            const int g0 = sub + r * LPE;
+            const bool valid = g0 > 0 && g0 < M::NG;
+            const int g = min(max(g0, 1), M::NG - 1);
+            const int o = g * GF;
+            const float *cd = cdr[r];
+            const float q = s(o + F_Q), qd = s(o + F_QD), qdd0 = s(o + F_UU);
+            const int mode = (int)rintf(cd[1]);
+            const float kp = cd[2], kd = cd[3];
+            const float eff = cd[4];
+            const bool drv = mode == TG_DOF_MODE_POS || mode == TG_DOF_MODE_VEL;
+            const float te = kp * (cd[7] - q - h * qd) + kd * (cd[8] - qd);
+            const float K = h * kd + h * h * kp;
+            // implicit, or (rerun) clamped to +-effort when the implicit torque of the first solve exceeds it
+            const float ti = te - K * qdd0;   // qdd0: qdd of the first solve
+            const bool clampd = drv && cp == 1 && fabsf(ti) > eff;
+            const bool implicit = drv && !clampd;
+            const float ef = (mode == TG_DOF_MODE_EFFORT && a.act) ? fminf(fmaxf(cd[9], -eff), eff) : 0.f;
+            const float tau = implicit ? te : (clampd ? (ti > 0.f ? eff : -eff) : ef);
+            const float Dimp = implicit ? K : 0.f;
+            const float cl0 = drv ? te : 0.f, cl1 = drv ? K : -1.f;   // clamp scratch (te, K) of the first solve
+            // limit spring + damping (kl = lim_k D0 / h^2, cl = lim_c D0 / h),
+            // damping/implicit terms ramped in past the limit
+            const float lo = cd[5], hi = cd[6];
+            const float qp = q + h * qd;
+            const bool below = qp < lo && lo > -1e30f, above = !below && qp > hi && hi < 1e30f;
+            const float lim = below ? lo : hi;
+            const float rr = fminf(fabsf(lim - qp) * (1.0f / TG_LIMIT_RAMP), 1.0f);
+            const bool on = below || above;
+            const float al = on ? a.lim_k / (h * h) * (lim - qp) - rr * a.lim_c / h * qd : 0.f;
+            const float be = on ? rr * (a.lim_c + a.lim_k) : 0.f;
+            // with D0 = S.I^A.S + armature: D = (1 + be) D0 + Dimp, tau + al D0
+            // cb replaces v (dead after pass 1b) in F_V; on a SEPC rerun pass 1
+            // was not rerun and F_V already holds cb
+            const SV cbv = crm(ldsv(s, o + F_V), qd * ldS(s, g, gi[g * GIW + GI_JT]));
+            if (valid) {
+                if (cp == 0) {
+                    s(o + F_CL) = cl0;
+                    s(o + F_CL + 1) = cl1;
+                    s(o + F_CL + 2) = eff;
+                }
+                if (!SEPC || cp == 0) stsv(s, o + F_V, cbv);
+                s(o + F_DINV) = (1.f + be) * cd[0] + Dimp;
+                s(o + F_UU) = tau + al * cd[0];
+                s(o + F_QDS) = al;
+                s(o + F_C1) = 1.f + be;
+            }
+        }
+        } else {   // one round (small trees): loads consumed at once, branches kept
 #pragma unroll
         for (int r = 0; r < NR1; ++r) {
             const int g = sub + r * LPE;
@@ -637,6 +698,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                 s(o + F_QDS) = al;
                 s(o + F_C1) = 1.f + be;
             }
+        }
         }
         TG_SYNC();
         TG_PROF(17)
