@@ -877,25 +877,39 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         }
         TG_SYNC();
         {
-        I4 d1 = dsc(0);
-#pragma unroll 1
+        // fully unrolled; a step's own-group inputs (written by passes 2a/2b,
+        // untouched by the earlier steps) are loaded one step ahead, so only
+        // the parent's acceleration is waited on along the chain
+        struct Own { SV cb, U, S; float qd, uu, dinv, te, K, eff; };
+        auto ld_own = [&](const I4 &dc) {
+            const int g = max(dc.x, 0), o = g * GF;
+            return Own{ldsv(s, o + F_V), ldsv(s, o + F_U), ldS(s, g, d_jt(dc)),
+                       s(o + F_QD), s(o + F_UU), s(o + F_DINV),
+                       s(o + F_CL), s(o + F_CL + 1), s(o + F_CL + 2)};
+        };
+        I4 dr[2];
+        Own ow[2];
+        dr[0] = dsc(0);
+        ow[0] = ld_own(dr[0]);
+#pragma unroll
         for (int t = 0; t < M::NSTEP; ++t) {
-            const I4 dc = d1;
-            d1 = t + 1 < M::NSTEP ? dsc(t + 1) : I4{0, 0, 0, 0};
+            const I4 dc = dr[t % 2];
+            const Own &w = ow[t % 2];
             const int g = dc.x;
+            const SV apar = ldsv(s, ac_s(max(dc.y, 0)));
+            if (t + 1 < M::NSTEP) {
+                dr[(t + 1) % 2] = dsc(t + 1);
+                ow[(t + 1) % 2] = ld_own(dr[(t + 1) % 2]);
+            }
             if (g > 0) {
                 const int o = g * GF;
-                const SV apar = ldsv(s, ac_s(dc.y)), cb = ldsv(s, o + F_V), Ug = ldsv(s, o + F_U);
-                const SV Sg = ldS(s, g, d_jt(dc));
-                const float qd = s(o + F_QD), uu = s(o + F_UU), dinv = s(o + F_DINV);
-                const float te = s(o + F_CL), K = s(o + F_CL + 1), eff = s(o + F_CL + 2);
-                const SV ap = apar + cb;   // cb: pass 2a
-                const float qdd = (uu - dot(Ug, ap)) * dinv;
-                stsv(s, ac_s(g), ap + qdd * Sg);
-                s(o + F_QDS) = qd + h * qdd;
+                const SV ap = apar + w.cb;   // cb: pass 2a
+                const float qdd = (w.uu - dot(w.U, ap)) * w.dinv;
+                stsv(s, ac_s(g), ap + qdd * w.S);
+                s(o + F_QDS) = w.qd + h * qdd;
                 if (cp == 0) {
                     s(o + F_UU) = qdd;
-                    if (K >= 0.f && fabsf(te - K * qdd) > eff) s(PL::FLG) = 1.f;
+                    if (w.K >= 0.f && fabsf(w.te - w.K * qdd) > w.eff) s(PL::FLG) = 1.f;
                 }
             }
             TG_SYNC();
@@ -1230,20 +1244,31 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
             if (lead) stsv(s, F_PA, da0);
             TG_SYNC();
             {
-            I4 d1 = dsc(0);
-#pragma unroll 1
+            // fully unrolled, own-group inputs one step ahead (as in pass 3)
+            struct OwnI { SV U, S; float uu, dinv, qds; };
+            auto ld_own = [&](const I4 &dc) {
+                const int g = max(dc.x, 0), o = g * GF;
+                return OwnI{ldsv(s, o + F_U), ldS(s, g, d_jt(dc)), s(o + F_UU), s(o + F_DINV), s(o + F_QDS)};
+            };
+            I4 dr[2];
+            OwnI ow[2];
+            dr[0] = dsc(0);
+            ow[0] = ld_own(dr[0]);
+#pragma unroll
             for (int t = 0; t < M::NSTEP; ++t) {
-                const I4 dc = d1;
-                d1 = t + 1 < M::NSTEP ? dsc(t + 1) : I4{0, 0, 0, 0};
+                const I4 dc = dr[t % 2];
+                const OwnI &w = ow[t % 2];
                 const int g = dc.x;
+                const SV ap = ldsv(s, max(dc.y, 0) * GF + F_PA);
+                if (t + 1 < M::NSTEP) {
+                    dr[(t + 1) % 2] = dsc(t + 1);
+                    ow[(t + 1) % 2] = ld_own(dr[(t + 1) % 2]);
+                }
                 if (g > 0) {
                     const int o = g * GF;
-                    const SV ap = ldsv(s, dc.y * GF + F_PA), Ug = ldsv(s, o + F_U);
-                    const SV Sg = ldS(s, g, d_jt(dc));
-                    const float uu = s(o + F_UU), dinv = s(o + F_DINV), qds = s(o + F_QDS);
-                    const float x = (uu - dot(Ug, ap)) * dinv;
-                    stsv(s, o + F_PA, ap + x * Sg);
-                    s(o + F_QDS) = qds + x;
+                    const float x = (w.uu - dot(w.U, ap)) * w.dinv;
+                    stsv(s, o + F_PA, ap + x * w.S);
+                    s(o + F_QDS) = w.qds + x;
                 }
                 TG_SYNC();
             }
