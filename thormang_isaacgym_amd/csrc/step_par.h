@@ -228,6 +228,24 @@ template <int L> __device__ __forceinline__ float sum_lanes(float v) {
     if constexpr (L == 8) return sum8(v);
     else return sum16(v);
 }
+// lane n of the env's LPE lanes, on every lane of the env: DPP row_newbcast
+// (lane n of each 16-lane row to the whole row); an 8-lane env takes its
+// half's lane
+template <int L> __device__ __forceinline__ float env_bcast(float v, int n, int sub) {
+    static_assert(L == 8 || L == 16, "env lanes: 8 or 16");
+    auto bc = [&](int m) {
+        switch (m) {
+        case 0: return dpp<0x150>(v); case 1: return dpp<0x151>(v); case 2: return dpp<0x152>(v);
+        case 3: return dpp<0x153>(v); case 4: return dpp<0x154>(v); case 5: return dpp<0x155>(v);
+        case 6: return dpp<0x156>(v); case 7: return dpp<0x157>(v); case 8: return dpp<0x158>(v);
+        case 9: return dpp<0x159>(v); case 10: return dpp<0x15A>(v); case 11: return dpp<0x15B>(v);
+        case 12: return dpp<0x15C>(v); case 13: return dpp<0x15D>(v); case 14: return dpp<0x15E>(v);
+        default: return dpp<0x15F>(v);
+        }
+    };
+    if constexpr (L == 16) return bc(n);
+    else return (threadIdx.x & 8) ? bc(n + 8) : bc(n);
+}
 // the partner lane's value (lane pairs sub, sub + 8 of a 16-lane row)
 __device__ __forceinline__ float pair_swap(float v) { return dpp<0x128>(v); }
 
@@ -1108,6 +1126,79 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                 for (int g = sub; g < M::NG; g += LPE) stsv(s, g * GF + F_PA, sv0());
                 TG_SYNC();
             }
+            if constexpr (LPE == 16) {
+            // projected Gauss-Seidel with patch friction, all LPE lanes of the env:
+            // lane sub owns rows k = sub + LPE*jj -- its W rows and its entries of
+            // the row velocities r = vfree + W lambda, kept current incrementally
+            // (a multiplier change d adds W[k][c] d, one FMA per lane); a row's
+            // velocity reaches every lane of the env by one DPP row broadcast,
+            // and every lane computes the same update (the full multiplier
+            // vector in registers, no LDS traffic in the sweeps)
+            {
+                constexpr int JL = (K + LPE - 1) / LPE;
+                float wr[JL][K], rv[JL], tg[K], onr[K], wd[K], lam[K];
+#pragma unroll
+                for (int jj = 0; jj < JL; ++jj) {
+                    const int k = sub + LPE * jj;
+#pragma unroll
+                    for (int c = 0; c < K; ++c) wr[jj][c] = k < K ? s(PL::W + k * K + c) : 0.f;
+                    rv[jj] = k < K ? s(PL::VFREE + k) : 0.f;
+                }
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    tg[i] = s(PL::ROW + i * 8 + 6);
+                    onr[i] = s(PL::ROW + i * 8 + 7);
+                    wd[i] = s(PL::W + i * K + i);
+                    lam[i] = 0.f;
+                }
+                auto row_v = [&](int i) {   // vfree_i + (W lambda)_i, from its owner lane
+                    return env_bcast<LPE>(rv[i / LPE], i % LPE, sub);
+                };
+                auto set_lam = [&](int i, float v) {
+                    const float d = v - lam[i];
+                    lam[i] = v;
+#pragma unroll
+                    for (int jj = 0; jj < JL; ++jj) rv[jj] += wr[jj][i] * d;
+                };
+#pragma unroll 1
+                for (int it = 0; it < a.iters; ++it) {
+#pragma unroll
+                    for (int sh = 0; sh < M::NS; ++sh) {
+                        const int rb = row_base<M>(sh), nr = M::shape_nrows[sh];
+                        float Nsum = 0.f;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            if (k >= nr) break;
+                            const int i = rb + k;
+                            const float vi = row_v(i);
+                            const float l = lam[i] + (tg[i] - vi) / wd[i];
+                            const float li = onr[i] * fmaxf(l, 0.f);
+                            set_lam(i, li);
+                            Nsum += li;
+                        }
+                        const int f = rb + nr;
+                        const float mu = s(PL::SHP + 2 * sh), reff = s(PL::SHP + 2 * sh + 1);
+                        // tangent 1, then tangent 2 with the cone projection of the
+                        // pair, then the torsional row clamped
+                        set_lam(f, lam[f] - row_v(f) / wd[f]);
+                        {
+                            const float l0 = lam[f], l1 = lam[f + 1] - row_v(f + 1) / wd[f + 1];
+                            const float lt = sqrtf(l0 * l0 + l1 * l1), lim = mu * Nsum;
+                            const float sc = lt > lim ? (lt > 0.f ? lim / lt : 0.f) : 1.f;
+                            set_lam(f, l0 * sc);
+                            set_lam(f + 1, l1 * sc);
+                        }
+                        const float lim3 = mu * Nsum * reff;
+                        set_lam(f + 2, fminf(fmaxf(lam[f + 2] - row_v(f + 2) / wd[f + 2], -lim3), lim3));
+                    }
+                }
+                if (lead) {
+#pragma unroll
+                    for (int i = 0; i < K; ++i) s(PL::LAM + i) = lam[i];
+                }
+            }
+            } else {   // 8-lane envs: the row velocity by an 8-lane reduction (two broadcasts
+                       // and a select measured slower than the three DPP levels)
             // projected Gauss-Seidel with patch friction, all LPE lanes of the env:
             // each lane holds W's columns j = sub + LPE*jj and the full multiplier
             // vector in registers; a row's W*lambda is an 8-lane reduction, so
@@ -1181,6 +1272,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
 #pragma unroll
                     for (int i = 0; i < K; ++i) s(PL::LAM + i) = lam[i];
                 }
+            }
             }
             TG_SYNC();
             SV da0 = sv0();
