@@ -1079,8 +1079,24 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
 #pragma unroll 1
             for (int j = sub; j < K; j += LPE) {
                 const int ck = M::shape_cg[row_shape<M>(j)];
-                const int lk = M::cpath_len[ck];
-                const int *pk = cpath + ck * M::MAXD;
+                // the path of contact group ck (groups, joint types) selected from
+                // the model's constant tables: no LDS round trip before the walk
+                int lk = M::cpath_len[0], pk[M::MAXD], pj[M::MAXD];
+#pragma unroll
+                for (int i = 0; i < M::MAXD; ++i) {
+                    pk[i] = M::cpath[0][i];
+                    pj[i] = M::jtype[M::cpath[0][i] > 0 ? M::cpath[0][i] : 0];
+                }
+#pragma unroll
+                for (int c = 1; c < M::NCG; ++c) {
+                    const bool on = ck == c;
+                    lk = on ? M::cpath_len[c] : lk;
+#pragma unroll
+                    for (int i = 0; i < M::MAXD; ++i) {
+                        pk[i] = on ? M::cpath[c][i] : pk[i];
+                        pj[i] = on ? M::jtype[M::cpath[c][i] > 0 ? M::cpath[c][i] : 0] : pj[i];
+                    }
+                }
                 SV p = -1.0f * rforce(j, 1.0f);
                 float du[M::MAXD];
 #pragma unroll
@@ -1088,7 +1104,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                     du[i] = 0.f;
                     if (i < lk) {
                         const int g = pk[i];
-                        const float u = -dot(ldS(s, g, ginfo<M>(gi, g).jt), p);
+                        const float u = -dot(ldS(s, g, pj[i]), p);
                         du[i] = u;
                         p = p + (u * s(g * GF + F_DINV)) * ldsv(s, g * GF + F_U);
                     }
