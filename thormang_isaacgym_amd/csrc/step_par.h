@@ -506,6 +506,14 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         // LDS store (the compiler keeps LDS loads and stores in program order).
         LDL6 rootf{};
         SV a0 = sv0();
+        // velocity limits of the lane's groups (used by the integration at the
+        // end of the substep), issued now so their latency is hidden
+        float vlim[(M::NG + LPE - 1) / LPE];
+#pragma unroll
+        for (int r = 0; r < (M::NG + LPE - 1) / LPE; ++r) {
+            const int g = 1 + sub + r * LPE;
+            vlim[r] = g < M::NG ? PR(TG_PROP_VELOCITY, gi[g * GIW + GI_DOF]) : 0.f;
+        }
 #pragma unroll 1
         for (int cp = 0; cp < 2; ++cp) {
 #if defined(TG_SECTION_PROF) && defined(TG_CLAMP_COUNT)
@@ -1385,9 +1393,12 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
             TG_PROF(7)
         }
         // ---- velocity limits + integration
-        for (int g = 1 + sub; g < M::NG; g += LPE) {
+#pragma unroll
+        for (int r = 0; r < (M::NG + LPE - 1) / LPE; ++r) {
+            const int g = 1 + sub + r * LPE;
+            if (g >= M::NG) break;
             const int o = g * GF;
-            const float vl = PR(TG_PROP_VELOCITY, gi[g * GIW + GI_DOF]);
+            const float vl = vlim[r];
             float x = s(o + F_QDS);
             if (vl > 0.f) x = fminf(fmaxf(x, -vl), vl);
             s(o + F_QD) = x;
