@@ -41,10 +41,44 @@ HBM_PEAK_GBS = 8000.0
 TIMING_PERIOD = 16
 
 
+def algorithmic_bytes_per_env_step(task_name: str, env) -> tuple[int, dict]:
+    """Algorithmic HBM bytes of one env-step: the state and
+    task buffers the step must read and write once -- inputs resident in HBM,
+    model constants (shared by every env) excluded, and none of this
+    library's own per-env caches counted.  Returns (bytes, breakdown)."""
+    if task_name == "Gogoro":
+        # §8(d) verbatim: read 444 B, write 457 B
+        rd = dict(action=4, root=52, dof=312, cmd=4, a_hist=20, steer_off=4, speed=4, yaw_cmd=4, imu_off=4,
+                  speed_off=4, progress=8, reset=8, steer_kd=4, seat_offsets=12)
+        wr = dict(root=52, dof=312, cmd=4, a_hist=20, progress=8, reset=8, obs=24, buffer_obs=24, rew=4, time_out=1)
+    elif task_name.startswith("ThormangWalk"):
+        # §8(d) "Thormang walk" with the frozen observation layout
+        # (13 + 3 D floats: height, body lin/ang vel, gravity, commands, dof pos/vel, actions)
+        D, O = env.num_dof, env.num_obs
+        rd = dict(action=4 * D, root=52, dof=8 * D, last_action=4 * D, commands=12, progress=8, reset=8)
+        wr = dict(root=52, dof=8 * D, obs=4 * O, last_action=4 * D, rew=4, reset=8, progress=8, time_out=1)
+        if task_name == "ThormangWalkDR":   # §8(d) cfg 5: body-mass scale, foot friction, push
+            G = env.sim.model.num_groups
+            rd.update(mass_scale=4 * G, friction=4 * len(env.sim.model.shapes), push=12)
+    elif task_name == "GogoroPaper":
+        # the paper variant's step: the Gogoro state plus its 20-step clean and
+        # noisy observation histories (8 x 20 floats each, read + written), the
+        # steering-delay ring and command history, the push wrench
+        D, O = env.num_dof, env.num_obs
+        rd = dict(action=4, root=52, dof=8 * D, buffer_obs=4 * O, buffer_obs_noisy=4 * O, cmd_hist=20,
+                  steer_delay=4 * 20, scalars=40, progress=8, reset=8)
+        wr = dict(root=52, dof=8 * D, buffer_obs=4 * O, buffer_obs_noisy=4 * O, obs=4 * O, cmd_hist=20,
+                  steer_delay=4 * 20, rew=4, reset=8, progress=8, time_out=1, push=12)
+    else:
+        raise ValueError(f"no algorithmic byte count for task {task_name}")
+    return sum(rd.values()) + sum(wr.values()), {"read": rd, "write": wr}
+
+
 def kernel_bytes_per_env(task_name: str, env) -> int:
-    """Algorithmic HBM bytes one articulation step reads + writes per env
-    (DESIGN.md §Roofline): root state r/w, dof_state r/w, active-dof targets and
-    properties, locked-dof lock windows, per-env composite cache, shape friction."""
+    """What the articulation step kernel itself moves per env (reported beside
+    the algorithmic count, never as it): root / dof state, active-dof targets
+    and property fields, lock windows, this library's per-env composite cache
+    and shape friction, plus the fused walk post-physics I/O."""
     m = env.sim.model
     D, G, S = m.num_dof, m.num_groups, len(m.shapes)
     na = len(m.active_dofs)
@@ -53,14 +87,48 @@ def kernel_bytes_per_env(task_name: str, env) -> int:
     read = 13 * 4 + na * 2 * 4 + na * 2 * 4 + na * 8 * 4 + nl * 2 * 4 + kc * 4 + S * 4 + 1
     write = 13 * 4 + D * 2 * 4
     if task_name.startswith("ThormangWalk"):
-        # post-physics fused into the kernel (tg_walk_step): progress, reset flag,
-        # actions, last actions, commands in; observations, last actions, reward,
-        # reset, timeout, progress out (+ the push wrench row for the DR variant)
         read += 8 + 8 + D * 4 * 2 + 3 * 4
         write += env.num_obs * 4 + D * 4 + 4 + 8 + 1 + 8
         if getattr(env, "push_enabled", False):
             write += 6 * 4
     return read + write
+
+
+def host_cpu_info() -> dict:
+    """The GPU box's host CPU as this process sees it: model name, logical
+    CPUs of the machine (nproc --all), CPUs this process may run on (affinity)
+    and its cgroup CPU quota, if any."""
+    info = {"model": None, "nproc_all": os.cpu_count(), "affinity": None, "cgroup_quota_cpus": None}
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    info["model"] = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                info["cgroup_quota_cpus"] = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    return info
+
+
+def baseline_threads(info: dict) -> int:
+    """All the host cores this process may use: the affinity set, capped by the
+    cgroup quota (a quota below the affinity count would only time-slice)."""
+    n = info.get("affinity") or info.get("nproc_all") or 1
+    q = info.get("cgroup_quota_cpus")
+    if q:
+        n = min(n, max(1, int(q)))
+    return int(n)
 
 
 def timed_region(step, steps: int, world: int, device, sync) -> float:
@@ -97,6 +165,35 @@ def committed_traffic(task_name: str, num_envs: int):
         if "step_par_kernel" in k and "hbm_bytes_per_dispatch" in v:
             return v["hbm_bytes_per_dispatch"], os.path.relpath(hits[-1], REPO) + " (FETCH_SIZE x2 + WRITE_SIZE)"
     return None, None
+
+
+def committed_sq(task_name: str, num_envs: int):
+    """VALU / wait fractions of the step kernel's wave cycles from the newest
+    committed SQ-counter summary (profiles/*/sq_<task><envs>.json,
+    scripts/gpu_pmc_sq.sh), or None.  SQ_WAVE_CYCLES, SQ_ACTIVE_INST_* and
+    SQ_WAIT_* count the same (quad-)cycle unit, summed over the kernel's waves."""
+    import glob
+    hits = sorted(glob.glob(os.path.join(REPO, "profiles", "*", f"sq_{task_name.lower()}{num_envs}.json")))
+    if not hits:
+        return None
+    with open(hits[-1]) as f:
+        d = json.load(f)
+    for k, v in d.items():
+        a = v.get("avg", {})
+        if "step_par_kernel" in k and a.get("SQ_WAVE_CYCLES"):
+            wc = a["SQ_WAVE_CYCLES"]
+            out = {"source": os.path.relpath(hits[-1], REPO)}
+            for key, c in (("valu_active_frac", "SQ_ACTIVE_INST_VALU"), ("wait_any_frac", "SQ_WAIT_ANY"),
+                           ("wait_inst_any_frac", "SQ_WAIT_INST_ANY"), ("active_inst_any_frac", "SQ_ACTIVE_INST_ANY"),
+                           ("lds_active_frac", "SQ_ACTIVE_INST_LDS")):
+                if c in a:
+                    out[key] = a[c] / wc
+            if a.get("SQ_WAVES"):
+                out["valu_insts_per_wave"] = a.get("SQ_INSTS_VALU", 0.0) / a["SQ_WAVES"]
+            if a.get("SQ_LDS_IDX_ACTIVE") and "SQ_LDS_BANK_CONFLICT" in a:
+                out["lds_bank_conflict_frac"] = a["SQ_LDS_BANK_CONFLICT"] / a["SQ_LDS_IDX_ACTIVE"]
+            return out
+    return None
 
 
 def cpu_baseline(task_name: str, num_envs: int, threads: int, terrain_env=None):
@@ -181,7 +278,8 @@ def main():
             torch.distributed.destroy_process_group()
         return
     value = N * args.steps * world / elapsed
-    bpe = kernel_bytes_per_env(args.task, env)
+    bpe, breakdown = algorithmic_bytes_per_env_step(args.task, env)
+    kbpe = kernel_bytes_per_env(args.task, env)
     traffic, traffic_src = committed_traffic(args.task, N)
     achieved = bpe * N / (kern_ms * 1e-3) / 1e9
     sim_cfg = cfg["sim"]
@@ -205,13 +303,23 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "tg::step_par_kernel (one launch per simulate)", "kernel_ms": kern_ms,
-                     "kernel_launches": launches, "kernel_timing": f"HIP events around every {TIMING_PERIOD}th launch of the timed region", "bytes_per_env_step": bpe,
-                     "algorithmic_bytes_per_launch": bpe * N, "traffic_source": traffic_src},
+                     "kernel_launches": launches,
+                     "kernel_timing": f"HIP events around every {TIMING_PERIOD}th launch of the timed region",
+                     "bytes_per_env_step": bpe, "bytes_source": "SURVEY.md §8(d) algorithmic bytes per env-step",
+                     "bytes_breakdown": breakdown, "algorithmic_bytes_per_launch": bpe * N,
+                     "kernel_bytes_per_env_step": kbpe,
+                     "traffic_over_algorithmic": traffic / (bpe * N) if traffic else None,
+                     "traffic_source": traffic_src},
     }
+    sq = committed_sq(args.task, N)
+    if sq is not None:
+        out["roofline"]["issue"] = sq
     if not args.no_cpu_baseline and world == 1:
         try:
-            out["cpu_baseline"] = cpu_baseline(args.task, N, threads=min(16, os.cpu_count() or 1),
+            info = host_cpu_info()
+            out["cpu_baseline"] = cpu_baseline(args.task, N, threads=baseline_threads(info),
                                                terrain_env=env if args.terrain else None)
+            out["cpu_baseline"]["host"] = info
         except Exception as exc:  # baseline is reported, never the measured value
             out["cpu_baseline"] = {"value": None, "error": repr(exc)}
     print(json.dumps(out), flush=True)

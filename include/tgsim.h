@@ -56,6 +56,10 @@ extern "C" {
  * the limit (rad or m), keeping the step continuous at the limit */
 #define TG_LIMIT_RAMP 0.01f
 
+/* widest [lower, upper] window a locked DOF may carry (the reference locks
+ * with 1e-4, tasks/gogoro_new.py:257-262); wider is reported as TG_ERR_STATE */
+#define TG_LOCK_WINDOW_MAX 1e-3f
+
 #define TG_ERR_ARG -1
 #define TG_ERR_HIP -2
 #define TG_ERR_MODEL -3
@@ -191,9 +195,24 @@ int tg_simulate(tg_sim *sim);
  * linear velocity of the link's centre of mass (3, the root-state convention),
  * angular velocity (3); from the current root and dof state, stream-ordered. */
 int tg_rigid_body_states(tg_sim *sim, float *out);
+/* fetch_results(sim, True): waits for the sim stream.  Also reports (once, as
+ * TG_ERR_STATE) a state error a kernel raised since the last call: a locked
+ * DOF whose [lower, upper] window was widened beyond TG_LOCK_WINDOW_MAX. */
 int tg_sync(tg_sim *sim);
 const char *tg_last_error(void);
 uint64_t tg_compiled_model_hashes(uint64_t *out, int32_t cap); /* returns count */
+
+/* Random-number instrumentation (no reference counterpart; the task kernels'
+ * in-kernel draws replace the reference's torch.rand / torch.randn calls):
+ * tg_philox4x32_10 is the library's Philox4x32-10 block function on the host
+ * (ctr[4], key[2] -> out[4]; the same code the kernels run), checked against
+ * Random123's published known-answer vectors.  tg_rng_fill runs it on the
+ * device for blocks i = 0..n-1 with counter (i, counter lo, counter hi, 0) and
+ * key = seed: kind 0 writes the 4 raw 32-bit words per block (out holds 4n
+ * words), kind 1 the 4 uniforms u01(word) in [0, 1), kind 2 the 2 normals
+ * gauss(w0, w1), gauss(w2, w3) per block (out holds 2n floats). */
+void tg_philox4x32_10(const uint32_t *ctr, const uint32_t *key, uint32_t *out);
+int tg_rng_fill(tg_sim *sim, int32_t kind, uint64_t seed, uint64_t counter, float *out, int32_t n);
 
 /* Benchmark instrumentation (no reference counterpart): with period > 0,
  * tg_simulate brackets every period-th articulation step kernel launch with HIP

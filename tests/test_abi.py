@@ -17,7 +17,7 @@ def declared_symbols():
     out = set()
     for h in ("tgsim.h", "tg_gogoro.h", "tg_walk.h", "tg_gogoro_paper.h"):
         text = open(os.path.join(REPO, "include", h)).read()
-        out |= set(re.findall(r"^(?:int|const char \*|uint64_t)\s*(tg_\w+)\(", text, re.M))
+        out |= set(re.findall(r"^(?:int|void|const char \*|uint64_t)\s*(tg_\w+)\(", text, re.M))
     return out
 
 

@@ -52,3 +52,57 @@ def test_two_rank_timed_region_takes_max_over_ranks():
     N = 4096
     value = N * 25 * world / e0                # bench.py: whole-job env-steps/s
     assert value > 0
+
+
+def _rank_rlgames(rank, world, port, out):
+    """One torchrun-style rank: the env creator (make mocked) and the
+    per-iteration episode-statistics gather over gloo."""
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import thormang_isaacgym_amd as tia
+    from thormang_isaacgym_amd import rlgames
+    seen = {}
+
+    def fake_make(seed, task, num_envs, sim_device, rl_device, **kw):
+        seen.update(seed=seed, task=task, num_envs=num_envs, sim_device=sim_device, rl_device=rl_device)
+        return "env"
+
+    real = tia.make
+    tia.make = fake_make
+    try:
+        create = rlgames.get_rlgames_env_creator(seed=42, task_config={"env": {"numEnvs": 8}}, task_name="Gogoro",
+                                                 sim_device="cuda:0", rl_device="cuda:0", multi_gpu=True)
+        env = create()
+    finally:
+        tia.make = real
+    # episode statistics: rank r runs 4 envs; env k finishes an episode of
+    # length k + 1 with reward (r + 1) per step
+    st = rlgames.EpisodeStats(4, "cpu")
+    for t in range(4):
+        rew = torch.full((4,), float(rank + 1))
+        reset = (torch.arange(4) == t).long()
+        st.update(rew, reset)
+    g = st.gather()
+    again = st.gather()
+    out[rank] = (env, dict(seen), g, again)
+    dist.destroy_process_group()
+
+
+def test_two_rank_env_creator_and_episode_gather():
+    world, port = 2, _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_rank_rlgames, args=(world, port, out), nprocs=world, join=True)
+    for r in range(world):
+        env, seen, g, again = out[r]
+        assert env == "env"
+        # rank -> device (LOCAL_RANK) and a distinct Philox key per rank (train.py:81: seed + rank)
+        assert seen["sim_device"] == seen["rl_device"] == f"cuda:{r}"
+        assert seen["seed"] == 42 + r and seen["num_envs"] == 8
+        # 4 episodes per rank, lengths 1..4; returns (r+1)*len; summed over both ranks
+        assert g["episodes"] == 8
+        assert abs(g["mean_length"] - 2.5) < 1e-12
+        assert abs(g["mean_return"] - (1 * 10 + 2 * 10) / 8) < 1e-12
+        assert again["episodes"] == 0          # sums reset after each gather

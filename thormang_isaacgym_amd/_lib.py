@@ -38,6 +38,8 @@ SIGNATURES = {
     "tg_simulate": [_VP],
     "tg_rigid_body_states": [_VP, _VP],
     "tg_sync": [_VP],
+    "tg_philox4x32_10": [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)],
+    "tg_rng_fill": [_VP, C.c_int32, C.c_uint64, C.c_uint64, _VP, C.c_int32],
     "tg_last_error": [],
     "tg_set_kernel_timing": [_VP, C.c_int32],
     "tg_read_kernel_timing": [_VP, C.POINTER(C.c_double), C.POINTER(C.c_int64)],
@@ -65,6 +67,9 @@ SIGNATURES = {
 }
 
 
+RESTYPES = {"tg_last_error": C.c_char_p, "tg_compiled_model_hashes": C.c_uint64, "tg_philox4x32_10": None}
+
+
 def lib() -> C.CDLL:
     global _lib
     if _lib is None:
@@ -75,8 +80,7 @@ def lib() -> C.CDLL:
         for name, args in SIGNATURES.items():
             f = getattr(L, name)
             f.argtypes = args
-            f.restype = C.c_char_p if name == "tg_last_error" else (
-                C.c_uint64 if name == "tg_compiled_model_hashes" else C.c_int)
+            f.restype = RESTYPES.get(name, C.c_int)
         _lib = L
     return _lib
 

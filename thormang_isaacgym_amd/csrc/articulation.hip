@@ -21,6 +21,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "../../include/tgsim.h"
 #include "generated/models.inc"
 #include "tg_math.h"
@@ -173,7 +175,11 @@ template <class M> __global__ __launch_bounds__(64 * COMPOSE_WPB) void compose_k
             tl = v3(o[9], o[10], o[11]);
             const int d = M::link_dof[l];
             if (d >= 0) {
-                const float q = 0.5f * (prop(a, TG_PROP_LOWER, e, d) + prop(a, TG_PROP_UPPER, e, d));
+                const float lo = prop(a, TG_PROP_LOWER, e, d), hi = prop(a, TG_PROP_UPPER, e, d);
+                const float q = 0.5f * (lo + hi);
+                // a locked joint is rigid at its window centre: a wider window
+                // (props set as if the joint were free) is reported by tg_sync
+                if (a.err && !(hi - lo <= TG_LOCK_WINDOW_MAX)) atomicOr(a.err, 1);
                 const float *ax = M::link_axis[l];
                 if (M::link_jtype[l] == TG_JOINT_REVOLUTE) Rl = mul(Rl, rot_axis(ax[0], ax[1], ax[2], q));
                 else if (M::link_jtype[l] == TG_JOINT_PRISMATIC) tl = tl + q * mul(Rl, v3(ax[0], ax[1], ax[2]));
@@ -661,12 +667,18 @@ template <class M, bool HF, class P = NoPost>
 int launch_par(const StepArgs &a, hipStream_t stream, const typename P::Args &pa = {}) {
     constexpr size_t bytes = ParLayout<M>::template bytes<M::EPB>();
     static_assert(bytes <= 160 * 1024, "LDS budget");
-    static bool attr = false;
-    if (!attr) {
+    // the dynamic-LDS attribute is per device: one bit per device of this
+    // instantiation, set the first time the kernel launches there (sims on
+    // several devices in one process, from any thread)
+    static std::atomic<uint64_t> attr_set{0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return TG_ERR_HIP;
+    const uint64_t bit = 1ull << dev;
+    if (!(attr_set.load(std::memory_order_acquire) & bit)) {
         if (hipFuncSetAttribute((const void *)step_par_kernel<M, M::EPB, HF, P>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess)
             return TG_ERR_HIP;
-        attr = true;
+        attr_set.fetch_or(bit, std::memory_order_acq_rel);
     }
     hipLaunchKernelGGL((step_par_kernel<M, M::EPB, HF, P>), dim3((a.N + M::EPB - 1) / M::EPB), dim3(M::EPB * M::LPE),
                        bytes, stream, a, pa);

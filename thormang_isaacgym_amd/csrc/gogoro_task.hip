@@ -416,4 +416,31 @@ int launch_mark_dirty(uint8_t *dirty, const int32_t *ids, int n, hipStream_t str
     return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
 }
 
+// ---------------------------------------------------------------- RNG test hook (tg_rng_fill)
+// Block i = philox({i, counter lo, counter hi, 0}, seed): kind 0 the 4 raw
+// words (bit patterns in the float slots), kind 1 u01 of each word, kind 2
+// gauss(x, y), gauss(z, w) -- the very functions the task kernels draw with.
+__global__ void rng_fill_kernel(int kind, uint32_t k0, uint32_t k1, uint32_t c_lo, uint32_t c_hi, float *out, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const U4 x = philox(U4{(uint32_t)i, c_lo, c_hi, 0u}, k0, k1);
+    if (kind == 0) {
+        uint32_t *o = reinterpret_cast<uint32_t *>(out) + 4 * (size_t)i;
+        o[0] = x.x; o[1] = x.y; o[2] = x.z; o[3] = x.w;
+    } else if (kind == 1) {
+        float *o = out + 4 * (size_t)i;
+        o[0] = u01(x.x); o[1] = u01(x.y); o[2] = u01(x.z); o[3] = u01(x.w);
+    } else {
+        float *o = out + 2 * (size_t)i;
+        o[0] = gauss(x.x, x.y); o[1] = gauss(x.z, x.w);
+    }
+}
+
+int launch_rng_fill(int kind, uint64_t seed, uint64_t counter, float *out, int n, hipStream_t stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(rng_fill_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, kind, (uint32_t)seed,
+                       (uint32_t)(seed >> 32), (uint32_t)counter, (uint32_t)(counter >> 32), out, n);
+    return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
+}
+
 }  // namespace tg

@@ -41,6 +41,7 @@ struct StepArgs {
     const float *mass_scale;  // [N,L] or null
     float *comp;              // [KC,N]
     uint8_t *dirty;           // [N]
+    int *err;                 // [1] sticky state-error flag (compose: a locked dof's window widened), read by tg_sync
     const float *hf;          // terrain heights [rows, cols] or null (z = 0 plane)
     int hf_rows, hf_cols;
     float hf_hs, hf_vs, hf_ox, hf_oy, hf_mu;
@@ -100,16 +101,25 @@ int launch_scatter_rows(float *dst, const float *src, const int32_t *ids, int n,
 // dst[f][ids[i]][k] (field f of a [F,N,row] array) = src[ids[i]*row + k]
 int launch_scatter_field(float *dst, const float *src, const int32_t *ids, int n, int row, hipStream_t stream);
 int launch_mark_dirty(uint8_t *dirty, const int32_t *ids, int n, hipStream_t stream);
+// tg_rng_fill test hook (gogoro_task.hip): n Philox blocks, counter (i, c_lo, c_hi, 0)
+int launch_rng_fill(int kind, uint64_t seed, uint64_t counter, float *out, int n, hipStream_t stream);
 
 // ---------------------------------------------------------------- Philox4x32-10
 struct U4 {
     uint32_t x, y, z, w;
 };
-__device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
+// Random123's philox4x32 with 10 rounds (Salmon et al., SC'11): round
+// (hi0,lo0) = M0 * c0, (hi1,lo1) = M1 * c2, c' = (hi1^c1^k0, lo1, hi0^c3^k1, lo0),
+// then the Weyl key bump.  Host + device: the host copy backs tg_philox4x32_10
+// (the known-answer test against Random123's kat_vectors, tests/test_rng.py).
+__host__ __device__ __forceinline__ uint32_t mulhi32(uint32_t a, uint32_t b) {
+    return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
+}
+__host__ __device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
-        uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
-        uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+        uint32_t hi0 = mulhi32(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+        uint32_t hi1 = mulhi32(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
         c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;

@@ -13,6 +13,7 @@
 #include <string>
 #include <utility>
 #include <cstdlib>
+#include <memory>
 #include <vector>
 
 #include "../../include/tg_gogoro.h"
@@ -53,6 +54,7 @@ struct tg_sim {
     float *props = nullptr, *force = nullptr, *mass_scale = nullptr, *shape_mu = nullptr, *comp = nullptr;
     float *env_origin = nullptr;
     uint8_t *dirty = nullptr;
+    int *err = nullptr;   // sticky state-error flag set by kernels (tg_sync reports it)
     // terrain heightfield (tg_set_heightfield)
     float *hf = nullptr;
     int hf_rows = 0, hf_cols = 0;
@@ -122,6 +124,7 @@ tg::StepArgs step_args(tg_sim *s) {
     a.mass_scale = s->mass_scale;
     a.comp = s->comp;
     a.dirty = s->dirty;
+    a.err = s->err;
     a.hf = s->hf_rows > 0 ? s->hf : nullptr;
     a.hf_rows = s->hf_rows;
     a.hf_cols = s->hf_cols;
@@ -157,7 +160,8 @@ int tg_sim_create(const tg_model_desc *m, const tg_sim_params *params, int32_t n
     HIPCHK(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) return fail(TG_ERR_ARG, "device %d not present (%d visible)", device, ndev);
     HIPCHK(hipSetDevice(device));
-    tg_sim *s = new tg_sim();
+    std::unique_ptr<tg_sim> owner(new tg_sim());   // released to the caller on success only
+    tg_sim *s = owner.get();
     if (const char *u = getenv("TG_WALK_UNFUSED")) s->walk_unfused = u[0] == '1';
     s->device = device;
     s->N = num_envs;
@@ -183,12 +187,8 @@ int tg_sim_create(const tg_model_desc *m, const tg_sim_params *params, int32_t n
     rc |= s->alloc(&s->comp, (size_t)kc * N);
     rc |= s->alloc(&s->env_origin, N * 3);
     rc |= s->alloc(&s->dirty, N);
-    if (rc) {
-        std::string keep = g_err;
-        delete s;
-        g_err = keep;
-        return TG_ERR_HIP;
-    }
+    rc |= s->alloc(&s->err, 1);
+    if (rc) return TG_ERR_HIP;   // g_err holds the failing allocation; owner frees the rest
     // host-side initial values: identity root pose at the env origin grid,
     // unit mass scale, per-shape friction from the model, defaults for props
     std::vector<float> h_root(N * 13, 0.f), h_org(N * 3, 0.f), h_ms(N * s->L, 1.f);
@@ -215,7 +215,7 @@ int tg_sim_create(const tg_model_desc *m, const tg_sim_params *params, int32_t n
     HIPCHK(hipMemcpy(s->dirty, h_dirty.data(), N, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(s->props, h_props.data(), h_props.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipDeviceSynchronize());
-    *out = s;
+    *out = owner.release();
     return TG_OK;
 }
 
@@ -395,9 +395,24 @@ int tg_set_heightfield(tg_sim *s, const float *heights, int32_t rows, int32_t co
 // compose (+ optional prologue in a) and the step kernel of one simulate call;
 // with wp, the step kernel carrying the walk post-physics epilogue (returns 1,
 // nothing launched, when the model has no such instantiation)
+// makes the sim's device current for the launches of one call (per-device
+// kernel attributes, tg_set_stream's stream), restoring the caller's device
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) == hipSuccess && prev != dev) (void)hipSetDevice(dev);
+        else prev = -1;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
 static int simulate_args(tg_sim *s, const tg::StepArgs &a, const tg::WalkPostArgs *wp = nullptr) {
+    DeviceGuard dg(s->device);
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
-    if (s->timing > 0 && s->timing_count++ % s->timing == 0) {
+    const bool timed = s->timing > 0 && s->timing_count % s->timing == 0;
+    if (timed) {
         if (!s->ev_free.empty()) {
             ev = s->ev_free.back();
             s->ev_free.pop_back();
@@ -405,20 +420,19 @@ static int simulate_args(tg_sim *s, const tg::StepArgs &a, const tg::WalkPostArg
             HIPCHK(hipEventCreate(&ev.first));
             HIPCHK(hipEventCreate(&ev.second));
         }
-        s->ev_pending.push_back(ev);
     }
     int rc = wp ? tg::launch_step_walk(s->hash, a, *wp, s->stream, ev.first, ev.second)
                 : tg::launch_step(s->hash, a, s->stream, ev.first, ev.second);
-    if (rc == 1) {   // not launched: hand the event pair back
-        if (ev.first) {
-            s->ev_pending.pop_back();
-            s->ev_free.push_back(ev);
-        }
-        if (s->timing > 0) s->timing_count--;
-        return 1;
+    // the pair joins the pending list only once both events were recorded by a
+    // launch that went through; otherwise it goes back to the free list
+    if (rc != 0) {
+        if (ev.first) s->ev_free.push_back(ev);
+        if (rc == 1) return 1;   // not launched (no such instantiation): caller falls back
+        return fail(rc, "step launch failed: %s", hipGetErrorString(hipGetLastError()));
     }
+    if (s->timing > 0) s->timing_count++;
+    if (ev.first) s->ev_pending.push_back(ev);
     s->forces_pending = false;   // apply_rigid_body_force_tensors acts for one simulate call
-    if (rc) return fail(rc, "step launch failed: %s", hipGetErrorString(hipGetLastError()));
     return TG_OK;
 }
 
@@ -446,15 +460,16 @@ int tg_set_kernel_timing(tg_sim *s, int32_t period) {
 int tg_read_kernel_timing(tg_sim *s, double *total_ms, int64_t *launches) {
     if (int rc = check_sim(s)) return rc;
     if (!total_ms || !launches) return fail(TG_ERR_ARG, "tg_read_kernel_timing: null argument");
-    for (auto &e : s->ev_pending) {
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pend;
+    pend.swap(s->ev_pending);   // every pair leaves the pending list, read or not
+    for (auto &e : pend) s->ev_free.push_back(e);
+    for (auto &e : pend) {
         HIPCHK(hipEventSynchronize(e.second));
         float ms = 0.f;
         HIPCHK(hipEventElapsedTime(&ms, e.first, e.second));
         s->timed_ms += ms;
         s->timed_launches += 1;
-        s->ev_free.push_back(e);
     }
-    s->ev_pending.clear();
     *total_ms = s->timed_ms;
     *launches = s->timed_launches;
     s->timed_ms = 0.0;
@@ -465,6 +480,28 @@ int tg_read_kernel_timing(tg_sim *s, double *total_ms, int64_t *launches) {
 int tg_sync(tg_sim *s) {
     if (int rc = check_sim(s)) return rc;
     HIPCHK(hipStreamSynchronize(s->stream));
+    int err = 0;
+    HIPCHK(hipMemcpy(&err, s->err, sizeof err, hipMemcpyDeviceToHost));
+    if (err) {
+        HIPCHK(hipMemset(s->err, 0, sizeof err));
+        return fail(TG_ERR_STATE,
+                    "a locked dof was given a [lower, upper] window wider than %g: locked joints are merged into "
+                    "their parent's body in this model and stay rigid at the window centre (build the model "
+                    "with that joint free instead)", (double)TG_LOCK_WINDOW_MAX);
+    }
+    return TG_OK;
+}
+
+void tg_philox4x32_10(const uint32_t *ctr, const uint32_t *key, uint32_t *out) {
+    const tg::U4 r = tg::philox(tg::U4{ctr[0], ctr[1], ctr[2], ctr[3]}, key[0], key[1]);
+    out[0] = r.x; out[1] = r.y; out[2] = r.z; out[3] = r.w;
+}
+
+int tg_rng_fill(tg_sim *s, int32_t kind, uint64_t seed, uint64_t counter, float *out, int32_t n) {
+    if (int rc = check_sim(s)) return rc;
+    if (n < 0 || (n > 0 && !out)) return fail(TG_ERR_ARG, "tg_rng_fill: bad output");
+    if (kind < 0 || kind > 2) return fail(TG_ERR_ARG, "tg_rng_fill: unknown kind %d", kind);
+    if (int rc = tg::launch_rng_fill(kind, seed, counter, out, n, s->stream)) return fail(rc, "rng launch failed");
     return TG_OK;
 }
 

@@ -10,6 +10,8 @@ provides the same pieces over this package's tasks:
 * ``RLGPUEnv`` -- the vec-env rl_games drives: ``step`` / ``reset`` /
   ``reset_done`` / ``get_number_of_agents`` / ``get_env_info`` (+ the
   set_train_info / env-state hooks), tensors stay on the env's GPU;
+* ``EpisodeStats`` -- per-env episode return / length accumulation on the
+  device and the per-iteration all-rank gather of their sums;
 * ``register`` -- registers both with rl_games' ``vecenv`` /
   ``env_configurations`` when rl_games is importable (it is not in this image);
 * ``PolicyExport`` / ``export_policy`` -- export.py:130-170: the trained model
@@ -35,17 +37,62 @@ def get_rlgames_env_creator(seed: int, task_config: dict, task_name: str, sim_de
     """train.py:99-122: a thunk creating the task env (torchrun rank -> device)."""
     def create_env(**kwargs):
         from . import make
-        dev_sim, dev_rl = sim_device, rl_device
+        dev_sim, dev_rl, env_seed = sim_device, rl_device, seed
         if multi_gpu:
-            rank = int(os.getenv("LOCAL_RANK", "0"))
-            dev_sim = dev_rl = f"cuda:{rank}"
-        env = make(seed=seed, task=task_name, num_envs=task_config["env"]["numEnvs"], sim_device=dev_sim,
+            # one process per GPU (torchrun): rank -> device, and a distinct
+            # stream per rank -- train.py:81 adds the global rank to the seed,
+            # and the seed keys the in-kernel Philox streams
+            local = int(os.getenv("LOCAL_RANK", "0"))
+            dev_sim = dev_rl = f"cuda:{local}"
+            env_seed = seed + int(os.getenv("RANK", "0"))
+        env = make(seed=env_seed, task=task_name, num_envs=task_config["env"]["numEnvs"], sim_device=dev_sim,
                    rl_device=dev_rl, graphics_device_id=graphics_device_id, headless=headless,
                    virtual_screen_capture=virtual_screen_capture, force_render=force_render, cfg=task_config)
         if post_create_hook is not None:
             post_create_hook()
         return env
     return create_env
+
+
+class EpisodeStats:
+    """Per-iteration host gather of episode returns and lengths (north_star: the
+    env batch shards across GPUs with no collective on the hot path, "only a
+    per-iteration host gather of returns").
+
+    ``update(rew, reset)`` runs after every ``env.step`` on the env's device
+    with no host synchronisation: it accumulates each env's running return and
+    length and folds finished episodes (``reset != 0``) into three device sums.
+    ``gather()`` -- once per PPO iteration -- sums those over all ranks (one
+    all-reduce of 3 float64 scalars when torch.distributed is initialised;
+    gloo reduces on the host, RCCL on the device), resets the sums and returns
+    the job-wide ``{"episodes", "mean_return", "mean_length"}`` on every rank."""
+
+    def __init__(self, num_envs: int, device):
+        self.device = torch.device(device)
+        self.ret = torch.zeros(num_envs, dtype=torch.float64, device=self.device)
+        self.len = torch.zeros(num_envs, dtype=torch.float64, device=self.device)
+        self.sums = torch.zeros(3, dtype=torch.float64, device=self.device)   # return, length, episodes
+
+    def update(self, rew: torch.Tensor, reset: torch.Tensor) -> None:
+        self.ret += rew.to(torch.float64)
+        self.len += 1.0
+        done = reset != 0
+        d = done.to(torch.float64)
+        self.sums += torch.stack([(self.ret * d).sum(), (self.len * d).sum(), d.sum()])
+        self.ret.masked_fill_(done, 0.0)
+        self.len.masked_fill_(done, 0.0)
+
+    def gather(self) -> dict:
+        import torch.distributed as dist
+        t = self.sums.clone()
+        if dist.is_available() and dist.is_initialized():
+            if dist.get_backend() == "gloo":
+                t = t.cpu()
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        ret, length, n = (float(x) for x in t.cpu())
+        self.sums.zero_()
+        return {"episodes": int(round(n)), "mean_return": ret / n if n > 0 else float("nan"),
+                "mean_length": length / n if n > 0 else float("nan")}
 
 
 class RLGPUEnv:

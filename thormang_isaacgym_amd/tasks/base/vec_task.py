@@ -126,6 +126,17 @@ class Env(abc.ABC):
         return self.num_observations
 
 
+def mass_scale(sample: torch.Tensor, operation: str, base_mass: torch.Tensor) -> torch.Tensor:
+    """Per-link mass scale the library applies for one DR mass sample
+    ([N, L]): IsaacGym's 'scaling' sets m = m0 * s, 'additive' sets
+    m = m0 + s, i.e. a scale of (m0 + s) / m0 (massless links keep scale 1)."""
+    if operation == "scaling":
+        return sample
+    m0 = base_mass.to(sample.device, sample.dtype)
+    safe = torch.where(m0 > 0, m0, torch.ones_like(m0))
+    return torch.where(m0 > 0, (m0 + sample) / safe, torch.ones_like(sample))
+
+
 class VecTask(Env):
     metadata = {"render.modes": ["human", "rgb_array"], "video.frames_per_second": 24}
 
@@ -259,8 +270,9 @@ class VecTask(Env):
             return 0.0 if step < steps else 1.0
         return 1.0
 
-    def _sample(self, params, shape, step, gen=None):
+    def _sample(self, params, shape, step, gen=None, device=None):
         """generate_random_samples semantics: uniform / loguniform / gaussian, with schedule."""
+        device = self.device if device is None else device
         dist = params["distribution"]
         lo, hi = params["range"]
         op = params.get("operation", "additive")
@@ -272,13 +284,13 @@ class VecTask(Env):
             elif op == "scaling":
                 var = var * s
                 mu = mu * s + 1.0 * (1.0 - s)
-            x = torch.randn(shape, device=self.device, generator=gen) * var + mu
+            x = torch.randn(shape, device=device, generator=gen) * var + mu
         elif dist in ("uniform", "loguniform"):
             if op == "additive":
                 lo, hi = lo * s, hi * s
             elif op == "scaling":
                 lo, hi = lo * s + 1.0 * (1.0 - s), hi * s + 1.0 * (1.0 - s)
-            u = torch.rand(shape, device=self.device, generator=gen)
+            u = torch.rand(shape, device=device, generator=gen)
             if dist == "loguniform":
                 x = torch.exp(math.log(lo) + u * (math.log(hi) - math.log(lo)))
             else:
@@ -286,6 +298,10 @@ class VecTask(Env):
         else:
             raise ValueError(f"unknown distribution {dist}")
         return x
+
+    def _base_link_mass(self) -> torch.Tensor:
+        """[L] URDF link masses of the sim's model (the DR reference masses)."""
+        return torch.as_tensor(self.sim.desc.arrays["link_inertia"][:, 0], device=self.device)
 
     def apply_randomizations(self, dr_params):
         rand_freq = dr_params.get("frequency", 1)
@@ -356,8 +372,10 @@ class VecTask(Env):
             for attr, p in dr_params["sim_params"].items():
                 if attr != "gravity":
                     continue
+                # three numbers drawn on the host (as dr_utils does with numpy):
+                # no device round trip on this periodic path
                 base = torch.tensor(self.sim_params["gravity"], dtype=torch.float32)
-                smp = self._sample(p, (3,), self.last_step).cpu()
+                smp = self._sample(p, (3,), self.last_step, device="cpu")
                 g = base * smp if p.get("operation", "additive") == "scaling" else base + smp
                 self.sim.set_gravity(g.tolist())
         n = int(env_ids.numel())
@@ -368,7 +386,7 @@ class VecTask(Env):
                     p = rb["mass"]
                     if (p.get("setup_only", False) and not self.sim_initialized) or not p.get("setup_only", False):
                         smp = self._sample(p, (self.num_envs, self.sim.L), self.last_step)
-                        scale = smp if p.get("operation", "additive") == "scaling" else 1.0 + smp
+                        scale = mass_scale(smp, p.get("operation", "additive"), self._base_link_mass())
                         self.sim.set_body_mass_scale_indexed(scale.contiguous(), env_ids)
                 rs = props.get("rigid_shape_properties", {})
                 if "friction" in rs and self.sim.S > 0:

@@ -34,7 +34,7 @@ from .. import abi
 from .._lib import check, lib
 from ..sim import load_model
 from .base.vec_task import VecTask
-from .gogoro_cfg import ASSET_OPTIONS, gogoro_params, initial_dof_props, thormang_pose
+from .gogoro_cfg import ASSET_OPTIONS, check_lock_set, gogoro_params, initial_dof_props, thormang_pose
 from .gogoro_draws import post_draws, reset_draws
 from .terrain import Terrain
 
@@ -131,6 +131,7 @@ class Gogoro(VecTask):
 
     def create_sim(self):
         model = load_model("gogoro")
+        check_lock_set(self.cfg, model)
         asset_options = dict(ASSET_OPTIONS, fix_base_link=DEBUGFIXBASE)
         self.sim = self.create_sim_object(model, asset_options, env_spacing=self.env_spacing)
         self.terrain = None

@@ -96,6 +96,26 @@ def env_origins(num_envs: int, spacing: float) -> np.ndarray:
     return np.stack([2 * spacing * (e % per_row), 2 * spacing * (e // per_row), np.zeros(num_envs)], 1).astype(np.float32)
 
 
+SEAT_DOFS = ("base_x", "base_y", "base_z")
+
+
+def check_lock_set(cfg: dict, model) -> None:
+    """The compiled model merges every locked joint into its parent's group, so
+    the set of locked DOFs is part of the kernel specialisation.  The reference
+    locks exactly the ``joints_pos`` joints plus the seat joints
+    (gogoro_new.py:257-262,562-572); a cfg whose ``joints_pos`` names a
+    different set would otherwise leave a removed joint rigid (or an added one
+    free) without notice.  Raises ValueError naming the difference."""
+    want = set(cfg["joints_pos"]) | set(SEAT_DOFS)
+    have = set(model.locked)
+    if want != have:
+        raise ValueError(
+            f"cfg joints_pos locks a different joint set than model '{model.name}' was built with: "
+            f"missing from the model {sorted(want - have)}, locked in the model but not in the cfg "
+            f"{sorted(have - want)}; rebuild the model with this lock set "
+            "(thormang_isaacgym_amd.sim.load_asset(urdf, locked=...))")
+
+
 def lock_window(cfg: dict, dof_name_to_id: dict, lower: np.ndarray, upper: np.ndarray) -> None:
     """Apply the joints_pos lock windows [v, v+1e-4] to [.., D] limit arrays in place (:257-261)."""
     for name, val in cfg["joints_pos"].items():

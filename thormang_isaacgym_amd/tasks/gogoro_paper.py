@@ -40,7 +40,7 @@ from ..abi import (TG_PROP_ARMATURE, TG_PROP_DAMPING, TG_PROP_DRIVE_MODE, TG_PRO
                    TG_PROP_STIFFNESS, TG_PROP_UPPER, TG_PROP_VELOCITY, default_dof_props)
 from ..sim import load_model
 from .base.vec_task import VecTask
-from .gogoro_cfg import lock_window
+from .gogoro_cfg import check_lock_set, lock_window
 from .paper_draws import ctor_draws, post_draws, reset_draws
 
 # module switches of the reference (paper.py:23-34), committed values
@@ -244,6 +244,7 @@ class Gogoro(VecTask):
     # ------------------------------------------------------------ creation
     def create_sim(self):
         self.model = model = load_model("gogoro_v12")
+        check_lock_set(self.cfg, model)
         asset_options = dict(ASSET_OPTIONS, fix_base_link=bool(self.switches["DEBUGFIXBASE"]))
         self.sim = self.create_sim_object(model, asset_options, env_spacing=self.env_spacing)
         self._create_envs(model)
