@@ -34,7 +34,19 @@
 #define MAXD 64
 #define MAXC 32
 
+#ifdef ORACLE_REAL_F32
+/* fp32 build (oracle/_build/liboracle_f32.so, drift study scripts/parity_drift.py):
+ * every quantity stored and evaluated in float (with -fsingle-precision-constant
+ * and the float math functions), the same operation order */
+#define sqrt sqrtf
+#define sin sinf
+#define cos cosf
+#define fabs fabsf
+#define exp expf
+typedef float real;
+#else
 typedef double real;
+#endif
 typedef real V3[3];
 typedef real M3[9];
 typedef real V6[6];

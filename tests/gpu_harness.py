@@ -33,12 +33,18 @@ class NumpyDraws:
         return self.rs.standard_normal(n, dtype=np.float32)
 
 
-def parity_cfg(num_envs, max_steps=1000, freq=300):
+def parity_cfg(num_envs, max_steps=1000, freq=300, dr=False):
+    """The Gogoro cfg of the parity runs.  dr=False turns the reference's
+    randomisation off (both sides share one model); dr=True keeps it
+    (gravity x U[0.95,1.05] every 600 frames, link masses x U[0.95,1.05],
+    cfg/task/Gogoro.yaml randomization_params) and the oracle is handed the
+    GPU env's draws (sync_dr)."""
     cfg = load_task_cfg("Gogoro", num_envs=num_envs)
     cfg["env"]["max_steps"] = max_steps
     cfg["noises"]["speed_freq_update"] = freq
     cfg["noises"]["yaw_freq_update"] = freq
-    cfg["task"]["randomization_params"] = {"frequency": 10 ** 9}   # DR off: both sides share one model
+    if not dr:
+        cfg["task"]["randomization_params"] = {"frequency": 10 ** 9}
     return cfg
 
 
@@ -50,7 +56,9 @@ def load_gogoro_model():
 
 
 class OracleGogoro:
-    def __init__(self, cfg, draws, env_spacing=1.0, threads=8, spawn_z=None):
+    def __init__(self, cfg, draws, env_spacing=1.0, threads=8, spawn_z=None, precision="f64", fix_base=False):
+        self.L = L = lib(precision)
+        self.dr = {}   # per-env mass scale / friction / gravity injected from a GPU env (sync_dr)
         self.cfg = cfg
         self.src = draws
         self.threads = threads
@@ -59,7 +67,7 @@ class OracleGogoro:
         self.D = D = m.num_dof
         self.dni = m.dof_name_to_id()
         self.desc = abi.ModelDesc(m)
-        self.sp = abi.sim_params_from_cfg(cfg["sim"], ASSET_OPTIONS, n, env_spacing)
+        self.sp = abi.sim_params_from_cfg(cfg["sim"], dict(ASSET_OPTIONS, fix_base_link=fix_base), n, env_spacing)
         self.p = gogoro_params(cfg, self.dni, n)
         z = lambda *s, dt=np.float32: np.zeros(s, dt)
         self.a = dict(obs_buf=z(n, 6), rew_buf=z(n), reset_buf=np.ones(n, np.int64), progress_buf=z(n, dt=np.int64),
@@ -82,23 +90,22 @@ class OracleGogoro:
         lo, hi = cfg["noises"]["speed_range"]
         a["curent_speed"][:] = np.float32(lo) + draws.uniform(n) * np.float32(hi - lo)
         rd = reset_draws(draws, np.arange(n), n)
-        lib().oracle_gogoro_reset_env.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
         for e in range(n):
-            lib().oracle_gogoro_reset_env(C.byref(self.p), C.byref(self.b), e, ptr(np.ascontiguousarray(rd[e])))
+            L.oracle_gogoro_reset_env(C.byref(self.p), C.byref(self.b), e, ptr(np.ascontiguousarray(rd[e])))
         a["obs_buf"][:] = 0
         a["buffer_obs"][:] = 0
 
     def step(self, actions):
         a, n = self.a, self.n
         pre = self.src.normal(n)
-        lib().oracle_gogoro_pre_physics(C.byref(self.p), C.byref(self.b), ptr(np.ascontiguousarray(actions, np.float32)),
-                                        ptr(pre))
+        self.L.oracle_gogoro_pre_physics(C.byref(self.p), C.byref(self.b),
+                                         ptr(np.ascontiguousarray(actions, np.float32)), ptr(pre))
         physics_step(self.desc, self.sp, a["root"], a["dof_state"], a["dof_props"], a["pos_target"], a["vel_target"],
-                     threads=self.threads)
+                     threads=self.threads, L=self.L, **self.dr)
         ids = np.nonzero(a["reset_buf"])[0]
         rd, od, sd, yd = post_draws(self.src, ids, a["progress_buf"].copy(), self.p.speed_freq_update,
                                     self.p.yaw_freq_update)
-        lib().oracle_gogoro_post_physics(C.byref(self.p), C.byref(self.b), ptr(rd), ptr(od), ptr(sd), ptr(yd))
+        self.L.oracle_gogoro_post_physics(C.byref(self.p), C.byref(self.b), ptr(rd), ptr(od), ptr(sd), ptr(yd))
         return a["obs_buf"], a["rew_buf"], a["reset_buf"], a["timeout_buf"]
 
 
@@ -119,14 +126,23 @@ def balance_policy(obs):
     return np.clip(4.0 * roll + 0.8 * droll, -1.0, 1.0)[:, None].astype(np.float32)
 
 
-def gogoro_env_vs_oracle(num_envs=64, steps=20, seed=0, policy=None, max_steps=1000):
+def gogoro_env_vs_oracle(num_envs=64, steps=20, seed=0, policy=None, max_steps=1000, dr=False, fix_base=False):
+    """Free-running GPU Gogoro env vs the oracle env on the same draws."""
     import torch
-    cfg = parity_cfg(num_envs, max_steps=max_steps)
-    env = make_gpu_gogoro(cfg, NumpyDraws(seed))
-    orc = OracleGogoro(parity_cfg(num_envs, max_steps=max_steps), NumpyDraws(seed))
-    err = {"obs": 0.0, "rew": 0.0, "reset_equal": True, "timeout_equal": True, "root": 0.0, "steps": steps}
+    from thormang_isaacgym_amd.tasks import gogoro as gmod
+    cfg = parity_cfg(num_envs, max_steps=max_steps, dr=dr)
+    saved, gmod.DEBUGFIXBASE = gmod.DEBUGFIXBASE, fix_base
+    try:
+        env = make_gpu_gogoro(cfg, NumpyDraws(seed))
+    finally:
+        gmod.DEBUGFIXBASE = saved
+    orc = OracleGogoro(parity_cfg(num_envs, max_steps=max_steps, dr=dr), NumpyDraws(seed), fix_base=fix_base)
+    err = {"obs": 0.0, "rew": 0.0, "reset_equal": True, "timeout_equal": True, "root": 0.0, "steps": steps,
+           "resets": 0}
     obs_np = orc.a["obs_buf"].copy()
     for t in range(steps):
+        if dr:
+            sync_dr(orc, env)
         act = policy(obs_np) if policy is not None else np.zeros((num_envs, 1), np.float32)
         obs_d, rew, reset, extras = env.step(torch.from_numpy(act).to("cuda:0"))
         o_obs, o_rew, o_reset, o_to = orc.step(act[:, 0])
@@ -136,8 +152,14 @@ def gogoro_env_vs_oracle(num_envs=64, steps=20, seed=0, policy=None, max_steps=1
         err["root"] = max(err["root"], float(np.abs(env.root_tensor.cpu().numpy() - orc.a["root"]).max()))
         err["reset_equal"] &= bool(np.array_equal(reset.cpu().numpy(), o_reset))
         err["timeout_equal"] &= bool(np.array_equal(extras["time_outs"].cpu().numpy().astype(np.uint8), o_to))
+        err["resets"] += int(o_reset.sum())
+        if err["obs"] >= 1e-3 and "first_bad_step" not in err:
+            err["first_bad_step"] = t
         obs_np = o_obs.copy()
     err["resets_seen"] = int(orc.a["progress_buf"].min())
+    if dr:
+        err["mass_scale_range"] = [float(env.sim.body_mass_scale.min()), float(env.sim.body_mass_scale.max())]
+        err["gravity"] = list(env.sim.gravity)
     return err
 
 
@@ -152,6 +174,17 @@ def sync_oracle_from_gpu(orc, env):
         dst[...] = src.reshape(dst.shape).astype(dst.dtype, copy=False)
 
 
+def sync_dr(orc, env):
+    """Domain randomisation: hand the GPU env's current per-env link mass
+    scales, shape frictions and gravity (the values its DR sampling drew, from
+    the Sim mirrors) to the oracle env, which then simulates the same
+    randomised models."""
+    sim = env.sim
+    orc.dr = {"mass_scale": np.ascontiguousarray(sim.body_mass_scale.cpu().numpy(), np.float32),
+              "mu": np.ascontiguousarray(sim.shape_friction.cpu().numpy(), np.float32),
+              "gravity": np.asarray(sim.gravity, np.float32)}
+
+
 def forced_step_errors(env, orc, act_fn, steps, act_to_orc=lambda a: a):
     """1-step GPU-vs-oracle errors along a GPU trajectory (oracle re-synced from
     the GPU state before every step).  Returns max errors and exact-match flags."""
@@ -161,6 +194,7 @@ def forced_step_errors(env, orc, act_fn, steps, act_to_orc=lambda a: a):
     obs = orc.a["obs_buf"].copy()
     for t in range(steps):
         sync_oracle_from_gpu(orc, env)
+        sync_dr(orc, env)
         act = act_fn(obs)
         obs_d, rew, reset, extras = env.step(torch.from_numpy(act).to("cuda:0"))
         o_obs, o_rew, o_reset, o_to = orc.step(act_to_orc(act))
@@ -175,11 +209,15 @@ def forced_step_errors(env, orc, act_fn, steps, act_to_orc=lambda a: a):
     return err
 
 
-def gogoro_forced(num_envs=64, steps=1000, seed=0, max_steps=300):
-    cfg = parity_cfg(num_envs, max_steps=max_steps)
+def gogoro_forced(num_envs=64, steps=1000, seed=0, max_steps=300, dr=False):
+    cfg = parity_cfg(num_envs, max_steps=max_steps, dr=dr)
     env = make_gpu_gogoro(cfg, NumpyDraws(seed))
-    orc = OracleGogoro(parity_cfg(num_envs, max_steps=max_steps), NumpyDraws(seed))
-    return forced_step_errors(env, orc, balance_policy, steps, act_to_orc=lambda a: a[:, 0])
+    orc = OracleGogoro(parity_cfg(num_envs, max_steps=max_steps, dr=dr), NumpyDraws(seed))
+    err = forced_step_errors(env, orc, balance_policy, steps, act_to_orc=lambda a: a[:, 0])
+    if dr:
+        err["gravity"] = list(env.sim.gravity)
+        err["mass_scale_range"] = [float(env.sim.body_mass_scale.min()), float(env.sim.body_mass_scale.max())]
+    return err
 
 
 def gogoro_terrain(num_envs=64, steps=300, seed=0, max_steps=300, terrain_seed=5, forced=True):
@@ -238,9 +276,9 @@ def gogoro_terrain(num_envs=64, steps=300, seed=0, max_steps=300, terrain_seed=5
         set_heightfield(None)
 
 
-def walk_forced(num_envs=32, steps=1000, seed=0, task="ThormangWalk"):
-    env = make_gpu_walk(walk_cfg(num_envs, task), NumpyDraws(seed))
-    orc = OracleWalk(walk_cfg(num_envs, task), NumpyDraws(seed))
+def walk_forced(num_envs=32, steps=1000, seed=0, task="ThormangWalk", dr=False):
+    env = make_gpu_walk(walk_cfg(num_envs, task, dr=dr), NumpyDraws(seed))
+    orc = OracleWalk(walk_cfg(num_envs, task, dr=dr), NumpyDraws(seed))
     rs = np.random.default_rng(seed + 100)
     return forced_step_errors(env, orc, lambda o: rs.uniform(-0.5, 0.5, (num_envs, orc.D)).astype(np.float32), steps)
 
@@ -250,8 +288,10 @@ class OracleWalk:
     """CPU restatement of the ThormangWalk env step (oracle/walk_task.c around
     oracle/physics_ref.c), driven like thormang_isaacgym_amd.tasks.thormang_walk."""
 
-    def __init__(self, cfg, draws, threads=8):
+    def __init__(self, cfg, draws, threads=8, precision="f64"):
         import math
+        self.L = L = lib(precision)
+        self.dr = {}
         from thormang_isaacgym_amd.sim import load_model
         from thormang_isaacgym_amd.tasks.thormang_walk import walk_asset_options, walk_dof_props, walk_params
         self.cfg, self.src, self.threads = cfg, draws, threads
@@ -286,7 +326,7 @@ class OracleWalk:
             self.b.body_force = None
         for e in range(n):
             r = np.ascontiguousarray(draws.uniform(4 + 2 * D))
-            lib().oracle_walk_reset_env(C.byref(self.p), C.byref(self.b), e, ptr(r))
+            L.oracle_walk_reset_env(C.byref(self.p), C.byref(self.b), e, ptr(r))
         # the GPU reset_idx kernel also observes (prog 0): mirror it through a no-reset post pass
         self._observe_only()
 
@@ -296,28 +336,36 @@ class OracleWalk:
         a["progress_buf"][:] = -1
         a["reset_buf"][:] = 0
         zeros = np.zeros((self.n, 3), np.float32)
-        lib().oracle_walk_post_physics(C.byref(self.p), C.byref(self.b), None, ptr(zeros))
+        self.L.oracle_walk_post_physics(C.byref(self.p), C.byref(self.b), None, ptr(zeros))
         a["progress_buf"][:] = saved
 
     def step(self, actions):
         a, n, D = self.a, self.n, self.D
-        lib().oracle_walk_pre_physics(C.byref(self.p), C.byref(self.b), ptr(np.ascontiguousarray(actions, np.float32)))
+        self.L.oracle_walk_pre_physics(C.byref(self.p), C.byref(self.b),
+                                       ptr(np.ascontiguousarray(actions, np.float32)))
         force = a["body_force"] if self.push else None
         physics_step(self.desc, self.sp, a["root"], a["dof_state"], self.props, a["pos_target"],
-                     np.zeros((n, D), np.float32), force=force, threads=self.threads)
+                     np.zeros((n, D), np.float32), force=force, threads=self.threads, L=self.L, **self.dr)
         ids = np.nonzero(a["reset_buf"])[0]
         self.reset_count = getattr(self, "reset_count", 0) + len(ids)
         rd = np.zeros((n, 4 + 2 * D), np.float32)
         for i in ids:
             rd[i] = self.src.uniform(4 + 2 * D)
         pd = self.src.uniform(3 * n).reshape(n, 3)
-        lib().oracle_walk_post_physics(C.byref(self.p), C.byref(self.b), ptr(rd), ptr(np.ascontiguousarray(pd)))
+        self.L.oracle_walk_post_physics(C.byref(self.p), C.byref(self.b), ptr(rd), ptr(np.ascontiguousarray(pd)))
         return a["obs_buf"], a["rew_buf"], a["reset_buf"], a["timeout_buf"]
 
 
-def walk_cfg(num_envs, task="ThormangWalk"):
+def walk_cfg(num_envs, task="ThormangWalk", dr=False, fix_base=False, spawn_height=None):
+    """Walk cfg of the parity runs: the task's own DR (mass, friction) off
+    unless dr=True (then the oracle is handed the GPU env's draws, sync_dr);
+    pushes follow the task cfg."""
     cfg = load_task_cfg(task, num_envs=num_envs)
-    cfg["task"]["randomize"] = False
+    cfg["task"]["randomize"] = bool(dr)
+    if fix_base:
+        cfg["env"]["asset"] = dict(cfg["env"].get("asset", {}), fix_base_link=True)
+    if spawn_height is not None:
+        cfg["env"]["spawnHeight"] = float(spawn_height)
     return cfg
 
 
@@ -334,15 +382,21 @@ def n_resets(orc):
     return getattr(orc, "reset_count", 0)
 
 
-def walk_env_vs_oracle(num_envs=32, steps=30, seed=0, task="ThormangWalk"):
+def walk_env_vs_oracle(num_envs=32, steps=30, seed=0, task="ThormangWalk", dr=False, fix_base=False,
+                       spawn_height=None, amp=0.3):
+    """Free-running GPU walk env vs the oracle env on the same draws and
+    actions U(-amp, amp) (amp 0: the PD-held default pose)."""
     import torch
-    env = make_gpu_walk(walk_cfg(num_envs, task), NumpyDraws(seed))
-    orc = OracleWalk(walk_cfg(num_envs, task), NumpyDraws(seed))
+    mk = lambda: walk_cfg(num_envs, task, dr=dr, fix_base=fix_base, spawn_height=spawn_height)
+    env = make_gpu_walk(mk(), NumpyDraws(seed))
+    orc = OracleWalk(mk(), NumpyDraws(seed))
     rs = np.random.default_rng(seed + 100)
     err = {"obs": 0.0, "rew": 0.0, "reset_equal": True, "timeout_equal": True, "root": 0.0, "steps": steps}
     err["obs0"] = float(np.abs(env.obs_buf.cpu().numpy() - orc.a["obs_buf"]).max())
     for t in range(steps):
-        act = rs.uniform(-0.3, 0.3, (num_envs, orc.D)).astype(np.float32)
+        if dr:
+            sync_dr(orc, env)
+        act = rs.uniform(-amp, amp, (num_envs, orc.D)).astype(np.float32)
         obs_d, rew, reset, extras = env.step(torch.from_numpy(act).to("cuda:0"))
         o_obs, o_rew, o_reset, o_to = orc.step(act)
         err["obs"] = max(err["obs"], float(np.abs(obs_d["obs"].cpu().numpy() - o_obs).max()))

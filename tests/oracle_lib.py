@@ -13,18 +13,21 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(REPO, "oracle", "_build", "liboracle.so")
+LIB_F32 = os.path.join(REPO, "oracle", "_build", "liboracle_f32.so")   # physics in fp32 (drift study)
 
-_lib = None
+_libs = {}
 
 
-def lib():
-    global _lib
-    if _lib is None:
+def lib(precision: str = "f64"):
+    """The oracle library: ``f64`` (the parity oracle) or ``f32`` (the same
+    physics restatement evaluated in float, scripts/parity_drift.py)."""
+    if precision not in _libs:
+        path = {"f64": LIB, "f32": LIB_F32}[precision]
         srcs = [os.path.join(REPO, "oracle", f) for f in ("gogoro_task.c", "gogoro_paper_task.c", "physics_ref.c",
                                                               "walk_task.c")]
-        if not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in srcs):
+        if not os.path.exists(path) or any(os.path.getmtime(s) > os.path.getmtime(path) for s in srcs):
             subprocess.run(["make", "-C", os.path.join(REPO, "oracle")], check=True, capture_output=True)
-        _lib = C.CDLL(LIB)
+        _lib = C.CDLL(path)
         vp = C.c_void_p
         _lib.oracle_gogoro_observations.argtypes = [C.c_int, vp, vp, vp, vp]
         _lib.oracle_gogoro_reward.argtypes = [C.c_int, vp, vp, vp, C.c_int64, vp, vp]
@@ -41,7 +44,9 @@ def lib():
         _lib.oracle_physics_step.argtypes = [vp, vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_int]
         _lib.oracle_set_heightfield.argtypes = [vp, C.c_int, C.c_int] + [C.c_float] * 5
         _lib.oracle_rigid_body_states.argtypes = [vp, C.c_int, vp, vp, vp]
-    return _lib
+        _lib.oracle_gogoro_reset_env.argtypes = [vp, vp, C.c_int, vp]
+        _libs[precision] = _lib
+    return _libs[precision]
 
 
 def ptr(a):
@@ -52,7 +57,7 @@ def ptr(a):
 
 
 def physics_step(desc, sp, root, dof, props, pos_tgt, vel_tgt, act=None, force=None, mass_scale=None, mu=None,
-                 gravity=None, threads=1):
+                 gravity=None, threads=1, L=None):
     """One control step of the fp64 oracle engine, in place on root/dof."""
     n = root.shape[0]
     if mu is None:
@@ -60,7 +65,7 @@ def physics_step(desc, sp, root, dof, props, pos_tgt, vel_tgt, act=None, force=N
                                   dtype=np.float32)
     if gravity is None:
         gravity = np.array(list(sp.gravity), np.float32)
-    lib().oracle_physics_step(C.byref(desc.desc), C.byref(sp), n, ptr(root), ptr(dof), ptr(props), ptr(pos_tgt),
+    (L or lib()).oracle_physics_step(C.byref(desc.desc), C.byref(sp), n, ptr(root), ptr(dof), ptr(props), ptr(pos_tgt),
                               ptr(vel_tgt), ptr(act), ptr(force), ptr(mass_scale), ptr(mu), ptr(gravity), threads)
 
 

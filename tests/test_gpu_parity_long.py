@@ -1,0 +1,87 @@
+"""north_star's parity criterion -- obs / reward / done within 1e-3 over 1000
+steps -- FREE-RUNNING (no re-sync of the oracle from the GPU state), on the
+configurations whose dynamics do not amplify 1e-7-size rounding differences:
+
+* Gogoro with a fixed base (the reference's DEBUGFIXBASE switch,
+  tasks/gogoro_new.py:22,206): steering drive, wheels, free grip joints;
+* ThormangWalk with a fixed base hung clear of the ground, random actions;
+* ThormangWalk standing on the ground under its PD drives (zero actions):
+  free base, both feet in contact for 1000 steps;
+* Gogoro with a free base under the balance controller: falls, resets and
+  re-spawns included, as long as no fall happens within rounding of the tilt
+  threshold (then the reset draw streams of the two sides part, see
+  scripts/parity_drift.py and DESIGN.md §2).
+
+plus the reference's domain randomisation live on the Gogoro path (link
+masses x U[0.95,1.05], gravity x U[0.95,1.05] every 600 frames; the oracle
+simulates the models the GPU env drew, tests/gpu_harness.py sync_dr).
+scripts/parity_drift.py measures, for the chaotic configurations, how far a
+1e-6 perturbation of the fp64 oracle and an fp32 build of the oracle drift
+from it (profiles/r2/drift_*.txt)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _cuda():
+    if not torch.cuda.is_available():
+        pytest.skip("needs the MI355X")
+
+
+def test_gpu_gogoro_fixed_base_free_running_1000_steps():
+    _cuda()
+    from tests.gpu_harness import balance_policy, gogoro_env_vs_oracle
+    err = gogoro_env_vs_oracle(num_envs=64, steps=1000, seed=31, policy=balance_policy, fix_base=True)
+    print(err)
+    assert err["obs"] < 1e-3 and err["rew"] < 1e-3, err
+    assert err["reset_equal"] and err["timeout_equal"], err
+    assert err["resets"] >= 64          # every env times out at step 999 and re-spawns
+
+
+def test_gpu_walk_fixed_base_free_running_1000_steps():
+    _cuda()
+    from tests.gpu_harness import walk_env_vs_oracle
+    err = walk_env_vs_oracle(num_envs=32, steps=1000, seed=32, fix_base=True, spawn_height=1.3, amp=0.3)
+    print(err)
+    assert err["obs"] < 1e-3 and err["rew"] < 1e-3, err
+    assert err["reset_equal"] and err["timeout_equal"], err
+
+
+def test_gpu_walk_standing_free_running_1000_steps():
+    _cuda()
+    from tests.gpu_harness import walk_env_vs_oracle
+    err = walk_env_vs_oracle(num_envs=32, steps=1000, seed=21, amp=0.0)
+    print(err)
+    assert err["resets"] == 0           # nobody falls (episodes last 1205 steps)
+    assert err["obs"] < 1e-3 and err["rew"] < 1e-3, err
+    assert err["reset_equal"] and err["timeout_equal"], err
+
+
+def test_gpu_gogoro_free_base_free_running_1000_steps():
+    _cuda()
+    from tests.gpu_harness import balance_policy, gogoro_env_vs_oracle
+    err = gogoro_env_vs_oracle(num_envs=32, steps=1000, seed=21, policy=balance_policy)
+    print(err)
+    assert err["resets"] > 32           # falls and re-spawns happen along the way
+    assert err["obs"] < 1e-3 and err["rew"] < 1e-3, err
+    assert err["reset_equal"] and err["timeout_equal"], err
+
+
+def test_gpu_gogoro_domain_randomisation_matches_oracle():
+    """The reference's randomization_params live on both sides: 150 free-running
+    steps, then 1000 teacher-forced steps (which cross the 600-frame gravity
+    resample)."""
+    _cuda()
+    from tests.gpu_harness import balance_policy, gogoro_env_vs_oracle, gogoro_forced
+    err = gogoro_env_vs_oracle(num_envs=64, steps=150, seed=41, policy=balance_policy, dr=True)
+    print(err)
+    lo, hi = err["mass_scale_range"]
+    assert 0.95 <= lo < 0.96 and 1.04 < hi <= 1.05, err      # masses really randomised
+    assert err["obs"] < 1e-3 and err["rew"] < 1e-3, err
+    assert err["reset_equal"] and err["timeout_equal"], err
+    err = gogoro_forced(num_envs=64, steps=1000, seed=42, dr=True)
+    print(err)
+    assert err["gravity"] != [0.0, 0.0, -9.81], err            # resampled at frame 600
+    assert err["obs"] < 1e-3 and err["rew"] < 1e-3, err
+    assert err["reset_equal"] and err["timeout_equal"], err

@@ -153,7 +153,7 @@ def test_gpu_gogoro_reset_and_noise_draws_follow_the_reference_distributions():
 
 
 def test_gpu_walk_reset_and_push_draws():
-    """ThormangWalkDR at 4096 envs: the first step resets every env (commands
+    """ThormangWalkDR at 4096 envs: the constructor resets every env (commands
     U[ranges], yaw U(-pi,pi), joint positions default + U(-1,1) x jointNoise,
     joint velocities 0.1 U(-1,1)); pushes of pushForce x U(-1,1) (x, y) and
     0.25 x (z) on the push steps."""
@@ -162,8 +162,7 @@ def test_gpu_walk_reset_and_push_draws():
     from thormang_isaacgym_amd.cfg import load_task_cfg
     cfg = load_task_cfg("ThormangWalkDR", num_envs=N)
     env = tia.make(seed=11, task="ThormangWalkDR", num_envs=N, sim_device="cuda:0", rl_device="cuda:0", cfg=cfg)
-    env.step(torch.zeros(N, env.num_actions, device="cuda:0"))
-    torch.cuda.synchronize()
+    torch.cuda.synchronize()   # the constructor's reset_idx of every env
     e = cfg["env"]
     r = e["randomCommandVelocityRanges"]
     cmd = env.commands.cpu()

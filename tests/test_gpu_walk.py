@@ -59,12 +59,12 @@ def test_gpu_walk_step_matches_oracle_along_1000_steps():
 
 
 def test_gpu_walk_8192_envs_step_matches_oracle():
-    """BASELINE config 4's per-GPU batch (8192 envs): teacher-forced steps of
-    every env against the oracle env (the partition a rank of the 8-GPU run
+    """BASELINE config 4's per-GPU batch (8192 envs): 100 teacher-forced steps
+    of every env against the oracle env (the partition a rank of the 8-GPU run
     owns is this same batch with its own seed)."""
     _cuda()
     from tests.gpu_harness import walk_forced
-    err = walk_forced(num_envs=8192, steps=8, seed=11)
+    err = walk_forced(num_envs=8192, steps=100, seed=11)
     print(err)
     assert err["obs"] < 1e-3 and err["rew"] < 1e-3, err
     assert err["reset_equal"] and err["timeout_equal"], err
@@ -73,11 +73,11 @@ def test_gpu_walk_8192_envs_step_matches_oracle():
 def test_gpu_walk_dr_16384_envs():
     """BASELINE config 5's per-GPU batch: ThormangWalkDR at 16384 envs with
     mass / friction / push randomisation live; the pushes path is checked
-    step-by-step against the oracle env (teacher-forced), then the full DR
-    env runs 150 steps."""
+    step-by-step against the oracle env (100 teacher-forced steps), then the
+    full DR env runs 150 steps."""
     _cuda()
     from tests.gpu_harness import walk_forced
-    err = walk_forced(num_envs=16384, steps=4, seed=12, task="ThormangWalkDR")
+    err = walk_forced(num_envs=16384, steps=100, seed=12, task="ThormangWalkDR")
     print(err)
     assert err["obs"] < 2e-3 and err["rew"] < 2e-3, err
     assert err["reset_equal"], err

@@ -72,6 +72,12 @@ class Sim:
             setattr(v, k, getattr(self, k).data_ptr())
         check(lib().tg_bind_state(self._h, C.byref(v)), "tg_bind_state")
         self.all_ids = torch.arange(N, dtype=torch.int32, device=self.device)
+        # mirrors of the per-env properties the library holds (read back by
+        # get_* style inspection and the parity harness; never on the hot path)
+        self.body_mass_scale = torch.ones(N, self.L, **f32)
+        self.shape_friction = torch.as_tensor(np.asarray(self.desc.arrays["shape_friction"], np.float32),
+                                              device=self.device).repeat(N, 1)
+        self.gravity = [float(x) for x in params.gravity]
 
     @property
     def handle(self):
@@ -111,14 +117,18 @@ class Sim:
         ids = self._ids(ids)
         check(lib().tg_set_body_mass_scale_indexed(self._h, _ptr(self._dev(scale)), _ptr(ids), ids.numel()),
               "mass scale")
+        # host-side mirror of the rigid-body mass properties (get_actor_rigid_body_properties)
+        self.body_mass_scale[ids.long()] = scale[ids.long()]
 
     def set_shape_friction_indexed(self, mu: torch.Tensor, ids: torch.Tensor):
         ids = self._ids(ids)
         check(lib().tg_set_shape_friction_indexed(self._h, _ptr(self._dev(mu)), _ptr(ids), ids.numel()), "friction")
+        self.shape_friction[ids.long()] = mu[ids.long()]   # mirror (get_actor_rigid_shape_properties)
 
     def set_gravity(self, g):
         arr = (C.c_float * 3)(*[float(x) for x in g])
         check(lib().tg_set_gravity(self._h, arr), "set_gravity")
+        self.gravity = [float(x) for x in g]
 
     def apply_body_forces(self, wrench: torch.Tensor):
         check(lib().tg_apply_body_forces(self._h, _ptr(self._dev(wrench))), "apply_rigid_body_force_tensors")
