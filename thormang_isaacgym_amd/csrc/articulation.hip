@@ -25,6 +25,7 @@
 
 #include "../../include/tgsim.h"
 #include "generated/models.inc"
+#include "gogoro_math.h"
 #include "tg_math.h"
 #include "tg_kernels.h"
 
@@ -657,6 +658,168 @@ struct WalkPost {
     }
 };
 
+// ---------------------------------------------------------------- fused Gogoro post-physics
+// tg_gogoro_step's last simulate: gogoro_task.hip post_kernel (progress,
+// masked resets with their property writes and dirty flag, observations,
+// reward, sensor noise, command resampling, timeouts) as the step kernel's
+// epilogue, LPE lanes per env on the final state it holds: the 9 Philox
+// blocks run on the env's lanes at once (lane l block l, the lead lane also
+// block 8) and reach the lead lane by DPP row broadcasts; a reset env's dof
+// rows are written by all its lanes; the lead lane does the task math.  The
+// state is stored once (the reset state for a reset env), and the separate
+// post launch and its re-read of the state disappear.  Same counters, draws
+// and fp32 operations (gogoro_math.h) as post_kernel.
+struct GogoroPost {
+    static constexpr bool on = true;
+    using Args = GogoroPostArgs;
+    template <class M, int LPE>
+    static __device__ __forceinline__ void epilogue(const Args &pa, const StepArgs &a, const LE &s, int e, bool owner,
+                                                    int sub, const float *rt0, float *root, float *dofs) {
+#pragma clang fp contract(off) reassociate(off)
+        constexpr int D = M::ND;
+        constexpr int NR = (D + LPE - 1) / LPE;
+        static_assert(LPE >= 8, "the 9 draw blocks need 8 lanes per env");
+        const tg_gogoro_params &p = pa.p;
+        const tg_gogoro_buffers &b = pa.b;
+        const bool lead = sub == 0;
+        const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
+        // ---- inputs, one batch
+        const int64_t prog1 = b.progress_buf[e] + 1;
+        const bool rflag = b.reset_buf[e] != 0;
+        float rt[13], ah[5];
+#pragma unroll
+        for (int k = 0; k < 13; ++k) rt[k] = rt0[k];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) ah[k] = b.action_history[5 * (size_t)e + k];
+        float yawc = b.yaw_command[e], cmdc = b.curent_command[e], imu = b.imu_offsets[e];
+        // ---- draws: lane l < 8 block l, the lead lane also block 8 (command resample)
+        float v[3], v8[3];
+        gogoro_post_block(sub < 8 ? sub : 7, e, pa.c_lo, pa.c_hi, k0, k1, v);
+        gogoro_post_block(8, e, pa.c_lo, pa.c_hi, k0, k1, v8);
+        auto slot = [&](int x) {   // exchange slot x = 3 l + j of block l, from lane l
+            const int l = x / 3, j = x % 3;
+            return env_bcast<LPE>(j == 0 ? v[0] : (j == 1 ? v[1] : v[2]), l, sub);
+        };
+        float r[TG_GOGORO_RESET_DRAWS], nd[5];
+#pragma unroll
+        for (int k = 0; k < TG_GOGORO_RESET_DRAWS; ++k) r[k] = slot(GOGORO_RSLOT[k]);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) nd[k] = slot(GOGORO_NSLOT[k]);
+        const float su = v8[0], yu = v8[1];
+        int64_t prog = prog1;
+        if (rflag) {
+            // reset_env: dof rows (every lane), the rest on the lead lane
+            if (owner) {
+#pragma unroll
+                for (int rr = 0; rr < NR; ++rr) {
+                    const int d = sub + LPE * rr;
+                    if (d < D) {
+                        dofs[2 * d] = b.thormang_pose[d];
+                        dofs[2 * d + 1] = 0.0f;
+                    }
+                }
+            }
+            const float target = (r[3] * 2.0f - 1.0f) * F_PI;
+            const float rot = target + u_aff(-1.57f, 1.57f, r[4]);
+            const float hh = rot / 2.0f;
+            const float *tpl = b.root_reset + 13 * (size_t)e;
+            rt[0] = tpl[0];
+            rt[1] = tpl[1];
+            rt[2] = p.terrain_spawn ? tpl[2] : p.spawn_z;
+            rt[3] = 0.0f;
+            rt[4] = 0.0f;
+            rt[5] = sinf(hh);
+            rt[6] = cosf(hh);
+#pragma unroll
+            for (int k = 7; k < 13; ++k) rt[k] = 0.0f;
+            float cv[5];
+            cv[0] = n_aff(p.seat_offset_x_range, r[5]);
+            cv[1] = n_aff(p.seat_offset_y_range, r[6]);
+            cv[2] = n_aff(p.seat_offset_z_range, r[7]);
+            cv[3] = n_aff(p.seat_offset_xr_range, r[8]);
+            cv[4] = n_aff(p.steering_offset, r[9]);
+            imu = cv[3];
+            yawc = target;
+            cmdc = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) ah[k] = 0.0f;
+            if (owner && lead) {
+                b.curent_speed[e] = u_aff(p.speed_range[0], p.speed_range[1], r[0]);
+                b.speed_offset[e] = u_aff(p.speed_sensor_offset[0], p.speed_sensor_offset[1], r[2]);
+#pragma unroll
+                for (int k = 0; k < 5; ++k) b.config_vector[5 * (size_t)e + k] = cv[k];
+                const size_t ND = (size_t)p.num_envs * D;
+                float *prop = b.dof_props + (size_t)e * D;
+                const int seat[3] = {p.dof_base_x, p.dof_base_y, p.dof_base_z};
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    prop[TG_PROP_DRIVE_MODE * ND + seat[k]] = 0.0f;
+                    prop[TG_PROP_LOWER * ND + seat[k]] = cv[k];
+                    prop[TG_PROP_UPPER * ND + seat[k]] = cv[k] + 0.0001f;
+                }
+                b.imu_offsets[e] = cv[3];
+                b.steer_offsets[e] = cv[4];
+                const int st = p.dof_steer;
+                prop[TG_PROP_DRIVE_MODE * ND + st] = 1.0f;
+                prop[TG_PROP_STIFFNESS * ND + st] = p.steer_stiffness;
+                prop[TG_PROP_DAMPING * ND + st] =
+                    u_aff(p.steering_damping_range[0], p.steering_damping_range[1], r[10]);
+                prop[TG_PROP_EFFORT * ND + st] = p.steer_effort;
+                prop[TG_PROP_VELOCITY * ND + st] = p.steer_velocity;
+                b.env_dirty[e] = 1;
+                b.curent_command[e] = 0.0f;
+#pragma unroll
+                for (int k = 0; k < 5; ++k) b.action_history[5 * (size_t)e + k] = 0.0f;
+            }
+            prog = 0;
+        } else if (owner) {
+            // the simulated state: active dofs from LDS, locked ones at their window centre
+#pragma unroll
+            for (int rr = 0; rr < NR; ++rr) {
+                const int d = sub + LPE * rr;
+                if (d < D) {
+                    const int g = DofGroup<M>::tab.g[d];
+                    if (g > 0) {
+                        dofs[2 * d] = s(g * GF + F_Q);
+                        dofs[2 * d + 1] = s(g * GF + F_QD);
+                    } else {
+                        dofs[2 * d] = 0.5f * (prop(a, TG_PROP_LOWER, e, d) + prop(a, TG_PROP_UPPER, e, d));
+                        dofs[2 * d + 1] = 0.f;
+                    }
+                }
+            }
+        }
+        if (!lead || !owner) return;
+#pragma unroll
+        for (int k = 0; k < 13; ++k) root[k] = rt[k];
+        float o[6];
+        observation(rt, yawc, cmdc, o);
+        bool felt;
+        const float rew = gogoro_reward(o, ah, felt);
+        const bool finished = prog >= p.max_episode_length - 1;
+        const int64_t reset = (finished || felt) ? 1 : 0;
+        float rr[6];
+        noisy_observation(p, o, nd, imu, rr);
+        float yc = yawc;
+        if (prog == p.yaw_freq_update) yc = u_aff(-F_PI, F_PI, yu);
+        if (yc > F_PI) yc = yc - F_2PI;
+        if (yc < -F_PI) yc = yc + F_2PI;
+        b.progress_buf[e] = prog;
+        float *bo = b.buffer_obs + 6 * (size_t)e;
+        float *ob = b.obs_buf + 6 * (size_t)e;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            bo[k] = o[k];
+            ob[k] = t_clamp(rr[k], -p.clip_obs, p.clip_obs);
+        }
+        b.rew_buf[e] = felt ? -100.0f : rew;
+        b.reset_buf[e] = reset;
+        if (prog == p.speed_freq_update) b.curent_speed[e] = u_aff(p.speed_range[0], p.speed_range[1], su);
+        b.yaw_command[e] = yc;
+        b.timeout_buf[e] = (prog >= p.max_episode_length - 1) && (reset != 0);
+    }
+};
+
 // ---------------------------------------------------------------- dispatch
 // compose (dirty envs only), then the tree-parallel LDS-resident step,
 // M::EPB envs x M::LPE lanes per workgroup (Thormang: 16 envs, 151 KB of LDS).
@@ -718,6 +881,34 @@ int launch_model_walk(const StepArgs &a, const WalkPostArgs &pa, hipStream_t str
         if (ev_end && hipEventRecord(ev_end, stream) != hipSuccess) return TG_ERR_HIP;
         return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
     }
+}
+
+// the fused Gogoro epilogue is instantiated for the registered task's model
+// (codegen FUSED bit 1), flat ground and terrain
+template <class M>
+int launch_model_gogoro(const StepArgs &a, const GogoroPostArgs &pa, hipStream_t stream, hipEvent_t ev_begin,
+                        hipEvent_t ev_end) {
+    if constexpr ((M::FUSED & 2) == 0) {
+        return 1;
+    } else {
+        if (pa.p.num_dof != M::ND) return 1;
+        hipLaunchKernelGGL(compose_kernel<M>, dim3((a.N + COMPOSE_WPB - 1) / COMPOSE_WPB), dim3(64 * COMPOSE_WPB), 0,
+                           stream, a);
+        if (ev_begin && hipEventRecord(ev_begin, stream) != hipSuccess) return TG_ERR_HIP;
+        if (int rc = a.hf ? launch_par<M, true, GogoroPost>(a, stream, pa) : launch_par<M, false, GogoroPost>(a, stream, pa))
+            return rc;
+        if (ev_end && hipEventRecord(ev_end, stream) != hipSuccess) return TG_ERR_HIP;
+        return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
+    }
+}
+
+#define TG_LAUNCH_GOGORO(MODEL) \
+    if (hash == MODEL::hash) return launch_model_gogoro<MODEL>(a, pa, stream, ev_begin, ev_end);
+
+int launch_step_gogoro(uint64_t hash, const StepArgs &a, const GogoroPostArgs &pa, hipStream_t stream,
+                       hipEvent_t ev_begin, hipEvent_t ev_end) {
+    TG_FOR_EACH_MODEL(TG_LAUNCH_GOGORO)
+    return TG_ERR_MODEL;
 }
 
 #define TG_LAUNCH_WALK(MODEL) \

@@ -14,46 +14,10 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include "gogoro_math.h"
 #include "tg_kernels.h"
 
 namespace tg {
-
-#define F_PI 3.14159265358979323846f
-#define F_2PI 6.28318530717958647692f
-
-__device__ __forceinline__ float t_rem(float a, float b) {
-    float m = fmodf(a, b);
-    if (m != 0.0f && ((b < 0.0f) != (m < 0.0f))) m += b;
-    return m;
-}
-__device__ __forceinline__ float t_clamp(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
-__device__ __forceinline__ float u_aff(float lo, float hi, float u) { return lo + u * (hi - lo); }
-__device__ __forceinline__ float n_aff(const float *mc, float r) { return mc[0] + r * mc[1]; }
-
-__device__ __forceinline__ void observation(const float *root, float desired_yaw, float cmd, float *obs) {
-    const float x = root[3], y = root[4], z = root[5], w = root[6];
-    float roll = t_rem(atan2f(2.0f * (w * x + y * z), w * w - x * x - y * y + z * z), F_2PI);
-    float yaw = t_rem(atan2f(2.0f * (w * z + x * y), w * w + x * x - y * y - z * z), F_2PI);
-    const float s = 2.0f * (w * w) - 1.0f;
-    // quat_rotate_inverse(q, v) = v*s - cross(q,v)*w*2 + q*dot(q,v)*2
-    const float *v = root + 7;
-    float d = x * v[0] + y * v[1] + z * v[2];
-    float lin_x = v[0] * s - (y * v[2] - z * v[1]) * w * 2.0f + x * d * 2.0f;
-    const float *o = root + 10;
-    float da = x * o[0] + y * o[1] + z * o[2];
-    float ang_x = o[0] * s - (y * o[2] - z * o[1]) * w * 2.0f + x * da * 2.0f;
-    float ang_z = o[2] * s - (x * o[1] - y * o[0]) * w * 2.0f + z * da * 2.0f;
-    if (roll > F_PI) roll = roll - F_2PI;
-    if (roll < -F_PI) roll = roll + F_2PI;
-    if (yaw > F_PI) yaw = yaw - F_2PI;
-    if (yaw < -F_PI) yaw = yaw + F_2PI;
-    obs[0] = roll;
-    obs[1] = ang_x;
-    obs[2] = ang_z;
-    obs[3] = lin_x;
-    obs[4] = t_rem(desired_yaw - yaw + F_PI, F_2PI) - F_PI;
-    obs[5] = cmd;
-}
 
 __global__ __launch_bounds__(256) void pre_kernel(tg_gogoro_params p, tg_gogoro_buffers b, const float *actions,
                                                   const float *pre_draws, uint32_t c_lo, uint32_t c_hi) {
@@ -172,13 +136,10 @@ __global__ __launch_bounds__(64) void post_kernel(tg_gogoro_params p, tg_gogoro_
     }
     // ---- draws: lane k < 9 runs Philox block k and leaves its (up to 3) floats in xch
     if (l < 9) {
-        const uint32_t key = l < 5 ? 0x52535430u + (uint32_t)l : (l < 8 ? 0x4F425330u + (uint32_t)(l - 5) : 0x434D4430u);
-        const U4 x = philox(U4{(uint32_t)e, c_lo, c_hi, key}, k0, k1);
-        const float A = u01(x.x), B = gauss(x.x, x.y), C = gauss(x.y, x.z), Dd = u01(x.w), E = u01(x.y),
-                    F = gauss(x.z, x.w);
-        xch[le][3 * l] = (l == 0 || l == 1 || l == 4 || l == 8) ? A : B;
-        xch[le][3 * l + 1] = l == 0 ? C : ((l == 1 || l == 8) ? E : F);
-        xch[le][3 * l + 2] = l == 0 ? Dd : F;
+        float v[3];
+        gogoro_post_block(l, e, c_lo, c_hi, k0, k1, v);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) xch[le][3 * l + j] = v[j];
     }
     __syncthreads();
     float r[TG_GOGORO_RESET_DRAWS];
@@ -187,9 +148,8 @@ __global__ __launch_bounds__(64) void post_kernel(tg_gogoro_params p, tg_gogoro_
 #pragma unroll
             for (int k = 0; k < TG_GOGORO_RESET_DRAWS; ++k) r[k] = reset_draws[(size_t)e * TG_GOGORO_RESET_DRAWS + k];
         } else {
-            const int slot[TG_GOGORO_RESET_DRAWS] = {0, 1, 2, 3, 4, 5, 6, 7, 9, 10, 12};
 #pragma unroll
-            for (int k = 0; k < TG_GOGORO_RESET_DRAWS; ++k) r[k] = xch[le][slot[k]];
+            for (int k = 0; k < TG_GOGORO_RESET_DRAWS; ++k) r[k] = xch[le][GOGORO_RSLOT[k]];
         }
         // reset_env: dof writes over the env's lanes, the rest on the lead lane
         if (owner) {
@@ -261,19 +221,8 @@ __global__ __launch_bounds__(64) void post_kernel(tg_gogoro_params p, tg_gogoro_
     float o[6];
     observation(rt, yawc, cmdc, o);
     // compute_gogoro_reward
-    const float max_tilt = 0.30f;
-    float tilt_err = t_clamp(o[0] / max_tilt, -1.0f, 1.0f);
-    float yaw_err = t_clamp(o[4] / F_PI, -1.0f, 1.0f);
-    float dtilt_err = t_clamp(o[1] / 0.3f, -1.0f, 1.0f);
-    float y30 = yaw_err * 30.0f;
-    float r1 = 1.0f / (1.0f + y30 * y30);
-    float r2 = 1.0f - tilt_err * tilt_err;
-    float r4 = 1.0f - dtilt_err * dtilt_err;
-    float ce = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) ce += 1.0f - ah[k] * ah[k];
-    float rew = r1 * 5.0f + r2 * 0.2f + r4 * 0.3f + ce * 0.5f;
-    const bool felt = fabsf(o[0]) >= max_tilt;
+    bool felt;
+    const float rew = gogoro_reward(o, ah, felt);
     const bool finished = prog >= p.max_episode_length - 1;
     const int64_t reset = (finished || felt) ? 1 : 0;
     // sensor noise (compute_obs_rwd :449-462)
@@ -282,16 +231,11 @@ __global__ __launch_bounds__(64) void post_kernel(tg_gogoro_params p, tg_gogoro_
 #pragma unroll
         for (int k = 0; k < 5; ++k) nd[k] = obs_draws[(size_t)e * 5 + k];
     } else {
-        nd[0] = xch[le][15]; nd[1] = xch[le][16]; nd[2] = xch[le][18]; nd[3] = xch[le][19]; nd[4] = xch[le][21];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) nd[k] = xch[le][GOGORO_NSLOT[k]];
     }
     float rr[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) rr[k] = o[k];
-    rr[0] += n_aff(p.imu_filter_noise, nd[0]) + imu;
-    rr[1] += n_aff(p.imu_noise, nd[1]);
-    rr[2] += n_aff(p.imu_noise, nd[2]);
-    rr[3] = rintf(rr[4]);                     // quirk :457-458 (speed-sensor value discarded)
-    rr[4] += n_aff(p.imu_filter_noise, nd[4]);
+    noisy_observation(p, o, nd, imu, rr);
     // command resampling (:384-389)
     float su, yu;
     if (speed_draws) { su = speed_draws[e]; yu = yaw_draws[e]; }

@@ -63,6 +63,16 @@ struct WalkPostArgs {
     const float *reset_draws, *push_draws;
     uint32_t c_lo, c_hi;
 };
+// tg_gogoro_step's fused post-physics epilogue (articulation.hip GogoroPost)
+struct GogoroPostArgs {
+    tg_gogoro_params p;
+    tg_gogoro_buffers b;
+    uint32_t c_lo, c_hi;
+};
+// compose + step kernel with the Gogoro post-physics fused in; returns 1 when
+// the model has no such instantiation
+int launch_step_gogoro(uint64_t hash, const StepArgs &a, const GogoroPostArgs &pa, hipStream_t stream,
+                       hipEvent_t ev_begin = nullptr, hipEvent_t ev_end = nullptr);
 // compose + step kernel with the walk post-physics fused in; returns 1 (nothing
 // launched) when the model / ground has no fused instantiation
 int launch_step_walk(uint64_t hash, const StepArgs &a, const WalkPostArgs &pa, hipStream_t stream,

@@ -62,6 +62,7 @@ struct tg_sim {
     std::vector<void *> allocs;
     // kernel timing (tg_set_kernel_timing): event pairs recorded, not yet read
     bool walk_unfused = false;   // tg_walk_step: separate post-physics launch (TG_WALK_UNFUSED=1)
+    bool post_unfused = false;   // tg_gogoro_step: separate post-physics launch (TG_POST_UNFUSED=1)
     int timing = 0;          // period (0: off)
     int64_t timing_count = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending, ev_free;
@@ -163,6 +164,7 @@ int tg_sim_create(const tg_model_desc *m, const tg_sim_params *params, int32_t n
     std::unique_ptr<tg_sim> owner(new tg_sim());   // released to the caller on success only
     tg_sim *s = owner.get();
     if (const char *u = getenv("TG_WALK_UNFUSED")) s->walk_unfused = u[0] == '1';
+    if (const char *u = getenv("TG_POST_UNFUSED")) s->post_unfused = u[0] == '1';
     s->device = device;
     s->N = num_envs;
     s->D = m->num_dofs;
@@ -408,7 +410,8 @@ struct DeviceGuard {
     }
 };
 
-static int simulate_args(tg_sim *s, const tg::StepArgs &a, const tg::WalkPostArgs *wp = nullptr) {
+static int simulate_args(tg_sim *s, const tg::StepArgs &a, const tg::WalkPostArgs *wp = nullptr,
+                         const tg::GogoroPostArgs *gp = nullptr) {
     DeviceGuard dg(s->device);
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     const bool timed = s->timing > 0 && s->timing_count % s->timing == 0;
@@ -421,8 +424,9 @@ static int simulate_args(tg_sim *s, const tg::StepArgs &a, const tg::WalkPostArg
             HIPCHK(hipEventCreate(&ev.second));
         }
     }
-    int rc = wp ? tg::launch_step_walk(s->hash, a, *wp, s->stream, ev.first, ev.second)
-                : tg::launch_step(s->hash, a, s->stream, ev.first, ev.second);
+    int rc = wp   ? tg::launch_step_walk(s->hash, a, *wp, s->stream, ev.first, ev.second)
+             : gp ? tg::launch_step_gogoro(s->hash, a, *gp, s->stream, ev.first, ev.second)
+                  : tg::launch_step(s->hash, a, s->stream, ev.first, ev.second);
     // the pair joins the pending list only once both events were recorded by a
     // launch that went through; otherwise it goes back to the free list
     if (rc != 0) {
@@ -542,6 +546,12 @@ int tg_gogoro_step(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_buffers
             g.k1 = (uint32_t)(p->seed >> 32);
             g.c_lo = (uint32_t)counter_pre;
             g.c_hi = (uint32_t)(counter_pre >> 32);
+        }
+        if (i == n_simulate - 1 && !s->post_unfused) {   // post-physics fused into the last step kernel
+            const tg::GogoroPostArgs gp{*p, *b, (uint32_t)counter_post, (uint32_t)(counter_post >> 32)};
+            const int rc = simulate_args(s, a, nullptr, &gp);
+            if (rc == 0) return TG_OK;
+            if (rc < 0) return rc;
         }
         if (int rc = simulate_args(s, a)) return rc;
     }

@@ -85,6 +85,16 @@ def axis_frame(a) -> np.ndarray:
     return np.stack([b1, b2, a], 1)
 
 
+#: models whose step kernel carries a task's post-physics epilogue (bit 1:
+#: ThormangWalk -- selected by tree size in articulation.hip; bit 2: the
+#: registered Gogoro task's scooter)
+FUSED_GOGORO_MODELS = ("gogoro",)
+
+
+def fused_tasks(m: Model) -> int:
+    return 2 if m.name in FUSED_GOGORO_MODELS else 0
+
+
 def emit(m: Model, cname: str) -> str:
     d = ModelDesc(m)
     a = d.arrays
@@ -178,6 +188,7 @@ def emit(m: Model, cname: str) -> str:
         f"{_arr([_arr(p) for p in cpaths] or [_arr([0] * maxd)])};",
         f"  static constexpr int shape_cg[{max(S, 1)}] = {_arr(shape_cg or [0])};",
         f"  static constexpr int SL = {SL}, PAIR = {PAIR}, LPE = {LPE}, EPB = {EPB}, NSTEP = {len(sched)}, MAXC = {maxc};",
+        f"  static constexpr int FUSED = {fused_tasks(m)};  // fused task epilogues: 1 walk, 2 Gogoro",
         f"  static constexpr int sched[{len(sched)}][{SL}] = {_arr([_arr(r) for r in sched])};",
         f"  static constexpr int nchild[{G}] = {_arr([len(c) for c in children])};",
         f"  static constexpr int child[{G}][{maxc}] = {_arr([_arr(c + [-1] * (maxc - len(c))) for c in children])};",
