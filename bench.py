@@ -39,6 +39,7 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0
 TIMING_PERIOD = 16
+MIN_KERNEL_SAMPLES = 32
 
 
 def algorithmic_bytes_per_env_step(task_name: str, env) -> tuple[int, dict]:
@@ -270,6 +271,14 @@ def main():
     env.sim.read_kernel_timing()
     env.sim.set_kernel_timing(TIMING_PERIOD)
     elapsed = timed_region(step, args.steps, world, dev, torch.cuda.synchronize)
+    # a short timed region (the driver's --steps 20) samples only a launch or
+    # two: keep stepping, after the clock has stopped, until MIN_KERNEL_SAMPLES
+    # launches are timed, so kernel_ms is never a one- or two-sample figure
+    extra = 0
+    while (args.steps + extra) // TIMING_PERIOD < MIN_KERNEL_SAMPLES:
+        step()
+        extra += 1
+    torch.cuda.synchronize()
     env.sim.set_kernel_timing(0)
     tot_ms, launches = env.sim.read_kernel_timing()
     kern_ms = tot_ms / max(launches, 1)
@@ -304,7 +313,8 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "tg::step_par_kernel (one launch per simulate)", "kernel_ms": kern_ms,
                      "kernel_launches": launches,
-                     "kernel_timing": f"HIP events around every {TIMING_PERIOD}th launch of the timed region",
+                     "kernel_timing": f"HIP events around every {TIMING_PERIOD}th launch of the timed region"
+                                      + (f" and of {extra} untimed steps after it" if extra else ""),
                      "bytes_per_env_step": bpe, "bytes_source": "SURVEY.md §8(d) algorithmic bytes per env-step",
                      "bytes_breakdown": breakdown, "algorithmic_bytes_per_launch": bpe * N,
                      "kernel_bytes_per_env_step": kbpe,

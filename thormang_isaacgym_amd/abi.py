@@ -215,10 +215,67 @@ def default_dof_props(m: Model, num_envs: int) -> np.ndarray:
     return np.repeat(p[:, None, :], num_envs, axis=1)
 
 
+#: physx keys that size PhysX's own thread pool / GPU buffers: no effect on the
+#: simulated result there either, accepted silently
+PHYSX_RESOURCE_KEYS = frozenset({
+    "num_threads", "num_subscenes", "use_gpu", "default_buffer_size_multiplier", "max_gpu_contact_pairs",
+    "contact_collection"})
+#: physx keys honoured by the solver (DESIGN.md §4 "Solver cfg")
+PHYSX_HONOURED_KEYS = frozenset({"num_position_iterations", "rest_offset", "max_depenetration_velocity"})
+
+
+class SolverCfgWarning(UserWarning):
+    """A cfg ``sim.physx`` key whose PhysX meaning the PGS solver does not reproduce."""
+
+
+def unhonoured_physx_keys(physx: dict, asset_opts: dict | None = None) -> Dict[str, str]:
+    """The ``sim.physx`` keys (``vec_task.py:470-482`` sets them on PhysX's
+    params) that would change a PhysX result but not this solver's, each with
+    the reason.  ``solver_type`` 1 (TGS) and ``num_velocity_iterations``: the
+    contact solve is one velocity-level projected Gauss-Seidel with
+    ``num_position_iterations`` sweeps and a Baumgarte push-out capped by
+    ``max_depenetration_velocity`` -- no bias-free velocity sweeps;
+    ``contact_offset``: contacts are speculative within the asset option
+    ``contact_margin`` instead; ``bounce_threshold_velocity``: no restitution
+    model (every material has restitution 0, as the reference sets none, so a
+    PhysX run would not bounce either).  Unknown keys are reported too."""
+    ao = asset_opts or {}
+    out: Dict[str, str] = {}
+    for k, v in physx.items():
+        if k in PHYSX_RESOURCE_KEYS or k in PHYSX_HONOURED_KEYS:
+            continue
+        if k == "solver_type":
+            if int(v) == 1:
+                out[k] = "TGS requested; the contact solve is velocity-level projected Gauss-Seidel"
+        elif k == "num_velocity_iterations":
+            if int(v) > 0:
+                out[k] = (f"{int(v)} bias-free velocity sweeps requested; only the "
+                          "num_position_iterations sweeps (with push-out bias) are run")
+        elif k == "contact_offset":
+            out[k] = (f"{v} ignored; contacts are speculative within contact_margin "
+                      f"{float(ao.get('contact_margin', 0.05))}")
+        elif k == "bounce_threshold_velocity":
+            out[k] = "no restitution model (restitution 0 everywhere), the threshold has no effect"
+        else:
+            out[k] = "unknown physx key, ignored"
+    return out
+
+
 def sim_params_from_cfg(cfg_sim: dict, asset_opts: dict | None = None, num_envs: int = 1,
-                        env_spacing: float = 1.0) -> tg_sim_params:
-    """Map the reference cfg 'sim' block (vec_task.py:442-490) onto tg_sim_params."""
+                        env_spacing: float = 1.0, warn: bool = True) -> tg_sim_params:
+    """Map the reference cfg 'sim' block (vec_task.py:442-490) onto tg_sim_params.
+
+    ``num_position_iterations`` is the number of PGS sweeps per substep (an
+    asset option ``contact_iterations`` overrides it); the physx keys the
+    solver does not reproduce raise one ``SolverCfgWarning`` naming each
+    (``unhonoured_physx_keys``)."""
+    import warnings
     physx = cfg_sim.get("physx", {})
+    if warn:
+        bad = unhonoured_physx_keys(physx, asset_opts)
+        if bad:
+            warnings.warn("sim.physx keys not reproduced by the PGS solver: " +
+                          "; ".join(f"{k}: {r}" for k, r in bad.items()), SolverCfgWarning, stacklevel=2)
     ao = asset_opts or {}
     sp = tg_sim_params()
     sp.dt = float(cfg_sim["dt"])
@@ -233,7 +290,7 @@ def sim_params_from_cfg(cfg_sim: dict, asset_opts: dict | None = None, num_envs:
     sp.baumgarte = float(ao.get("baumgarte", 0.2))
     sp.limit_stiffness = float(ao.get("limit_stiffness", 1.0))
     sp.limit_damping = float(ao.get("limit_damping", 1.0))
-    sp.contact_iterations = int(ao.get("contact_iterations", max(4, int(physx.get("num_position_iterations", 4)))))
+    sp.contact_iterations = int(ao.get("contact_iterations", max(1, int(physx.get("num_position_iterations", 4)))))
     sp.fix_base = int(bool(ao.get("fix_base_link", False)))
     sp.env_spacing = float(env_spacing)
     sp.envs_per_row = max(1, int(math.sqrt(num_envs)))
