@@ -30,8 +30,11 @@
  *                            domain randomisation (vec_task.py:538-768)
  *   tg_set_shape_friction_indexed
  *                            set_actor_rigid_shape_properties (gogoro_new.py:284-293)
- *   tg_apply_body_forces     apply_rigid_body_force_tensors
+ *   tg_apply_rigid_body_force_tensors
+ *                            apply_rigid_body_force_tensors(sim, forces [N*L,3],
+ *                            torques [N*L,3] | None, space)
  *                            (tasks/gogoro_realistic_turning_sim_paper.py:457)
+ *   tg_apply_body_forces     the same, pre-reduced: one wrench per group [N,G,6]
  *   tg_simulate              gym.simulate (vec_task.py:335): sim.substeps substeps
  *   tg_sync                  fetch_results(sim, True) (vec_task.py:339)
  *   tg_last_error            (replaces the reference's bool returns + assert,
@@ -175,6 +178,18 @@ int tg_set_body_mass_scale_indexed(tg_sim *sim, const float *scale, const int32_
 int tg_set_shape_friction_indexed(tg_sim *sim, const float *mu, const int32_t *ids, int32_t n);
 int tg_set_gravity(tg_sim *sim, const float *g3);
 int tg_apply_body_forces(tg_sim *sim, const float *wrench);
+/* apply_rigid_body_force_tensors (gymapi; tasks/gogoro_realistic_turning_sim_paper.py:457):
+ * forces [N*L,3] acting at each rigid body's centre of mass and torques
+ * [N*L,3], either may be NULL (the reference passes torqueTensor=None), in the
+ * world frame (TG_ENV_SPACE, isaacgym's default; envs are translated, not
+ * rotated) or each body's own frame (TG_LOCAL_SPACE).  Bodies in model.links
+ * order (the order of get_actor_rigid_body_dict).  Reduced on the sim stream,
+ * from the current root / dof state, to the group wrenches tg_apply_body_forces
+ * takes (world force, torque about the group centre of mass); they act for the
+ * next tg_simulate call, as PhysX's applied forces do for one simulate. */
+#define TG_ENV_SPACE 0
+#define TG_LOCAL_SPACE 1
+int tg_apply_rigid_body_force_tensors(tg_sim *sim, const float *forces, const float *torques, int32_t space);
 /* Terrain ground (gym.add_triangle_mesh of the heightfield trimesh,
  * tasks/gogoro_new.py:164-181 with terrain_utils.convert_heightfield_to_trimesh):
  * heights [rows, cols] row-major on the HOST, vertex (i, j) at

@@ -996,55 +996,60 @@ static void m3_to_quat_d(const M3 R, real *q) {
     }
 }
 
+/* world pose and velocity of every link of env e (links in tree order):
+ * R_l, P_l (link origin), W_l, V_l (velocity of the link origin) */
+static void fk_links(const tg_model_desc *m, const float *r, const float *q, M3 *R, V3 *P, V3 *W, V3 *V) {
+    int L = m->num_links;
+    for (int l = 0; l < L; ++l) {
+        int p = m->link_parent[l];
+        const float *in = m->link_inertia + 10 * l;
+        V3 c = {in[1], in[2], in[3]}, Rc;
+        if (p < 0) {
+            real qq[4] = {r[3], r[4], r[5], r[6]};
+            real nq = sqrt(qq[0] * qq[0] + qq[1] * qq[1] + qq[2] * qq[2] + qq[3] * qq[3]);
+            for (int k = 0; k < 4; ++k) qq[k] /= nq;
+            quat_to_m3(qq, R[l]);
+            for (int k = 0; k < 3; ++k) { P[l][k] = r[k]; W[l][k] = r[10 + k]; }
+            m3_v(R[l], c, Rc);
+            V3 wxc;
+            cross3(W[l], Rc, wxc);
+            for (int k = 0; k < 3; ++k) V[l][k] = r[7 + k] - wxc[k];
+            continue;
+        }
+        const float *o = m->link_origin + 12 * l;
+        M3 Ro, Rj;
+        V3 to = {o[9], o[10], o[11]}, ax = {m->link_axis[3 * l], m->link_axis[3 * l + 1], m->link_axis[3 * l + 2]};
+        for (int k = 0; k < 9; ++k) Ro[k] = o[k];
+        int d = m->link_dof[l];
+        real qq = d >= 0 ? q[2 * d] : 0.0, qd = d >= 0 ? q[2 * d + 1] : 0.0;
+        V3 s, aw;
+        m3_v(Ro, ax, s);
+        m3_v(R[p], s, aw);
+        memcpy(W[l], W[p], sizeof(V3));
+        if (m->link_jtype[l] == TG_JOINT_REVOLUTE) {
+            axis_angle(ax, qq, Rj);
+            m3_mul(Ro, Rj, Ro);
+            for (int k = 0; k < 3; ++k) W[l][k] += qd * aw[k];
+        } else if (m->link_jtype[l] == TG_JOINT_PRISMATIC) {
+            for (int k = 0; k < 3; ++k) to[k] += qq * s[k];
+        }
+        m3_mul(R[p], Ro, R[l]);
+        V3 t, dp, wxd;
+        m3_v(R[p], to, t);
+        for (int k = 0; k < 3; ++k) { P[l][k] = P[p][k] + t[k]; dp[k] = t[k]; }
+        cross3(W[p], dp, wxd);
+        for (int k = 0; k < 3; ++k) V[l][k] = V[p][k] + wxd[k];
+        if (m->link_jtype[l] == TG_JOINT_PRISMATIC)
+            for (int k = 0; k < 3; ++k) V[l][k] += qd * aw[k];
+    }
+}
+
 void oracle_rigid_body_states(const tg_model_desc *m, int n, const float *root, const float *dof, float *out) {
     int L = m->num_links, D = m->num_dofs;
     for (int e = 0; e < n; ++e) {
         M3 R[MAXL];
         V3 P[MAXL], W[MAXL], V[MAXL];
-        const float *r = root + 13L * e;
-        const float *q = dof + 2L * e * D;
-        for (int l = 0; l < L; ++l) {
-            int p = m->link_parent[l];
-            const float *in = m->link_inertia + 10 * l;
-            V3 c = {in[1], in[2], in[3]}, Rc;
-            if (p < 0) {
-                real qq[4] = {r[3], r[4], r[5], r[6]};
-                real nq = sqrt(qq[0] * qq[0] + qq[1] * qq[1] + qq[2] * qq[2] + qq[3] * qq[3]);
-                for (int k = 0; k < 4; ++k) qq[k] /= nq;
-                quat_to_m3(qq, R[l]);
-                for (int k = 0; k < 3; ++k) { P[l][k] = r[k]; W[l][k] = r[10 + k]; }
-                m3_v(R[l], c, Rc);
-                V3 wxc;
-                cross3(W[l], Rc, wxc);
-                for (int k = 0; k < 3; ++k) V[l][k] = r[7 + k] - wxc[k];
-                continue;
-            }
-            const float *o = m->link_origin + 12 * l;
-            M3 Ro, Rj;
-            V3 to = {o[9], o[10], o[11]}, ax = {m->link_axis[3 * l], m->link_axis[3 * l + 1], m->link_axis[3 * l + 2]};
-            for (int k = 0; k < 9; ++k) Ro[k] = o[k];
-            int d = m->link_dof[l];
-            real qq = d >= 0 ? q[2 * d] : 0.0, qd = d >= 0 ? q[2 * d + 1] : 0.0;
-            V3 s, aw;
-            m3_v(Ro, ax, s);
-            m3_v(R[p], s, aw);
-            memcpy(W[l], W[p], sizeof(V3));
-            if (m->link_jtype[l] == TG_JOINT_REVOLUTE) {
-                axis_angle(ax, qq, Rj);
-                m3_mul(Ro, Rj, Ro);
-                for (int k = 0; k < 3; ++k) W[l][k] += qd * aw[k];
-            } else if (m->link_jtype[l] == TG_JOINT_PRISMATIC) {
-                for (int k = 0; k < 3; ++k) to[k] += qq * s[k];
-            }
-            m3_mul(R[p], Ro, R[l]);
-            V3 t, dp, wxd;
-            m3_v(R[p], to, t);
-            for (int k = 0; k < 3; ++k) { P[l][k] = P[p][k] + t[k]; dp[k] = t[k]; }
-            cross3(W[p], dp, wxd);
-            for (int k = 0; k < 3; ++k) V[l][k] = V[p][k] + wxd[k];
-            if (m->link_jtype[l] == TG_JOINT_PRISMATIC)
-                for (int k = 0; k < 3; ++k) V[l][k] += qd * aw[k];
-        }
+        fk_links(m, root + 13L * e, dof + 2L * e * D, R, P, W, V);
         for (int l = 0; l < L; ++l) {
             const float *in = m->link_inertia + 10 * l;
             V3 c = {in[1], in[2], in[3]}, Rc, wxc;
@@ -1057,5 +1062,65 @@ void oracle_rigid_body_states(const tg_model_desc *m, int n, const float *root, 
             for (int k = 0; k < 4; ++k) o[3 + k] = (float)qo[k];
             for (int k = 0; k < 3; ++k) { o[7 + k] = (float)(V[l][k] + wxc[k]); o[10 + k] = (float)W[l][k]; }
         }
+    }
+}
+
+/* apply_rigid_body_force_tensors (isaacgym gymapi; reference call site
+ * tasks/gogoro_realistic_turning_sim_paper.py:457): per-link forces f_l
+ * [N*L,3] acting at the link's centre of mass and optional torques t_l
+ * [N*L,3], in the world frame (space 0, ENV_SPACE) or the link frame (space 1,
+ * LOCAL_SPACE), reduced to one wrench per group at the group's centre of mass
+ * (the tg_apply_body_forces layout [N,G,6], world frame):
+ *   F_g = sum f_l,   T_g = sum t_l + (p_l - c_g) x f_l,
+ * p_l = P_l + R_l c_l the link's com and c_g = sum m_l s_l p_l / sum m_l s_l
+ * (s_l: the per-env mass scale, NULL = 1) from the current root / dof state
+ * (massless group: its root link's origin).  Sums in link order. */
+void oracle_rigid_body_force_wrench(const tg_model_desc *m, int n, const float *root, const float *dof,
+                                    const float *mass_scale, const float *forces, const float *torques, int space,
+                                    float *out) {
+    int L = m->num_links, D = m->num_dofs, G = m->num_groups;
+    for (int e = 0; e < n; ++e) {
+        M3 R[MAXL];
+        V3 P[MAXL], W[MAXL], V[MAXL], pc[MAXL], f[MAXL], t[MAXL];
+        fk_links(m, root + 13L * e, dof + 2L * e * D, R, P, W, V);
+        real gm[MAXL], gc[MAXL][3];
+        for (int g = 0; g < G; ++g) { gm[g] = 0; gc[g][0] = gc[g][1] = gc[g][2] = 0; }
+        for (int l = 0; l < L; ++l) {
+            const float *in = m->link_inertia + 10 * l;
+            V3 c = {in[1], in[2], in[3]}, Rc;
+            m3_v(R[l], c, Rc);
+            for (int k = 0; k < 3; ++k) pc[l][k] = P[l][k] + Rc[k];
+            real ml = in[0] * (mass_scale ? mass_scale[(size_t)e * L + l] : 1.0f);
+            int g = m->link_group[l];
+            gm[g] += ml;
+            for (int k = 0; k < 3; ++k) gc[g][k] += ml * pc[l][k];
+            V3 fl = {forces[3 * ((size_t)e * L + l)], forces[3 * ((size_t)e * L + l) + 1],
+                     forces[3 * ((size_t)e * L + l) + 2]};
+            V3 tl = {0, 0, 0};
+            if (torques)
+                for (int k = 0; k < 3; ++k) tl[k] = torques[3 * ((size_t)e * L + l) + k];
+            if (space == 1) {
+                m3_v(R[l], fl, f[l]);
+                m3_v(R[l], tl, t[l]);
+            } else {
+                memcpy(f[l], fl, sizeof(V3));
+                memcpy(t[l], tl, sizeof(V3));
+            }
+        }
+        for (int g = 0; g < G; ++g) {
+            int r = m->group_root[g];
+            for (int k = 0; k < 3; ++k) gc[g][k] = gm[g] > 0 ? gc[g][k] / gm[g] : P[r][k];
+        }
+        float *o = out + (size_t)6 * G * e;
+        real acc[MAXL][6];
+        memset(acc, 0, sizeof(real) * 6 * G);
+        for (int l = 0; l < L; ++l) {
+            int g = m->link_group[l];
+            V3 d = {pc[l][0] - gc[g][0], pc[l][1] - gc[g][1], pc[l][2] - gc[g][2]}, dxf;
+            cross3(d, f[l], dxf);
+            for (int k = 0; k < 3; ++k) { acc[g][k] += f[l][k]; acc[g][3 + k] += t[l][k] + dxf[k]; }
+        }
+        for (int g = 0; g < G; ++g)
+            for (int k = 0; k < 6; ++k) o[6 * g + k] = (float)acc[g][k];
     }
 }

@@ -44,6 +44,7 @@ def lib(precision: str = "f64"):
         _lib.oracle_physics_step.argtypes = [vp, vp, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_int]
         _lib.oracle_set_heightfield.argtypes = [vp, C.c_int, C.c_int] + [C.c_float] * 5
         _lib.oracle_rigid_body_states.argtypes = [vp, C.c_int, vp, vp, vp]
+        _lib.oracle_rigid_body_force_wrench.argtypes = [vp, C.c_int, vp, vp, vp, vp, vp, C.c_int, vp]
         _lib.oracle_gogoro_reset_env.argtypes = [vp, vp, C.c_int, vp]
         _libs[precision] = _lib
     return _libs[precision]

@@ -72,7 +72,8 @@ class OraclePaper:
         rd = reset_draws(draws, np.arange(n), n, switches["RANDOM_DAMPING"], switches["CENTER_ROBOT"])
         for e in range(n):
             lib().oracle_paper_reset_env(C.byref(self.p), C.byref(self.b), e, ptr(np.ascontiguousarray(rd[e])))
-        self.desc = None
+        self.desc = self.sp = None
+        self.head_id = [l.name for l in m.links].index("head_p_link")
 
     def pre(self, actions):
         lib().oracle_paper_pre_physics(C.byref(self.p), C.byref(self.b),
@@ -84,8 +85,15 @@ class OraclePaper:
         rd, nd, sd, yd, pd = post_draws(self.src, ids, a["progress_buf"].copy(), int(self.p.speed_freq_update),
                                         self.sw["PUSH_ROBOT"], self.sw["RANDOM_DAMPING"], self.sw["CENTER_ROBOT"])
         lib().oracle_paper_post_physics(C.byref(self.p), C.byref(self.b), ptr(rd), ptr(nd), ptr(sd), ptr(yd), ptr(pd))
-        if self.sw["PUSH_ROBOT"]:
-            lib().oracle_paper_head_wrench(C.byref(self.p), C.byref(self.b))
+        if self.sw["PUSH_ROBOT"]:   # apply_rigid_body_force_tensors of the [N*L, 3] perturbations (:449-457)
+            if self.desc is None:
+                self.desc = abi.ModelDesc(self.model)
+            L = self.model.num_bodies
+            f = np.zeros((self.n, L, 3), np.float32)
+            f[:, self.head_id] = a["perturbation"]
+            self._forces = f
+            lib().oracle_rigid_body_force_wrench(C.byref(self.desc.desc), self.n, ptr(a["root"]), ptr(a["dof_state"]),
+                                                 None, ptr(f), None, 0, ptr(a["body_force"]))
         return a["obs_buf"], a["rew_buf"], a["reset_buf"], a["timeout_buf"]
 
     def step(self, actions):
@@ -98,8 +106,9 @@ class OraclePaper:
         """One control step of the fp64 oracle engine (the product's tg_simulate)."""
         if self.desc is None:
             self.desc = abi.ModelDesc(self.model)
+        if self.sp is None:
             ao = dict(ASSET_OPTIONS, fix_base_link=bool(self.sw["DEBUGFIXBASE"]))
-            self.sp = abi.sim_params_from_cfg(self.cfg["sim"], ao, self.n, env_spacing)
+            self.sp = abi.sim_params_from_cfg(self.cfg["sim"], ao, self.n, env_spacing, warn=False)
         a = self.a
         force = a["body_force"] if self.sw["PUSH_ROBOT"] else None
         physics_step(self.desc, self.sp, a["root"], a["dof_state"], a["dof_props"], a["pos_target"], a["vel_target"],

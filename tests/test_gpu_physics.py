@@ -132,3 +132,43 @@ def test_gpu_rigid_body_states_match_oracle(name):
     np.testing.assert_allclose(g[..., :3], o[..., :3], atol=3e-5)
     np.testing.assert_allclose(g[..., 3:7] * sgn, o[..., 3:7], atol=3e-5)
     np.testing.assert_allclose(g[..., 7:13], o[..., 7:13], atol=2e-4, rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["thormang", "gogoro"])
+@pytest.mark.parametrize("space", [0, 1])
+def test_gpu_rigid_body_force_tensors_match_oracle(name, space):
+    """apply_rigid_body_force_tensors (tg_apply_rigid_body_force_tensors, the
+    reference's [N*L,3] layout, gogoro_realistic_turning_sim_paper.py:457) vs
+    the oracle's reduction to group wrenches, on random states, forces,
+    torques and per-env mass scales; then torques only."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs the MI355X")
+    from tests.test_rb_forces import oracle_wrench
+    from tests.test_rigid_body_states import random_state
+    from thormang_isaacgym_amd import abi
+    from thormang_isaacgym_amd.sim import Sim, load_model
+    m = load_model(name)
+    n, L = 512, m.num_bodies
+    rs = np.random.default_rng(21 + space)
+    root, dof = random_state(m, n, rs)
+    f = rs.normal(0, 20.0, (n, L, 3)).astype(np.float32)
+    t = rs.normal(0, 2.0, (n, L, 3)).astype(np.float32)
+    ms = rs.uniform(0.9, 1.1, (n, L)).astype(np.float32)
+    sp = abi.sim_params_from_cfg({"dt": 0.01, "substeps": 1, "gravity": [0, 0, -9.81]}, {}, n)
+    s = Sim(m, sp, n, "cuda:0")
+    s.root_state.copy_(torch.from_numpy(root))
+    s.dof_state.copy_(torch.from_numpy(dof))
+    ids = torch.arange(n, device="cuda:0")
+    s.set_body_mass_scale_indexed(torch.from_numpy(ms).cuda(), ids)
+    assert s.apply_rigid_body_force_tensors(torch.from_numpy(f).cuda().reshape(-1, 3),
+                                            torch.from_numpy(t).cuda().reshape(-1, 3), space)
+    torch.cuda.synchronize()
+    got = s.body_force.cpu().numpy()
+    ref = oracle_wrench(m, root, dof, f, t, space, ms)
+    scale = np.abs(ref).max()
+    np.testing.assert_allclose(got, ref, atol=2e-5 * scale, rtol=1e-4)
+    s.apply_rigid_body_force_tensors(None, torch.from_numpy(t).cuda(), space)
+    torch.cuda.synchronize()
+    ref_t = oracle_wrench(m, root, dof, np.zeros_like(f), t, space, ms)
+    np.testing.assert_allclose(s.body_force.cpu().numpy(), ref_t, atol=2e-5 * scale, rtol=1e-4)

@@ -34,6 +34,7 @@ SIGNATURES = {
     "tg_set_shape_friction_indexed": [_VP, _VP, _VP, C.c_int32],
     "tg_set_gravity": [_VP, C.POINTER(C.c_float)],
     "tg_apply_body_forces": [_VP, _VP],
+    "tg_apply_rigid_body_force_tensors": [_VP, _VP, _VP, C.c_int32],
     "tg_set_heightfield": [_VP, _VP, C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float],
     "tg_simulate": [_VP],
     "tg_rigid_body_states": [_VP, _VP],

@@ -459,6 +459,106 @@ template <class M> __global__ __launch_bounds__(64) void body_state_kernel(const
     }
 }
 
+// ---------------------------------------------------------------- rigid-body forces
+// apply_rigid_body_force_tensors (reference call site
+// tasks/gogoro_realistic_turning_sim_paper.py:457): per-link forces [N*L,3] at
+// the link coms and optional torques [N*L,3], world (space 0) or link frame
+// (space 1), reduced to the step kernel's group wrenches [N,G,6] (world force,
+// torque about the group com): F_g = sum f_l, T_g = sum t_l + (p_l - c_g) x f_l,
+// c_g the mass-weighted (per-env mass scale) com of the group's links.  One
+// wavefront per env: link poses level by level (lane = link), then lane = group
+// sums its links in link order.  The same function as oracle/physics_ref.c
+// oracle_rigid_body_force_wrench.
+template <class M> __global__ __launch_bounds__(64) void rb_force_kernel(const float *root, const float *dof, int n,
+                                                                         const float *mass_scale, const float *forces,
+                                                                         const float *torques, int space, float *out) {
+    const int e = blockIdx.x;
+    if (e >= n) return;
+    __shared__ float T[M::NL][12];    // R (9), p (3); then com (3), mass, f (3), t (3) per link
+    __shared__ float F[M::NL][10];
+    const int lane = threadIdx.x;
+    const float *r = root + 13 * (size_t)e;
+    const float *q = dof + 2 * (size_t)e * M::ND;
+    auto wsync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    for (int lev = 0; lev <= M::NDEPTH; ++lev) {
+        for (int l = lane; l < M::NL; l += 64) {
+            if (M::link_depth[l] != lev) continue;
+            M3 R;
+            V3 P;
+            if (M::link_parent[l] < 0) {
+                float qx = r[3], qy = r[4], qz = r[5], qw = r[6];
+                const float in = rsqrtf(qx * qx + qy * qy + qz * qz + qw * qw);
+                R = quat_to_m3(qx * in, qy * in, qz * in, qw * in);
+                P = v3(r[0], r[1], r[2]);
+            } else {
+                const int pl = M::link_parent[l];
+                M3 Rp;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) Rp.a[k] = T[pl][k];
+                const V3 Pp = v3(T[pl][9], T[pl][10], T[pl][11]);
+                const float *o = M::link_origin[l];
+                M3 Ro{{o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7], o[8]}};
+                V3 to = v3(o[9], o[10], o[11]);
+                const int d = M::link_dof[l];
+                const float qq = d >= 0 ? q[2 * d] : 0.f;
+                const float *ax = M::link_axis[l];
+                if (M::link_jtype[l] == TG_JOINT_REVOLUTE) Ro = mul(Ro, rot_axis(ax[0], ax[1], ax[2], qq));
+                else if (M::link_jtype[l] == TG_JOINT_PRISMATIC) to = to + qq * mul(Ro, v3(ax[0], ax[1], ax[2]));
+                R = mul(Rp, Ro);
+                P = Pp + mul(Rp, to);
+            }
+#pragma unroll
+            for (int k = 0; k < 9; ++k) T[l][k] = R.a[k];
+            T[l][9] = P.x; T[l][10] = P.y; T[l][11] = P.z;
+        }
+        wsync();
+    }
+    for (int l = lane; l < M::NL; l += 64) {
+        M3 R;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) R.a[k] = T[l][k];
+        const V3 pc = v3(T[l][9], T[l][10], T[l][11]) +
+                      mul(R, v3(M::link_inertia[l][1], M::link_inertia[l][2], M::link_inertia[l][3]));
+        const size_t i = (size_t)e * M::NL + l;
+        V3 f = v3(forces[3 * i], forces[3 * i + 1], forces[3 * i + 2]);
+        V3 t = torques ? v3(torques[3 * i], torques[3 * i + 1], torques[3 * i + 2]) : v3(0, 0, 0);
+        if (space == 1) {
+            f = mul(R, f);
+            t = mul(R, t);
+        }
+        F[l][0] = pc.x; F[l][1] = pc.y; F[l][2] = pc.z;
+        F[l][3] = M::link_inertia[l][0] * (mass_scale ? mass_scale[i] : 1.f);
+        F[l][4] = f.x; F[l][5] = f.y; F[l][6] = f.z;
+        F[l][7] = t.x; F[l][8] = t.y; F[l][9] = t.z;
+    }
+    wsync();
+    for (int g = lane; g < M::NG; g += 64) {
+        float gm = 0.f;
+        V3 gc = v3(0, 0, 0);
+        for (int k = 0; k < M::group_nlinks[g]; ++k) {
+            const int l = M::group_links[g][k];
+            gm += F[l][3];
+            gc = gc + F[l][3] * v3(F[l][0], F[l][1], F[l][2]);
+        }
+        const int rl = M::group_links[g][0];
+        gc = gm > 0.f ? (1.0f / gm) * gc : v3(T[rl][9], T[rl][10], T[rl][11]);
+        V3 fs = v3(0, 0, 0), ts = v3(0, 0, 0);
+        for (int k = 0; k < M::group_nlinks[g]; ++k) {
+            const int l = M::group_links[g][k];
+            const V3 f = v3(F[l][4], F[l][5], F[l][6]);
+            fs = fs + f;
+            ts = ts + v3(F[l][7], F[l][8], F[l][9]) + cross(v3(F[l][0], F[l][1], F[l][2]) - gc, f);
+        }
+        float *o = out + ((size_t)e * M::NG + g) * 6;
+        o[0] = fs.x; o[1] = fs.y; o[2] = fs.z;
+        o[3] = ts.x; o[4] = ts.y; o[5] = ts.z;
+    }
+}
+
 // ---------------------------------------------------------------- contact row layout
 // rows of shape s: shape_nrows[s] normal rows, then friction t1, t2 and torsion
 template <class M> __device__ __forceinline__ constexpr int row_shape(int i) {
@@ -955,6 +1055,19 @@ extern "C" int tg_prof_read(unsigned long long *out, int n) {
 
 int launch_body_states(uint64_t hash, const float *root, const float *dof, int n, float *out, hipStream_t stream) {
     TG_FOR_EACH_MODEL(TG_BODY_STATES)
+    return TG_ERR_MODEL;
+}
+
+#define TG_RB_FORCES(MODEL)                                                                               \
+    if (hash == MODEL::hash) {                                                                            \
+        hipLaunchKernelGGL(rb_force_kernel<MODEL>, dim3(n), dim3(64), 0, stream, root, dof, n, mass_scale,  \
+                           forces, torques, space, out);                                                  \
+        return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;                                          \
+    }
+
+int launch_rb_forces(uint64_t hash, const float *root, const float *dof, int n, const float *mass_scale,
+                     const float *forces, const float *torques, int space, float *out, hipStream_t stream) {
+    TG_FOR_EACH_MODEL(TG_RB_FORCES)
     return TG_ERR_MODEL;
 }
 

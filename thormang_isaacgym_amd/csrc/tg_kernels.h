@@ -84,6 +84,9 @@ int launch_step(uint64_t hash, const StepArgs &a, hipStream_t stream, hipEvent_t
 int launch_compose(uint64_t hash, const StepArgs &a, hipStream_t stream);
 int compiled_hashes(uint64_t *out, int cap);
 int launch_body_states(uint64_t hash, const float *root, const float *dof, int n, float *out, hipStream_t stream);
+// per-link forces / torques [N*L,3] -> group wrenches [N,G,6] (rb_force_kernel)
+int launch_rb_forces(uint64_t hash, const float *root, const float *dof, int n, const float *mass_scale,
+                     const float *forces, const float *torques, int space, float *out, hipStream_t stream);
 int model_kc(uint64_t hash);
 
 int launch_gogoro_pre(const tg_gogoro_params &p, const tg_gogoro_buffers &b, const float *actions,

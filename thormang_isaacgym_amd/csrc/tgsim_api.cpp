@@ -52,6 +52,7 @@ struct tg_sim {
     // device buffers
     float *root = nullptr, *dof = nullptr, *pos_tgt = nullptr, *vel_tgt = nullptr, *act = nullptr;
     float *props = nullptr, *force = nullptr, *mass_scale = nullptr, *shape_mu = nullptr, *comp = nullptr;
+    float *zero_link3 = nullptr;   // [N*L*3] zeros (torque-only rigid-body force calls), lazily allocated
     float *env_origin = nullptr;
     uint8_t *dirty = nullptr;
     int *err = nullptr;   // sticky state-error flag set by kernels (tg_sync reports it)
@@ -443,6 +444,26 @@ static int simulate_args(tg_sim *s, const tg::StepArgs &a, const tg::WalkPostArg
 int tg_simulate(tg_sim *s) {
     if (int rc = check_sim(s)) return rc;
     return simulate_args(s, step_args(s));
+}
+
+int tg_apply_rigid_body_force_tensors(tg_sim *s, const float *forces, const float *torques, int32_t space) {
+    if (int rc = check_sim(s)) return rc;
+    if (!forces && !torques) return fail(TG_ERR_ARG, "apply_rigid_body_force_tensors: no force or torque tensor");
+    if (space != TG_ENV_SPACE && space != TG_LOCAL_SPACE) return fail(TG_ERR_ARG, "space must be TG_ENV_SPACE or TG_LOCAL_SPACE");
+    DeviceGuard dg(s->device);
+    const float *f = forces;
+    if (!f) {   // torques only: a zero force tensor
+        if (!s->zero_link3) {
+            if (int rc = s->alloc(&s->zero_link3, (size_t)s->N * s->L * 3)) return fail(rc, "allocation failed");
+            HIPCHK(hipMemsetAsync(s->zero_link3, 0, (size_t)s->N * s->L * 3 * 4, s->stream));
+        }
+        f = s->zero_link3;
+    }
+    if (int rc = tg::launch_rb_forces(s->hash, s->root, s->dof, (int)s->N, s->mass_scale, f, torques, space, s->force,
+                                      s->stream))
+        return fail(rc, "rigid-body force launch failed");
+    s->forces_pending = true;
+    return TG_OK;
 }
 
 int tg_rigid_body_states(tg_sim *s, float *out) {

@@ -131,7 +131,29 @@ class Sim:
         self.gravity = [float(x) for x in g]
 
     def apply_body_forces(self, wrench: torch.Tensor):
-        check(lib().tg_apply_body_forces(self._h, _ptr(self._dev(wrench))), "apply_rigid_body_force_tensors")
+        """Group wrenches [N, G, 6] (world force, torque about the group com) for the next simulate."""
+        check(lib().tg_apply_body_forces(self._h, _ptr(self._dev(wrench))), "apply_body_forces")
+
+    ENV_SPACE, LOCAL_SPACE = 0, 1
+
+    def apply_rigid_body_force_tensors(self, forces, torques=None, space: int = 0):
+        """gym.apply_rigid_body_force_tensors(sim, forceTensor, torqueTensor, space)
+        (tasks/gogoro_realistic_turning_sim_paper.py:457): forces / torques
+        [N*L, 3] (or [N, L, 3]) at the rigid bodies' coms, world (ENV_SPACE) or
+        body frame (LOCAL_SPACE), for the next simulate.  Returns True, as gym does."""
+        def flat(t):
+            if t is None:
+                return None
+            t = self._dev(t)
+            if t.numel() != self.num_envs * self.L * 3:
+                raise ValueError(f"rigid-body force tensor must hold N*L*3 = {self.num_envs * self.L * 3} floats, "
+                                 f"got shape {tuple(t.shape)}")
+            return t.reshape(-1, 3).contiguous()
+        f, t = flat(forces), flat(torques)
+        check(lib().tg_apply_rigid_body_force_tensors(self._h, _ptr(f), _ptr(t), int(space)),
+              "apply_rigid_body_force_tensors")
+        self._keep_forces = (f, t)   # the reduction runs on the sim stream; hold the inputs until the next call
+        return True
 
     def set_heightfield(self, heights, horizontal_scale: float = 1.0, vertical_scale: float = 1.0,
                         origin_x: float = 0.0, origin_y: float = 0.0, friction: float = 1.0):

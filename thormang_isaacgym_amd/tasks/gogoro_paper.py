@@ -228,6 +228,8 @@ class Gogoro(VecTask):
         self.root_reset_tensor = self.root_tensor.clone().detach()
         self.root_reset_tensor[:, 7:13] = 0
         self.head_perturbation = torch.zeros((n, 3), device=dev)  # curent_perturbations[:, head_p_link]
+        self._perturbations = torch.zeros((n, self.num_rgbd, 3), device=dev)
+        self._head_id = self.rgid_body_to_id["head_p_link"]
         self.scratch = torch.zeros(n, device=dev)
         self.current_steering = None
         self.params = paper_params(self.cfg, self.model, n, self.switches, self.seed)
@@ -236,10 +238,8 @@ class Gogoro(VecTask):
 
     @property
     def curent_perturbations(self) -> torch.Tensor:
-        """[N, num_rgbd, 3] view of the reference's perturbation tensor (only head_p_link is ever pushed)."""
-        out = torch.zeros((self.n_envs, self.num_rgbd, 3), device=self.device)
-        out[:, self.rgid_body_to_id["head_p_link"]] = self.head_perturbation
-        return out
+        """[N, num_rgbd, 3] the reference's perturbation tensor (:457); only head_p_link is ever pushed."""
+        return self._perturbations
 
     # ------------------------------------------------------------ creation
     def create_sim(self):
@@ -274,7 +274,7 @@ class Gogoro(VecTask):
                      root_reset=self.root_reset_tensor, thormang_pose=self.thormang_pose, root=self.sim.root_state,
                      dof_state=self.sim.dof_state, pos_target=self.sim.dof_pos_target,
                      vel_target=self.sim.dof_vel_target, dof_props=self.sim.dof_props,
-                     body_force=self.sim.body_force if push else None, env_dirty=self.sim.env_dirty,
+                     body_force=None, env_dirty=self.sim.env_dirty,
                      scratch=self.scratch)
         for k, t in pairs.items():
             if t is None:
@@ -313,8 +313,9 @@ class Gogoro(VecTask):
                                           _p(sd), _p(yd), _p(pd), self._counter()), "tg_paper_post_physics")
         self._keep_post = keep
         self.curent_step += 1
-        if self.switches["PUSH_ROBOT"]:
-            self.sim.apply_body_forces(self.sim.body_force)   # apply_rigid_body_force_tensors (:457)
+        if self.switches["PUSH_ROBOT"]:   # :449-457, the reference's own [N*L, 3] tensor
+            self._perturbations[:, self._head_id] = self.head_perturbation
+            self.sim.apply_rigid_body_force_tensors(torch.flatten(self._perturbations, end_dim=-2), None)
 
     def compute_obs_rwd(self):
         raise NotImplementedError("compute_obs_rwd runs inside the fused post-physics kernel")
