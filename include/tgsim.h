@@ -216,6 +216,18 @@ int tg_rigid_body_states(tg_sim *sim, float *out);
 int tg_sync(tg_sim *sim);
 const char *tg_last_error(void);
 uint64_t tg_compiled_model_hashes(uint64_t *out, int32_t cap); /* returns count */
+/* gym.load_asset of a model that is not compiled in (gogoro_new.py:198-213
+ * loads its URDF at run time): compile the articulation kernels for it with
+ * hipRTC (gfx950) and register them under model_hash, after which
+ * tg_sim_create accepts a tg_model_desc with that hash.  model_source is the
+ * model's constexpr table text as thormang_isaacgym_amd/model/codegen.py emits
+ * it (one `struct <struct_name> {...}`; the Python host parses the URDF and
+ * produces both it and the tg_model_desc).  include_dir: the kernel headers
+ * (NULL: the csrc/ directory beside libtgsim.so); cache_dir: where code objects
+ * are cached by hash and source digest (NULL: no cache).  A no-op for a
+ * compiled-in hash or one already registered in this process. */
+int tg_model_jit(uint64_t model_hash, const char *struct_name, const char *model_source, const char *include_dir,
+                 const char *cache_dir);
 
 /* Random-number instrumentation (no reference counterpart; the task kernels'
  * in-kernel draws replace the reference's torch.rand / torch.randn calls):

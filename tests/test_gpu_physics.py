@@ -12,6 +12,30 @@ from thormang_isaacgym_amd.abi import TG_PROP_DAMPING, TG_PROP_DRIVE_MODE, TG_PR
 pytestmark = pytest.mark.gpu
 
 
+def jit_walker():
+    """A URDF that is not compiled into libtgsim.so (run-time load_asset /
+    tg_model_jit test): a box torso with two legs, hips driven, one knee
+    locked, sphere feet and a box body shape."""
+    from thormang_isaacgym_amd.model.kat_models import _inertial, urdf_model
+    from thormang_isaacgym_amd.model.urdf import Shape
+    eye = np.eye(3).tolist()
+    legs = ""
+    for side, y in (("l", 0.12), ("r", -0.12)):
+        legs += (f'<link name="{side}_thigh">{_inertial(0.8, (0, 0, -0.15), (0.006, 0.006, 0.001))}</link>'
+                 f'<link name="{side}_shin">{_inertial(0.5, (0, 0, -0.12), (0.003, 0.003, 0.0005))}</link>'
+                 f'<joint name="{side}_hip" type="revolute"><parent link="torso"/><child link="{side}_thigh"/>'
+                 f'<origin xyz="0 {y} -0.1" rpy="0.05 0 0"/><axis xyz="0 1 0"/>'
+                 '<limit lower="-1.2" upper="1.2" effort="80" velocity="10"/></joint>'
+                 f'<joint name="{side}_knee" type="revolute"><parent link="{side}_thigh"/><child link="{side}_shin"/>'
+                 '<origin xyz="0 0 -0.3"/><axis xyz="0 1 0"/>'
+                 '<limit lower="-0.5" upper="1.5" effort="80" velocity="10"/></joint>')
+    shapes = [Shape("box", "torso", [0, 0, 0], eye, [0.12, 0.18, 0.1], 0.9),
+              Shape("sphere", "l_shin", [0, 0, -0.26], eye, [0.04], 1.0),
+              Shape("sphere", "r_shin", [0, 0, -0.26], eye, [0.04], 1.0)]
+    return urdf_model("jit_walker", f'<link name="torso">{_inertial(4.0, (0, 0, 0.02), (0.05, 0.04, 0.03))}</link>'
+                      + legs, shapes, locked=["r_knee"])
+
+
 def gpu_sim(model, sp, n, root, dof, props, pt, vt):
     from thormang_isaacgym_amd.sim import Sim
     s = Sim(model, sp, n, "cuda:0")
@@ -172,3 +196,85 @@ def test_gpu_rigid_body_force_tensors_match_oracle(name, space):
     torch.cuda.synchronize()
     ref_t = oracle_wrench(m, root, dof, np.zeros_like(f), t, space, ms)
     np.testing.assert_allclose(s.body_force.cpu().numpy(), ref_t, atol=2e-5 * scale, rtol=1e-4)
+
+
+def test_gpu_runtime_loaded_model_matches_oracle():
+    """gym.load_asset of a URDF that is not compiled in: Sim compiles its
+    kernels at run time (tg_model_jit, hipRTC) and the GPU trajectory -- a
+    hanging two-legged body, hips and a knee on PD drives, the other knee
+    locked, joint limits -- matches the oracle over 150 steps."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs the MI355X")
+    from thormang_isaacgym_amd import abi
+    from thormang_isaacgym_amd.sim import compiled_model_hashes
+    m = jit_walker()
+    assert abi.ModelDesc(m).hash not in compiled_model_hashes()
+    dl = m.dof_name_to_id()
+
+    def setup(rs, root, dof, props, pt, vt):
+        n = root.shape[0]
+        root[:, 2] = 1.0
+        for j in ("l_hip", "r_hip", "l_knee"):
+            d = dl[j]
+            props[TG_PROP_DRIVE_MODE, :, d] = 1
+            props[TG_PROP_STIFFNESS, :, d] = 60.0
+            props[TG_PROP_DAMPING, :, d] = 4.0
+            props[TG_PROP_EFFORT, :, d] = 30.0
+            pt[:, d] = rs.uniform(-1.0, 1.0, n)
+        k = dl["r_knee"]
+        props[4, :, k] = 0.3            # lock window [0.3, 0.3 + 1e-4]
+        props[5, :, k] = 0.3001
+        dof.reshape(n, -1, 2)[:, k, 0] = 0.30005
+        dof.reshape(n, -1, 2)[:, dl["r_hip"], 1] = rs.normal(0, 2, n)
+
+    worst, g, *_ = side_by_side(m, 150, n=32, setup=setup, dt=0.01, substeps=2, fix_base_link=True)
+    assert g.jit, "expected a run-time specialisation"
+    assert worst < 2e-3, worst
+
+
+@pytest.mark.parametrize("name", ["kat_box", "thormang"])
+def test_gpu_runtime_specialisation_equals_compiled(name):
+    """The run-time (hipRTC) specialisation of a compiled-in model, registered
+    under another hash, against the compiled-in kernels on identical inputs:
+    the box exercises the contact rows / PGS, the Thormang tree 16 lanes per
+    env and ~150 KB of dynamic LDS through hipModuleLaunchKernel."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs the MI355X")
+    from thormang_isaacgym_amd.sim import Sim, load_model
+    m = load_model(name)
+    n = 64
+    kw = dict(dt=0.01, substeps=2) if name == "kat_box" else dict(dt=1 / 60, substeps=2, fix_base_link=True)
+    desc, sp, root, dof, props, pt, vt = pm.sim(m, n=n, **kw)
+    rs = np.random.default_rng(4)
+    if name == "kat_box":
+        root[:, 2] = rs.uniform(0.06, 0.3, n)
+        root[:, 7:9] = rs.normal(0, 0.8, (n, 2))
+        root[:, 10:13] = rs.normal(0, 2.0, (n, 3))
+    else:
+        root[:, 2] = 1.2
+        dof[:, 0] = rs.uniform(-0.3, 0.3, dof.shape[0])
+    sims = []
+    for jh in (None, 0x7E57_0000_0000_0000 | (abi_hash(m) & 0xFFFF_FFFF)):
+        s = Sim(m, sp, n, "cuda:0", jit_hash=jh)
+        s.root_state.copy_(torch.from_numpy(root))
+        s.dof_state.copy_(torch.from_numpy(dof))
+        s.dof_props.copy_(torch.from_numpy(props))
+        s.env_dirty.fill_(1)
+        sims.append(s)
+    assert not sims[0].jit and sims[1].jit
+    for _ in range(60):
+        for s in sims:
+            s.simulate()
+    torch.cuda.synchronize()
+    for k in ("root_state", "dof_state"):
+        a, b = getattr(sims[0], k), getattr(sims[1], k)
+        if a.numel() == 0:   # the box has no dofs
+            continue
+        assert torch.isfinite(a).all()
+        d = float((a - b).abs().max())
+        assert d <= 1e-5, (k, d)
+
+
+def abi_hash(m):
+    from thormang_isaacgym_amd import abi
+    return abi.ModelDesc(m).hash

@@ -45,6 +45,7 @@ SIGNATURES = {
     "tg_set_kernel_timing": [_VP, C.c_int32],
     "tg_read_kernel_timing": [_VP, C.POINTER(C.c_double), C.POINTER(C.c_int64)],
     "tg_compiled_model_hashes": [C.POINTER(C.c_uint64), C.c_int32],
+    "tg_model_jit": [C.c_uint64, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p],
     "tg_gogoro_step": [_VP, C.POINTER(abi.tg_gogoro_params), C.POINTER(abi.tg_gogoro_buffers), _VP, C.c_int32,
                        C.c_uint64, C.c_uint64],
     "tg_gogoro_pre_physics": [_VP, C.POINTER(abi.tg_gogoro_params), C.POINTER(abi.tg_gogoro_buffers), _VP, _VP,

@@ -33,6 +33,8 @@ UNITS = {
     "walk_task.hip": ["-O3", "-ffp-contract=off"],
     "gogoro_paper_task.hip": ["-O3", "-ffp-contract=off"],
     "tgsim_api.cpp": ["-O2", "-x", "hip"],
+    # run-time specialisations (hipRTC) of the articulation kernels
+    "jit.cpp": ["-O2", "-x", "hip"],
 }
 
 
@@ -66,7 +68,7 @@ def build(verbose: bool = False, jobs: int = 4) -> str:
         if verbose and out:
             print(out.decode(errors="replace")[-3000:])
     if procs or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB]
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB, "-lhiprtc", "-ldl"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")

@@ -1,0 +1,908 @@
+// articulation_kernels.h -- the model-generic kernel templates of the
+// articulation step (compose, step_par_kernel with its task epilogues, link
+// states, rigid-body force reduction).  Included by articulation.hip, which
+// instantiates them for the models compiled into libtgsim.so, and compiled at
+// run time by hipRTC (jit.cpp) for a model loaded from a URDF that is not
+// compiled in.  See articulation.hip for the algorithm overview.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+
+#include "../../include/tgsim.h"
+#include "gogoro_math.h"
+#include "tg_math.h"
+#include "tg_kernels.h"
+
+namespace tg {
+
+// per-env composite cache layout (SoA, [KC][N])
+// Per-env composite cache, env-major ([N][KC] floats): group g's block of 24
+// floats (joint placement R (9) + t (3), then mass, com (3), inertia about the
+// com (6), 2 pad) at 24 g, then 12 floats (R, t) per contact shape.  A lane
+// takes a group's 22 inputs with 6 16-byte loads from one base address.
+template <class M> struct CompLayout {
+    static constexpr int GB = 24;
+    static constexpr int xtree(int g) { return GB * g; }
+    static constexpr int inertia(int g) { return GB * g + 12; }
+    static constexpr int shape(int s) { return GB * M::NG + 12 * s; }
+    static_assert(M::KC == GB * M::NG + 12 * M::NS, "codegen KC");
+};
+
+__device__ __forceinline__ float prop(const StepArgs &a, int f, int e, int d) {
+    return a.props[((size_t)f * a.N + e) * a.D + d];
+}
+
+// ---------------------------------------------------------------- compose
+// Per-env group composites from the locked joint positions (centre of each
+// lock window) and the per-link mass scale (domain randomisation).  One
+// wavefront per env (envs that are not dirty exit at once): link poses in
+// their group-root frame level by level (lane = link), per-link mass terms in
+// parallel, then lane g sums group g's links in link order (deterministic, the
+// order of oracle/physics_ref.c) and writes the group's cache rows.
+#ifdef TG_SECTION_PROF
+__device__ unsigned long long tg_cprof_acc[8];   // compose sections, lane 0 of every composed env
+#define TG_CPROF_INIT unsigned long long tg_c0 = clock64();
+#define TG_CPROF(k)                                                              \
+    {                                                                            \
+        const unsigned long long t1 = clock64();                                \
+        if (threadIdx.x % 64 == 0) atomicAdd(&tg_cprof_acc[k], t1 - tg_c0);      \
+        tg_c0 = t1;                                                              \
+    }
+#else
+#define TG_CPROF_INIT
+#define TG_CPROF(k)
+#endif
+
+// groups with more links than this are summed by wave reductions (lane = link)
+constexpr int COMPOSE_SERIAL_MAX = 8;
+template <class M> constexpr int max_small_group() {
+    int m = 0;
+    for (int g = 0; g < M::NG; ++g)
+        if (M::group_nlinks[g] <= COMPOSE_SERIAL_MAX && M::group_nlinks[g] > m) m = M::group_nlinks[g];
+    return m;
+}
+template <int NV> __device__ __forceinline__ void wave_sum_n(float *v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[k] += __shfl_xor(v[k], m, 64);
+}
+
+// COMPOSE_WPB wavefronts per workgroup, one env each: a launch over all envs
+// is N / COMPOSE_WPB workgroups (most waves exit at once), not N
+constexpr int COMPOSE_WPB = 8;
+
+// Prologue (tg_walk_step): the walk task's pre_physics_step fused into the
+// compose launch that precedes every step kernel -- the same fp32 operations
+// as walk_task.hip walk_pre_kernel (no contraction: default + scale * a).
+__device__ __forceinline__ void target_prologue(const StepArgs &a, int e, int lane) {
+#pragma clang fp contract(off)
+    if (lane >= a.D) return;
+    const unsigned i = (unsigned)e * (unsigned)a.D + (unsigned)lane;
+    const float x = a.pm_actions[i];
+    const float c = x < -a.pm_clip ? -a.pm_clip : (x > a.pm_clip ? a.pm_clip : x);
+    a.pm_act_out[i] = c;
+    a.pm_tgt_out[i] = a.pm_default[lane] + a.pm_scale * c;
+}
+
+// Prologue (tg_gogoro_step): gogoro_task.hip pre_kernel for env e on one lane
+// -- the same fp32 operations (no contraction / reassociation here either)
+// and the same Philox draw.
+__device__ __forceinline__ void gogoro_pre_prologue(const GogoroPre &g, int e, int D) {
+#pragma clang fp contract(off) reassociate(off)
+    const float x = g.actions[e];
+    const float a = x < -g.clip_actions ? -g.clip_actions : (x > g.clip_actions ? g.clip_actions : x);
+    float *ah = g.action_history + 5 * (size_t)e;
+    const float h0 = ah[1], h1 = ah[2], h2 = ah[3], h3 = ah[4];
+    ah[0] = h0; ah[1] = h1; ah[2] = h2; ah[3] = h3; ah[4] = a;
+    const float m = g.max_steering_change, ms = g.max_steering;
+    float da = a * m;
+    da = da < -m ? -m : (da > m ? m : da);
+    float c = g.curent_command[e] + da;
+    c = c < -ms ? -ms : (c > ms ? ms : c);
+    g.curent_command[e] = c;
+    const U4 u = philox(U4{(uint32_t)e, g.c_lo, g.c_hi, 0x50524531u}, g.k0, g.k1);
+    const float noise = g.noise_mean + gauss(u.x, u.y) * g.noise_std;
+    g.pos_target[(size_t)e * D + g.dof_steer] = c + g.steer_offsets[e] + noise;
+    g.vel_target[(size_t)e * D + g.dof_rear] = g.curent_speed[e];
+}
+
+template <class M> __global__ __launch_bounds__(64 * COMPOSE_WPB) void compose_kernel(StepArgs a) {
+    const int wv = threadIdx.x / 64;
+    const int e = blockIdx.x * COMPOSE_WPB + wv;
+    const bool dirty = e < a.N && a.dirty[e] != 0;   // read before the prologue: one memory latency
+    if (a.pm_actions && e < a.N) target_prologue(a, e, threadIdx.x % 64);
+    if (a.gp.actions && e < a.N && threadIdx.x % 64 == 0) gogoro_pre_prologue(a.gp, e, a.D);
+    if (!dirty) return;
+    TG_CPROF_INIT
+    using CL = CompLayout<M>;
+    static_assert(M::NL <= 64 && M::NG <= 64 && M::NS <= 64, "compose: one lane per link / group / shape");
+    __shared__ float Ts[COMPOSE_WPB][M::NL][12];    // link pose in its group-root frame: R (9), p (3)
+    __shared__ float LMs[COMPOSE_WPB][M::NL + 1][10];   // link mass, com (group frame), inertia about com; row NL = 0
+    __shared__ int GLs[COMPOSE_WPB][M::NG][M::MAXGL];   // group links, padded with NL (the zero row): branch-free sums
+    float(&T)[M::NL][12] = Ts[wv];
+    float(&LM)[M::NL + 1][10] = LMs[wv];
+    int(&GL)[M::NG][M::MAXGL] = GLs[wv];
+    const int lane = threadIdx.x % 64;
+    auto wsync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    auto ldT = [&](int l, M3 &R, V3 &P) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) R.a[k] = T[l][k];
+        P = v3(T[l][9], T[l][10], T[l][11]);
+    };
+    auto ld9 = [](const float *o) { return M3{{o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7], o[8]}}; };
+    // ---- every model constant and per-env input this lane needs, loaded up
+    // front as one batch (the level loop below then runs on LDS only while
+    // the group / shape loads are still in flight)
+    for (int i = lane; i < M::NG * M::MAXGL; i += 64) {
+        const int k = M::group_links[i / M::MAXGL][i % M::MAXGL];
+        GL[i / M::MAXGL][i % M::MAXGL] = k < 0 ? M::NL : k;
+    }
+    if (lane < 10) LM[M::NL][lane] = 0.f;
+    const int l = lane;                      // lane = link
+    const bool lact = l < M::NL;
+    M3 Rl = eye3();
+    V3 tl = v3(0, 0, 0);
+    int lev = -1, par = 0;
+    float msc = 1.f, lin[10];
+    if (lact) {
+        lev = M::link_level[l];
+        par = M::link_parent[l];
+#pragma unroll
+        for (int k = 0; k < 10; ++k) lin[k] = M::link_inertia[l][k];
+        if (lev > 0) {
+            const float *o = M::link_origin[l];
+            Rl = ld9(o);
+            tl = v3(o[9], o[10], o[11]);
+            const int d = M::link_dof[l];
+            if (d >= 0) {
+                const float lo = prop(a, TG_PROP_LOWER, e, d), hi = prop(a, TG_PROP_UPPER, e, d);
+                const float q = 0.5f * (lo + hi);
+                // a locked joint is rigid at its window centre: a wider window
+                // (props set as if the joint were free) is reported by tg_sync
+                if (a.err && !(hi - lo <= TG_LOCK_WINDOW_MAX)) atomicOr(a.err, 1);
+                const float *ax = M::link_axis[l];
+                if (M::link_jtype[l] == TG_JOINT_REVOLUTE) Rl = mul(Rl, rot_axis(ax[0], ax[1], ax[2], q));
+                else if (M::link_jtype[l] == TG_JOINT_PRISMATIC) tl = tl + q * mul(Rl, v3(ax[0], ax[1], ax[2]));
+            }
+        }
+        if (a.mass_scale) msc = a.mass_scale[(size_t)e * M::NL + l];
+    }
+    const int g = lane;                      // lane = group
+    const bool gact = g < M::NG;
+    int gnl = 0, gpl = 0;
+    M3 Qg = eye3(), Qp = eye3(), Rgo = eye3();
+    V3 tgo = v3(0, 0, 0);
+    if (gact) {
+        gnl = M::group_nlinks[g];
+        Qg = ld9(M::gq[g]);
+        if (g > 0) {
+            Qp = ld9(M::gq[M::parent[g]]);
+            const int r = M::group_root[g];
+            gpl = M::link_parent[r];
+            Rgo = ld9(M::link_origin[r]);
+            tgo = v3(M::link_origin[r][9], M::link_origin[r][10], M::link_origin[r][11]);
+        }
+    }
+    const int sh = lane;                     // lane = shape
+    const bool sact = sh < M::NS;
+    int sl = 0;
+    M3 Qs = eye3(), Rso = eye3();
+    V3 tso = v3(0, 0, 0);
+    if (sact) {
+        sl = M::shape_link[sh];
+        Qs = ld9(M::gq[M::shape_group[sh]]);
+        Rso = ld9(M::shape_pose[sh]);
+        tso = v3(M::shape_pose[sh][9], M::shape_pose[sh][10], M::shape_pose[sh][11]);
+    }
+    TG_CPROF(0)
+    // ---- link poses in their group-root frame, level by level (LDS only)
+    M3 R = eye3();
+    V3 P = v3(0, 0, 0);
+    for (int lv = 0; lv <= M::NLEV; ++lv) {
+        if (lev == lv) {
+            if (lv > 0) {
+                M3 Rp;
+                V3 Pp;
+                ldT(par, Rp, Pp);
+                R = mul(Rp, Rl);
+                P = Pp + mul(Rp, tl);
+            }
+#pragma unroll
+            for (int k = 0; k < 9; ++k) T[l][k] = R.a[k];
+            T[l][9] = P.x; T[l][10] = P.y; T[l][11] = P.z;
+        }
+        wsync();
+    }
+    if (lact) {   // per-link mass terms
+        const float s = msc;
+        const V3 cg = mul(R, v3(lin[1], lin[2], lin[3])) + P;
+        const M3 Il{{lin[4] * s, lin[7] * s, lin[8] * s, lin[7] * s, lin[5] * s, lin[9] * s, lin[8] * s, lin[9] * s,
+                     lin[6] * s}};
+        const M3 RI = mul(mul(R, Il), transpose(R));
+        LM[l][0] = lin[0] * s;
+        LM[l][1] = cg.x; LM[l][2] = cg.y; LM[l][3] = cg.z;
+        LM[l][4] = RI.a[0]; LM[l][5] = RI.a[4]; LM[l][6] = RI.a[8];
+        LM[l][7] = RI.a[1]; LM[l][8] = RI.a[2]; LM[l][9] = RI.a[5];
+    }
+    wsync();
+    TG_CPROF(1)
+    // ---- group sums in link order (deterministic, the order of
+    // oracle/physics_ref.c), written to the cache in joint-aligned group
+    // frames (axis e_z, codegen gq): v' = Q^T v, I' = Q^T I Q, placements
+    // R' = Q_p^T R Q_g, t' = Q_p^T t
+    float *c = a.comp + (size_t)e * M::KC;
+    // large groups (the scooter's root group holds the locked rider: 55 links)
+    // by wave reductions over lane = link, in tree order; the others by their
+    // own lane in link order
+    float bm = 0.f, bI[6] = {0, 0, 0, 0, 0, 0};
+    V3 bc = v3(0, 0, 0);
+#pragma unroll
+    for (int gb = 0; gb < M::NG; ++gb) {
+        if constexpr (M::MAXGL > COMPOSE_SERIAL_MAX) {
+            if (M::group_nlinks[gb] <= COMPOSE_SERIAL_MAX) continue;
+            const bool mine = lact && M::link_group[l] == gb;
+            float v4[4] = {0.f, 0.f, 0.f, 0.f};
+            if (mine) { v4[0] = LM[l][0]; v4[1] = LM[l][0] * LM[l][1]; v4[2] = LM[l][0] * LM[l][2]; v4[3] = LM[l][0] * LM[l][3]; }
+            wave_sum_n<4>(v4);
+            const float im = v4[0] > 0.f ? 1.0f / v4[0] : 0.f;
+            const V3 gcb = v3(v4[1] * im, v4[2] * im, v4[3] * im);
+            float v6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            if (mine) {
+                const float ml = LM[l][0];
+                const V3 dd = v3(LM[l][1], LM[l][2], LM[l][3]) - gcb;
+                const float d2 = dot(dd, dd);
+                v6[0] = LM[l][4] + ml * (d2 - dd.x * dd.x);
+                v6[1] = LM[l][5] + ml * (d2 - dd.y * dd.y);
+                v6[2] = LM[l][6] + ml * (d2 - dd.z * dd.z);
+                v6[3] = LM[l][7] - ml * dd.x * dd.y;
+                v6[4] = LM[l][8] - ml * dd.x * dd.z;
+                v6[5] = LM[l][9] - ml * dd.y * dd.z;
+            }
+            wave_sum_n<6>(v6);
+            if (lane == gb) {
+                bm = v4[0];
+                bc = gcb;
+#pragma unroll
+                for (int k = 0; k < 6; ++k) bI[k] = v6[k];
+            }
+        }
+    }
+    if (gact) {
+        float gm = 0.f;
+        V3 gc = v3(0, 0, 0);
+        float gI[6] = {0, 0, 0, 0, 0, 0};
+        constexpr int SM = max_small_group<M>();
+        if (gnl > COMPOSE_SERIAL_MAX) {
+            gm = bm;
+            gc = bc;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) gI[k] = bI[k];
+        } else {
+#pragma unroll
+            for (int i = 0; i < SM; ++i) {   // unrolled and branch-free (padding = the zero row)
+                const int k = GL[g][i];
+                gm += LM[k][0];
+                gc = gc + LM[k][0] * v3(LM[k][1], LM[k][2], LM[k][3]);
+            }
+            gc = (gm > 0.f ? 1.0f / gm : 0.f) * gc;
+#pragma unroll
+            for (int i = 0; i < SM; ++i) {
+                const int k = GL[g][i];
+                const float ml = LM[k][0];
+                const V3 dd = v3(LM[k][1], LM[k][2], LM[k][3]) - gc;
+                const float d2 = dot(dd, dd);
+                gI[0] += LM[k][4] + ml * (d2 - dd.x * dd.x);
+                gI[1] += LM[k][5] + ml * (d2 - dd.y * dd.y);
+                gI[2] += LM[k][6] + ml * (d2 - dd.z * dd.z);
+                gI[3] += LM[k][7] - ml * dd.x * dd.y;
+                gI[4] += LM[k][8] - ml * dd.x * dd.z;
+                gI[5] += LM[k][9] - ml * dd.y * dd.z;
+            }
+        }
+        const V3 gcq = mulT(Qg, gc);
+        float gIq[6];
+        sym_from(gIq, mul(mul(transpose(Qg), sym_to(gI)), Qg));
+        float *ci = c + CL::inertia(g);
+        ci[0] = gm;
+        ci[1] = gcq.x; ci[2] = gcq.y; ci[3] = gcq.z;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) ci[4 + k] = gIq[k];
+        ci[10] = 0.f;
+        ci[11] = 0.f;
+        if (g > 0) {
+            M3 Rp;
+            V3 Pp;
+            ldT(gpl, Rp, Pp);
+            const M3 Rx = mul(mul(transpose(Qp), mul(Rp, Rgo)), Qg);
+            const V3 t = mulT(Qp, Pp + mul(Rp, tgo));
+            float *cx = c + CL::xtree(g);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) cx[k] = Rx.a[k];
+            cx[9] = t.x; cx[10] = t.y; cx[11] = t.z;
+        }
+    }
+    TG_CPROF(2)
+    if (sact) {   // shape poses in their group frame
+        M3 Rsl;
+        V3 Psl;
+        ldT(sl, Rsl, Psl);
+        const M3 Rx = mul(transpose(Qs), mul(Rsl, Rso));
+        const V3 t = mulT(Qs, Psl + mul(Rsl, tso));
+        float *cs = c + CL::shape(sh);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) cs[k] = Rx.a[k];
+        cs[9] = t.x; cs[10] = t.y; cs[11] = t.z;
+    }
+    if (lane == 0) a.dirty[e] = 0;
+    TG_CPROF(3)
+}
+
+// ---------------------------------------------------------------- rigid-body states
+// World state of every link (acquire/refresh_rigid_body_state_tensor): one
+// wavefront per env, links level by level (lane = link): R_l = R_p Ro Rj(q),
+// p_l = p_p + R_p (to + q s), w_l = w_p + qd R_p Ro a (revolute),
+// v_l = v_p + w_p x (p_l - p_p) + qd R_p Ro a (prismatic), v_l at the link
+// origin; out[e][l] = (p_l, quat(R_l) xyzw, v_l + w_l x R_l c_l, w_l).
+// The same function as oracle/physics_ref.c oracle_rigid_body_states.
+__device__ __forceinline__ void m3_to_quat(const M3 &R, float &x, float &y, float &z, float &w) {
+    const float m00 = R.a[0], m11 = R.a[4], m22 = R.a[8], tr = m00 + m11 + m22;
+    if (tr > 0.f) {
+        const float s = 0.5f / sqrtf(tr + 1.f);
+        w = 0.25f / s; x = (R.a[7] - R.a[5]) * s; y = (R.a[2] - R.a[6]) * s; z = (R.a[3] - R.a[1]) * s;
+    } else if (m00 > m11 && m00 > m22) {
+        const float s = 2.f * sqrtf(1.f + m00 - m11 - m22);
+        w = (R.a[7] - R.a[5]) / s; x = 0.25f * s; y = (R.a[1] + R.a[3]) / s; z = (R.a[2] + R.a[6]) / s;
+    } else if (m11 > m22) {
+        const float s = 2.f * sqrtf(1.f + m11 - m00 - m22);
+        w = (R.a[2] - R.a[6]) / s; x = (R.a[1] + R.a[3]) / s; y = 0.25f * s; z = (R.a[5] + R.a[7]) / s;
+    } else {
+        const float s = 2.f * sqrtf(1.f + m22 - m00 - m11);
+        w = (R.a[3] - R.a[1]) / s; x = (R.a[2] + R.a[6]) / s; y = (R.a[5] + R.a[7]) / s; z = 0.25f * s;
+    }
+}
+
+template <class M> __global__ __launch_bounds__(64) void body_state_kernel(const float *root, const float *dof, int n,
+                                                                           float *out) {
+    const int e = blockIdx.x;
+    if (e >= n) return;
+    __shared__ float T[M::NL][18];   // R (9), p (3), w (3), v at the origin (3)
+    const int lane = threadIdx.x;
+    const float *r = root + 13 * (size_t)e;
+    const float *q = dof + 2 * (size_t)e * M::ND;
+    auto wsync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    for (int lev = 0; lev <= M::NDEPTH; ++lev) {
+        for (int l = lane; l < M::NL; l += 64) {
+            if (M::link_depth[l] != lev) continue;
+            M3 R;
+            V3 P, W, V;
+            if (M::link_parent[l] < 0) {
+                float qx = r[3], qy = r[4], qz = r[5], qw = r[6];
+                const float in = rsqrtf(qx * qx + qy * qy + qz * qz + qw * qw);
+                R = quat_to_m3(qx * in, qy * in, qz * in, qw * in);
+                P = v3(r[0], r[1], r[2]);
+                W = v3(r[10], r[11], r[12]);
+                const V3 c = v3(M::link_inertia[l][1], M::link_inertia[l][2], M::link_inertia[l][3]);
+                V = v3(r[7], r[8], r[9]) - cross(W, mul(R, c));   // root state: velocity of the root link's com
+            } else {
+                const int pl = M::link_parent[l];
+                M3 Rp;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) Rp.a[k] = T[pl][k];
+                const V3 Pp = v3(T[pl][9], T[pl][10], T[pl][11]);
+                const V3 Wp = v3(T[pl][12], T[pl][13], T[pl][14]), Vp = v3(T[pl][15], T[pl][16], T[pl][17]);
+                const float *o = M::link_origin[l];
+                M3 Ro{{o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7], o[8]}};
+                V3 to = v3(o[9], o[10], o[11]);
+                const int d = M::link_dof[l];
+                const float qq = d >= 0 ? q[2 * d] : 0.f, qd = d >= 0 ? q[2 * d + 1] : 0.f;
+                const float *ax = M::link_axis[l];
+                const V3 axw = mul(Rp, mul(Ro, v3(ax[0], ax[1], ax[2])));   // joint axis, world
+                W = Wp;
+                if (M::link_jtype[l] == TG_JOINT_REVOLUTE) {
+                    Ro = mul(Ro, rot_axis(ax[0], ax[1], ax[2], qq));
+                    W = W + qd * axw;
+                } else if (M::link_jtype[l] == TG_JOINT_PRISMATIC) {
+                    to = to + qq * mul(Ro, v3(ax[0], ax[1], ax[2]));
+                }
+                R = mul(Rp, Ro);
+                P = Pp + mul(Rp, to);
+                V = Vp + cross(Wp, P - Pp);
+                if (M::link_jtype[l] == TG_JOINT_PRISMATIC) V = V + qd * axw;
+            }
+#pragma unroll
+            for (int k = 0; k < 9; ++k) T[l][k] = R.a[k];
+            T[l][9] = P.x; T[l][10] = P.y; T[l][11] = P.z;
+            T[l][12] = W.x; T[l][13] = W.y; T[l][14] = W.z;
+            T[l][15] = V.x; T[l][16] = V.y; T[l][17] = V.z;
+        }
+        wsync();
+    }
+    for (int l = lane; l < M::NL; l += 64) {
+        M3 R;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) R.a[k] = T[l][k];
+        const V3 W = v3(T[l][12], T[l][13], T[l][14]);
+        const V3 c = v3(M::link_inertia[l][1], M::link_inertia[l][2], M::link_inertia[l][3]);
+        const V3 vc = v3(T[l][15], T[l][16], T[l][17]) + cross(W, mul(R, c));
+        float qx, qy, qz, qw;
+        m3_to_quat(R, qx, qy, qz, qw);
+        float *o = out + ((size_t)e * M::NL + l) * 13;
+        o[0] = T[l][9]; o[1] = T[l][10]; o[2] = T[l][11];
+        o[3] = qx; o[4] = qy; o[5] = qz; o[6] = qw;
+        o[7] = vc.x; o[8] = vc.y; o[9] = vc.z;
+        o[10] = W.x; o[11] = W.y; o[12] = W.z;
+    }
+}
+
+// ---------------------------------------------------------------- rigid-body forces
+// apply_rigid_body_force_tensors (reference call site
+// tasks/gogoro_realistic_turning_sim_paper.py:457): per-link forces [N*L,3] at
+// the link coms and optional torques [N*L,3], world (space 0) or link frame
+// (space 1), reduced to the step kernel's group wrenches [N,G,6] (world force,
+// torque about the group com): F_g = sum f_l, T_g = sum t_l + (p_l - c_g) x f_l,
+// c_g the mass-weighted (per-env mass scale) com of the group's links.  One
+// wavefront per env: link poses level by level (lane = link), then lane = group
+// sums its links in link order.  The same function as oracle/physics_ref.c
+// oracle_rigid_body_force_wrench.
+template <class M> __global__ __launch_bounds__(64) void rb_force_kernel(const float *root, const float *dof, int n,
+                                                                         const float *mass_scale, const float *forces,
+                                                                         const float *torques, int space, float *out) {
+    const int e = blockIdx.x;
+    if (e >= n) return;
+    __shared__ float T[M::NL][12];    // R (9), p (3); then com (3), mass, f (3), t (3) per link
+    __shared__ float F[M::NL][10];
+    const int lane = threadIdx.x;
+    const float *r = root + 13 * (size_t)e;
+    const float *q = dof + 2 * (size_t)e * M::ND;
+    auto wsync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    for (int lev = 0; lev <= M::NDEPTH; ++lev) {
+        for (int l = lane; l < M::NL; l += 64) {
+            if (M::link_depth[l] != lev) continue;
+            M3 R;
+            V3 P;
+            if (M::link_parent[l] < 0) {
+                float qx = r[3], qy = r[4], qz = r[5], qw = r[6];
+                const float in = rsqrtf(qx * qx + qy * qy + qz * qz + qw * qw);
+                R = quat_to_m3(qx * in, qy * in, qz * in, qw * in);
+                P = v3(r[0], r[1], r[2]);
+            } else {
+                const int pl = M::link_parent[l];
+                M3 Rp;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) Rp.a[k] = T[pl][k];
+                const V3 Pp = v3(T[pl][9], T[pl][10], T[pl][11]);
+                const float *o = M::link_origin[l];
+                M3 Ro{{o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7], o[8]}};
+                V3 to = v3(o[9], o[10], o[11]);
+                const int d = M::link_dof[l];
+                const float qq = d >= 0 ? q[2 * d] : 0.f;
+                const float *ax = M::link_axis[l];
+                if (M::link_jtype[l] == TG_JOINT_REVOLUTE) Ro = mul(Ro, rot_axis(ax[0], ax[1], ax[2], qq));
+                else if (M::link_jtype[l] == TG_JOINT_PRISMATIC) to = to + qq * mul(Ro, v3(ax[0], ax[1], ax[2]));
+                R = mul(Rp, Ro);
+                P = Pp + mul(Rp, to);
+            }
+#pragma unroll
+            for (int k = 0; k < 9; ++k) T[l][k] = R.a[k];
+            T[l][9] = P.x; T[l][10] = P.y; T[l][11] = P.z;
+        }
+        wsync();
+    }
+    for (int l = lane; l < M::NL; l += 64) {
+        M3 R;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) R.a[k] = T[l][k];
+        const V3 pc = v3(T[l][9], T[l][10], T[l][11]) +
+                      mul(R, v3(M::link_inertia[l][1], M::link_inertia[l][2], M::link_inertia[l][3]));
+        const size_t i = (size_t)e * M::NL + l;
+        V3 f = v3(forces[3 * i], forces[3 * i + 1], forces[3 * i + 2]);
+        V3 t = torques ? v3(torques[3 * i], torques[3 * i + 1], torques[3 * i + 2]) : v3(0, 0, 0);
+        if (space == 1) {
+            f = mul(R, f);
+            t = mul(R, t);
+        }
+        F[l][0] = pc.x; F[l][1] = pc.y; F[l][2] = pc.z;
+        F[l][3] = M::link_inertia[l][0] * (mass_scale ? mass_scale[i] : 1.f);
+        F[l][4] = f.x; F[l][5] = f.y; F[l][6] = f.z;
+        F[l][7] = t.x; F[l][8] = t.y; F[l][9] = t.z;
+    }
+    wsync();
+    for (int g = lane; g < M::NG; g += 64) {
+        float gm = 0.f;
+        V3 gc = v3(0, 0, 0);
+        for (int k = 0; k < M::group_nlinks[g]; ++k) {
+            const int l = M::group_links[g][k];
+            gm += F[l][3];
+            gc = gc + F[l][3] * v3(F[l][0], F[l][1], F[l][2]);
+        }
+        const int rl = M::group_links[g][0];
+        gc = gm > 0.f ? (1.0f / gm) * gc : v3(T[rl][9], T[rl][10], T[rl][11]);
+        V3 fs = v3(0, 0, 0), ts = v3(0, 0, 0);
+        for (int k = 0; k < M::group_nlinks[g]; ++k) {
+            const int l = M::group_links[g][k];
+            const V3 f = v3(F[l][4], F[l][5], F[l][6]);
+            fs = fs + f;
+            ts = ts + v3(F[l][7], F[l][8], F[l][9]) + cross(v3(F[l][0], F[l][1], F[l][2]) - gc, f);
+        }
+        float *o = out + ((size_t)e * M::NG + g) * 6;
+        o[0] = fs.x; o[1] = fs.y; o[2] = fs.z;
+        o[3] = ts.x; o[4] = ts.y; o[5] = ts.z;
+    }
+}
+
+// ---------------------------------------------------------------- contact row layout
+// rows of shape s: shape_nrows[s] normal rows, then friction t1, t2 and torsion
+template <class M> __device__ __forceinline__ constexpr int row_shape(int i) {
+    int base = 0;
+    for (int s = 0; s < M::NS; ++s) {
+        if (i < base + M::shape_nrows[s] + 3) return s;
+        base += M::shape_nrows[s] + 3;
+    }
+    return 0;
+}
+template <class M> __device__ __forceinline__ constexpr int row_base(int s) {
+    int base = 0;
+    for (int k = 0; k < s; ++k) base += M::shape_nrows[k] + 3;
+    return base;
+}
+
+}  // namespace tg
+
+#include "step_par.h"
+
+namespace tg {
+
+// ---------------------------------------------------------------- fused walk post-physics
+// tg_walk_step's last simulate: the ThormangWalk post-physics step
+// (walk_task.hip walk_post_kernel: progress, masked resets, observations,
+// reward, termination, timeouts, pushes) as the step kernel's epilogue, LPE
+// lanes per env (lane = dof mod LPE) on the final state the kernel holds, so
+// the state is stored once (reset values for a reset env) and the separate
+// launch disappears.  Same operations as walk_env; the fp contraction and
+// reassociation are off here as in walk_task.hip, the transcendentals are this
+// translation unit's (fast-math) ones.
+struct WalkPost {
+    static constexpr bool on = true;
+    using Args = WalkPostArgs;
+    static __device__ __forceinline__ float clampw(float x, float lo, float hi) {
+        return x < lo ? lo : (x > hi ? hi : x);
+    }
+    template <class M, int LPE>
+    static __device__ __forceinline__ void epilogue(const Args &pa, const StepArgs &a, const LE &s, int e, bool owner,
+                                                    int sub, const float *rt0, float *root, float *dofs) {
+#pragma clang fp contract(off) reassociate(off)
+        constexpr int D = M::ND;
+        constexpr int NR = (D + LPE - 1) / LPE;
+        const tg_walk_params &p = pa.p;
+        const tg_walk_buffers &b = pa.b;
+        const uint32_t c_lo = pa.c_lo, c_hi = pa.c_hi;
+        const bool lead = sub == 0;
+        const size_t eD = (size_t)e * D;
+        // every input of the env in one batch
+        const int64_t prog1 = b.progress_buf[e] + 1;
+        const bool reset = b.reset_buf[e] != 0;
+        float q[NR], qd[NR], act[NR], la[NR], pt[NR], cmd[3], rt[13];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const int d = sub + LPE * r;
+            q[r] = qd[r] = act[r] = la[r] = pt[r] = 0.f;
+            if (d < D) {
+                const int g = DofGroup<M>::tab.g[d];
+                if (g > 0) {
+                    q[r] = s(g * GF + F_Q);
+                    qd[r] = s(g * GF + F_QD);
+                } else {
+                    q[r] = 0.5f * (prop(a, TG_PROP_LOWER, e, d) + prop(a, TG_PROP_UPPER, e, d));
+                }
+                act[r] = b.actions[eD + d];
+                la[r] = b.last_actions[eD + d];
+                pt[r] = b.pos_target[eD + d];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) cmd[k] = b.commands[3 * (size_t)e + k];
+#pragma unroll
+        for (int k = 0; k < 13; ++k) rt[k] = rt0[k];
+        const int64_t prog = reset ? 0 : prog1;
+        if (reset) {
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const int d = sub + LPE * r;
+                if (d < D) {
+                    q[r] = p.default_pos[d] +
+                           (walk_draw(p, pa.reset_draws, e, 4 + d, c_lo, c_hi) * 2.0f - 1.0f) * p.joint_noise;
+                    qd[r] = 0.1f * (walk_draw(p, pa.reset_draws, e, 4 + D + d, c_lo, c_hi) * 2.0f - 1.0f);
+                    act[r] = la[r] = 0.f;
+                    if (owner) b.actions[eD + d] = 0.f;
+                }
+            }
+            if (lead) {
+                float r4[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) r4[k] = walk_draw(p, pa.reset_draws, e, k, c_lo, c_hi);
+                cmd[0] = p.cmd_vx[0] + r4[0] * (p.cmd_vx[1] - p.cmd_vx[0]);
+                cmd[1] = p.cmd_vy[0] + r4[1] * (p.cmd_vy[1] - p.cmd_vy[0]);
+                cmd[2] = p.cmd_wz[0] + r4[2] * (p.cmd_wz[1] - p.cmd_wz[0]);
+                const float yaw = (r4[3] * 2.0f - 1.0f) * 3.14159265358979323846f;
+                const float *tpl = b.root_reset + 13 * (size_t)e;
+                rt[0] = tpl[0];
+                rt[1] = tpl[1];
+                rt[2] = p.spawn_height;
+                rt[3] = 0.0f;
+                rt[4] = 0.0f;
+                rt[5] = sinf(0.5f * yaw);
+                rt[6] = cosf(0.5f * yaw);
+#pragma unroll
+                for (int k = 7; k < 13; ++k) rt[k] = 0.0f;
+                if (owner) {
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) b.commands[3 * (size_t)e + k] = cmd[k];
+                }
+            }
+        }
+        // dof observations and the per-dof reward terms
+        float *o = b.obs_buf + (size_t)p.num_obs * e;
+        const float co = p.clip_obs;
+        float rate = 0.0f, vel2 = 0.0f, tq = 0.0f;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const int d = sub + LPE * r;
+            if (d < D) {
+                if (owner) {
+                    o[13 + d] = clampw((q[r] - p.default_pos[d]) * p.dof_pos_scale, -co, co);
+                    o[13 + D + d] = clampw(qd[r] * p.dof_vel_scale, -co, co);
+                    o[13 + 2 * D + d] = clampw(act[r], -co, co);
+                    b.last_actions[eD + d] = act[r];
+                }
+                rate += (act[r] - la[r]) * (act[r] - la[r]);
+                vel2 += qd[r] * qd[r];
+                const float tt = p.stiffness[d] * (pt[r] - q[r]);
+                tq += tt * tt;
+            }
+        }
+        rate = sum_lanes<LPE>(rate);
+        vel2 = sum_lanes<LPE>(vel2);
+        tq = sum_lanes<LPE>(tq);
+        if (owner) {
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const int d = sub + LPE * r;
+                if (d < D) {
+                    dofs[2 * d] = q[r];
+                    dofs[2 * d + 1] = qd[r];
+                }
+            }
+        }
+        if (!lead || !owner) return;
+#pragma unroll
+        for (int k = 0; k < 13; ++k) root[k] = rt[k];
+        b.progress_buf[e] = prog;
+        const float x = rt[3], y = rt[4], z = rt[5], w = rt[6];
+        const float Rw[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w),
+                             2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w),
+                             2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)};
+        float vb[3], wb[3], gb[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            vb[k] = Rw[k] * rt[7] + Rw[3 + k] * rt[8] + Rw[6 + k] * rt[9];
+            wb[k] = Rw[k] * rt[10] + Rw[3 + k] * rt[11] + Rw[6 + k] * rt[12];
+            gb[k] = -Rw[6 + k];
+        }
+        o[0] = clampw(rt[2], -co, co);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            o[1 + k] = clampw(vb[k] * p.lin_vel_scale, -co, co);
+            o[4 + k] = clampw(wb[k] * p.ang_vel_scale, -co, co);
+            o[7 + k] = clampw(gb[k], -co, co);
+        }
+        o[10] = clampw(cmd[0] * p.lin_vel_scale, -co, co);
+        o[11] = clampw(cmd[1] * p.lin_vel_scale, -co, co);
+        o[12] = clampw(cmd[2] * p.ang_vel_scale, -co, co);
+        const float lin_err = (cmd[0] - vb[0]) * (cmd[0] - vb[0]) + (cmd[1] - vb[1]) * (cmd[1] - vb[1]);
+        const float ang_err = (cmd[2] - wb[2]) * (cmd[2] - wb[2]);
+        const float dz = rt[2] - p.target_height;
+        float rew = p.rew_lin_vel_xy * expf(-lin_err / 0.25f) + p.rew_ang_vel_z * expf(-ang_err / 0.25f) +
+                    p.rew_upright * (-gb[2]) + p.rew_alive + p.rew_height * expf(-dz * dz / 0.01f) +
+                    p.rew_action_rate * rate + p.rew_dof_vel * vel2 + p.rew_torque * tq;
+        const bool fall = (rt[2] < p.termination_height) || (-gb[2] < p.termination_up);
+        if (fall) rew += p.rew_termination;
+        const bool rs = fall || prog >= p.max_episode_length - 1;
+        b.rew_buf[e] = rew;
+        b.reset_buf[e] = rs ? 1 : 0;
+        b.timeout_buf[e] = (prog >= p.max_episode_length - 1) && rs;
+        if (!b.body_force) return;
+        // push wrench for the next simulate (walk_post_kernel)
+        float *f = b.body_force + (size_t)6 * p.num_groups * e;
+        const bool push = p.push_force > 0.0f && p.push_interval > 0 && prog > 0 && (prog % p.push_interval) == 0;
+        float u[3];
+        if (pa.push_draws) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) u[k] = pa.push_draws[3 * (size_t)e + k];
+        } else {
+            const U4 xx = philox(U4{(uint32_t)e, c_lo, c_hi, 0x50555348u}, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+            u[0] = u01(xx.x); u[1] = u01(xx.y); u[2] = u01(xx.z);
+        }
+        f[0] = push ? p.push_force * (u[0] * 2.0f - 1.0f) : 0.0f;
+        f[1] = push ? p.push_force * (u[1] * 2.0f - 1.0f) : 0.0f;
+        f[2] = push ? 0.25f * p.push_force * (u[2] * 2.0f - 1.0f) : 0.0f;
+        f[3] = 0.0f; f[4] = 0.0f; f[5] = 0.0f;
+    }
+};
+
+// ---------------------------------------------------------------- fused Gogoro post-physics
+// tg_gogoro_step's last simulate: gogoro_task.hip post_kernel (progress,
+// masked resets with their property writes and dirty flag, observations,
+// reward, sensor noise, command resampling, timeouts) as the step kernel's
+// epilogue, LPE lanes per env on the final state it holds: the 9 Philox
+// blocks run on the env's lanes at once (lane l block l, the lead lane also
+// block 8) and reach the lead lane by DPP row broadcasts; a reset env's dof
+// rows are written by all its lanes; the lead lane does the task math.  The
+// state is stored once (the reset state for a reset env), and the separate
+// post launch and its re-read of the state disappear.  Same counters, draws
+// and fp32 operations (gogoro_math.h) as post_kernel.
+struct GogoroPost {
+    static constexpr bool on = true;
+    using Args = GogoroPostArgs;
+    template <class M, int LPE>
+    static __device__ __forceinline__ void epilogue(const Args &pa, const StepArgs &a, const LE &s, int e, bool owner,
+                                                    int sub, const float *rt0, float *root, float *dofs) {
+#pragma clang fp contract(off) reassociate(off)
+        constexpr int D = M::ND;
+        constexpr int NR = (D + LPE - 1) / LPE;
+        static_assert(LPE >= 8, "the 9 draw blocks need 8 lanes per env");
+        const tg_gogoro_params &p = pa.p;
+        const tg_gogoro_buffers &b = pa.b;
+        const bool lead = sub == 0;
+        const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
+        // ---- inputs, one batch
+        const int64_t prog1 = b.progress_buf[e] + 1;
+        const bool rflag = b.reset_buf[e] != 0;
+        float rt[13], ah[5];
+#pragma unroll
+        for (int k = 0; k < 13; ++k) rt[k] = rt0[k];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) ah[k] = b.action_history[5 * (size_t)e + k];
+        float yawc = b.yaw_command[e], cmdc = b.curent_command[e], imu = b.imu_offsets[e];
+        // ---- draws: lane l < 8 block l, the lead lane also block 8 (command resample)
+        float v[3], v8[3];
+        gogoro_post_block(sub < 8 ? sub : 7, e, pa.c_lo, pa.c_hi, k0, k1, v);
+        gogoro_post_block(8, e, pa.c_lo, pa.c_hi, k0, k1, v8);
+        auto slot = [&](int x) {   // exchange slot x = 3 l + j of block l, from lane l
+            const int l = x / 3, j = x % 3;
+            return env_bcast<LPE>(j == 0 ? v[0] : (j == 1 ? v[1] : v[2]), l, sub);
+        };
+        float r[TG_GOGORO_RESET_DRAWS], nd[5];
+#pragma unroll
+        for (int k = 0; k < TG_GOGORO_RESET_DRAWS; ++k) r[k] = slot(GOGORO_RSLOT[k]);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) nd[k] = slot(GOGORO_NSLOT[k]);
+        const float su = v8[0], yu = v8[1];
+        int64_t prog = prog1;
+        if (rflag) {
+            // reset_env: dof rows (every lane), the rest on the lead lane
+            if (owner) {
+#pragma unroll
+                for (int rr = 0; rr < NR; ++rr) {
+                    const int d = sub + LPE * rr;
+                    if (d < D) {
+                        dofs[2 * d] = b.thormang_pose[d];
+                        dofs[2 * d + 1] = 0.0f;
+                    }
+                }
+            }
+            const float target = (r[3] * 2.0f - 1.0f) * F_PI;
+            const float rot = target + u_aff(-1.57f, 1.57f, r[4]);
+            const float hh = rot / 2.0f;
+            const float *tpl = b.root_reset + 13 * (size_t)e;
+            rt[0] = tpl[0];
+            rt[1] = tpl[1];
+            rt[2] = p.terrain_spawn ? tpl[2] : p.spawn_z;
+            rt[3] = 0.0f;
+            rt[4] = 0.0f;
+            rt[5] = sinf(hh);
+            rt[6] = cosf(hh);
+#pragma unroll
+            for (int k = 7; k < 13; ++k) rt[k] = 0.0f;
+            float cv[5];
+            cv[0] = n_aff(p.seat_offset_x_range, r[5]);
+            cv[1] = n_aff(p.seat_offset_y_range, r[6]);
+            cv[2] = n_aff(p.seat_offset_z_range, r[7]);
+            cv[3] = n_aff(p.seat_offset_xr_range, r[8]);
+            cv[4] = n_aff(p.steering_offset, r[9]);
+            imu = cv[3];
+            yawc = target;
+            cmdc = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) ah[k] = 0.0f;
+            if (owner && lead) {
+                b.curent_speed[e] = u_aff(p.speed_range[0], p.speed_range[1], r[0]);
+                b.speed_offset[e] = u_aff(p.speed_sensor_offset[0], p.speed_sensor_offset[1], r[2]);
+#pragma unroll
+                for (int k = 0; k < 5; ++k) b.config_vector[5 * (size_t)e + k] = cv[k];
+                const size_t ND = (size_t)p.num_envs * D;
+                float *prop = b.dof_props + (size_t)e * D;
+                const int seat[3] = {p.dof_base_x, p.dof_base_y, p.dof_base_z};
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    prop[TG_PROP_DRIVE_MODE * ND + seat[k]] = 0.0f;
+                    prop[TG_PROP_LOWER * ND + seat[k]] = cv[k];
+                    prop[TG_PROP_UPPER * ND + seat[k]] = cv[k] + 0.0001f;
+                }
+                b.imu_offsets[e] = cv[3];
+                b.steer_offsets[e] = cv[4];
+                const int st = p.dof_steer;
+                prop[TG_PROP_DRIVE_MODE * ND + st] = 1.0f;
+                prop[TG_PROP_STIFFNESS * ND + st] = p.steer_stiffness;
+                prop[TG_PROP_DAMPING * ND + st] =
+                    u_aff(p.steering_damping_range[0], p.steering_damping_range[1], r[10]);
+                prop[TG_PROP_EFFORT * ND + st] = p.steer_effort;
+                prop[TG_PROP_VELOCITY * ND + st] = p.steer_velocity;
+                b.env_dirty[e] = 1;
+                b.curent_command[e] = 0.0f;
+#pragma unroll
+                for (int k = 0; k < 5; ++k) b.action_history[5 * (size_t)e + k] = 0.0f;
+            }
+            prog = 0;
+        } else if (owner) {
+            // the simulated state: active dofs from LDS, locked ones at their window centre
+#pragma unroll
+            for (int rr = 0; rr < NR; ++rr) {
+                const int d = sub + LPE * rr;
+                if (d < D) {
+                    const int g = DofGroup<M>::tab.g[d];
+                    if (g > 0) {
+                        dofs[2 * d] = s(g * GF + F_Q);
+                        dofs[2 * d + 1] = s(g * GF + F_QD);
+                    } else {
+                        dofs[2 * d] = 0.5f * (prop(a, TG_PROP_LOWER, e, d) + prop(a, TG_PROP_UPPER, e, d));
+                        dofs[2 * d + 1] = 0.f;
+                    }
+                }
+            }
+        }
+        if (!lead || !owner) return;
+#pragma unroll
+        for (int k = 0; k < 13; ++k) root[k] = rt[k];
+        float o[6];
+        observation(rt, yawc, cmdc, o);
+        bool felt;
+        const float rew = gogoro_reward(o, ah, felt);
+        const bool finished = prog >= p.max_episode_length - 1;
+        const int64_t reset = (finished || felt) ? 1 : 0;
+        float rr[6];
+        noisy_observation(p, o, nd, imu, rr);
+        float yc = yawc;
+        if (prog == p.yaw_freq_update) yc = u_aff(-F_PI, F_PI, yu);
+        if (yc > F_PI) yc = yc - F_2PI;
+        if (yc < -F_PI) yc = yc + F_2PI;
+        b.progress_buf[e] = prog;
+        float *bo = b.buffer_obs + 6 * (size_t)e;
+        float *ob = b.obs_buf + 6 * (size_t)e;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            bo[k] = o[k];
+            ob[k] = t_clamp(rr[k], -p.clip_obs, p.clip_obs);
+        }
+        b.rew_buf[e] = felt ? -100.0f : rew;
+        b.reset_buf[e] = reset;
+        if (prog == p.speed_freq_update) b.curent_speed[e] = u_aff(p.speed_range[0], p.speed_range[1], su);
+        b.yaw_command[e] = yc;
+        b.timeout_buf[e] = (prog >= p.max_episode_length - 1) && (reset != 0);
+    }
+};
+
+}  // namespace tg

@@ -6,7 +6,9 @@
 // compute_gogoro_reward; :474-601 reset_idx draws).
 #pragma once
 #include <hip/hip_runtime.h>
+#ifndef __HIPCC_RTC__   // hipRTC (jit.cpp) provides the device math itself
 #include <math.h>
+#endif
 
 #include "tg_kernels.h"
 

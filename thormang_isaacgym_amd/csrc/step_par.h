@@ -57,6 +57,12 @@ __device__ unsigned long long tg_prof_acc[24];   // [16..]: sub-sections (see sc
 #define TG_PROF(k)
 #endif
 
+// a compile-time int argument (std::integral_constant without <type_traits>,
+// which a hipRTC unit, jit.cpp, does not have)
+template <int N> struct IntC {
+    static constexpr int value = N;
+};
+
 // one env's LDS state
 struct LE {
     float *b;
@@ -789,9 +795,9 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                     }
                 };
                 const int smax = d_smax(dc);
-                if (smax == 1) gather2(std::integral_constant<int, 1>{});
-                else if (smax == 2) gather2(std::integral_constant<int, 2>{});
-                else if (smax >= 3) gather2(std::integral_constant<int, 3>{});
+                if (smax == 1) gather2(IntC<1>{});
+                else if (smax == 2) gather2(IntC<2>{});
+                else if (smax >= 3) gather2(IntC<3>{});
                 // the half's orientation of B
                 float Y[9];
                 Y[0] = Bm[0]; Y[4] = Bm[4]; Y[8] = Bm[8];
@@ -853,9 +859,9 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                 const SV cb = ldsv(s, o + F_V);
                 const float c0 = s(o + F_DINV), tau = s(o + F_UU), al = s(o + F_QDS), c1 = s(o + F_C1);
                 const int smax = d_smax(dc);
-                if (smax == 1) gather(std::integral_constant<int, 1>{}, dc, IA, pA);
-                else if (smax == 2) gather(std::integral_constant<int, 2>{}, dc, IA, pA);
-                else if (smax >= 3) gather(std::integral_constant<int, 3>{}, dc, IA, pA);
+                if (smax == 1) gather(IntC<1>{}, dc, IA, pA);
+                else if (smax == 2) gather(IntC<2>{}, dc, IA, pA);
+                else if (smax >= 3) gather(IntC<3>{}, dc, IA, pA);
                 const SV U = mul(IA, Sg);
                 const float D0 = dot(Sg, U);   // without the armature (folded into c0, tau)
                 const float Dinv = 1.0f / (c1 * D0 + c0);

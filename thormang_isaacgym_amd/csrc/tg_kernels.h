@@ -3,6 +3,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#ifndef __HIPCC_RTC__
+#include <string>
+#endif
 
 #include "../../include/tg_gogoro.h"
 #include "../../include/tg_gogoro_paper.h"
@@ -69,6 +72,7 @@ struct GogoroPostArgs {
     tg_gogoro_buffers b;
     uint32_t c_lo, c_hi;
 };
+#ifndef __HIPCC_RTC__   // host launchers (not part of a hipRTC unit, jit.cpp)
 // compose + step kernel with the Gogoro post-physics fused in; returns 1 when
 // the model has no such instantiation
 int launch_step_gogoro(uint64_t hash, const StepArgs &a, const GogoroPostArgs &pa, hipStream_t stream,
@@ -81,13 +85,23 @@ int launch_step_walk(uint64_t hash, const StepArgs &a, const WalkPostArgs &pa, h
 // ev_begin / ev_end (optional) are recorded around the step kernel itself
 int launch_step(uint64_t hash, const StepArgs &a, hipStream_t stream, hipEvent_t ev_begin = nullptr,
                 hipEvent_t ev_end = nullptr);
-int launch_compose(uint64_t hash, const StepArgs &a, hipStream_t stream);
 int compiled_hashes(uint64_t *out, int cap);
 int launch_body_states(uint64_t hash, const float *root, const float *dof, int n, float *out, hipStream_t stream);
 // per-link forces / torques [N*L,3] -> group wrenches [N,G,6] (rb_force_kernel)
 int launch_rb_forces(uint64_t hash, const float *root, const float *dof, int n, const float *mass_scale,
                      const float *forces, const float *torques, int space, float *out, hipStream_t stream);
 int model_kc(uint64_t hash);
+
+// run-time compiled models (jit.cpp, tg_model_jit): the launchers above fall
+// through to these when no compiled-in specialisation matches the hash
+int jit_compile(uint64_t hash, const char *struct_name, const char *model_source, const char *include_dir,
+                const char *cache_dir, std::string &err);
+bool jit_has(uint64_t hash);
+int jit_kc(uint64_t hash);
+int jit_launch_step(uint64_t hash, const StepArgs &a, hipStream_t stream, hipEvent_t ev_begin, hipEvent_t ev_end);
+int jit_launch_body_states(uint64_t hash, const float *root, const float *dof, int n, float *out, hipStream_t stream);
+int jit_launch_rb_forces(uint64_t hash, const float *root, const float *dof, int n, const float *mass_scale,
+                         const float *forces, const float *torques, int space, float *out, hipStream_t stream);
 
 int launch_gogoro_pre(const tg_gogoro_params &p, const tg_gogoro_buffers &b, const float *actions,
                       const float *pre_draws, uint64_t counter, hipStream_t stream);
@@ -116,6 +130,8 @@ int launch_scatter_field(float *dst, const float *src, const int32_t *ids, int n
 int launch_mark_dirty(uint8_t *dirty, const int32_t *ids, int n, hipStream_t stream);
 // tg_rng_fill test hook (gogoro_task.hip): n Philox blocks, counter (i, c_lo, c_hi, 0)
 int launch_rng_fill(int kind, uint64_t seed, uint64_t counter, float *out, int n, hipStream_t stream);
+
+#endif   // __HIPCC_RTC__
 
 // ---------------------------------------------------------------- Philox4x32-10
 struct U4 {

@@ -145,6 +145,16 @@ const char *tg_last_error(void) { return g_err.c_str(); }
 
 uint64_t tg_compiled_model_hashes(uint64_t *out, int32_t cap) { return (uint64_t)tg::compiled_hashes(out, cap); }
 
+int tg_model_jit(uint64_t model_hash, const char *struct_name, const char *model_source, const char *include_dir,
+                 const char *cache_dir) {
+    if (!struct_name || !model_source) return fail(TG_ERR_ARG, "tg_model_jit: null argument");
+    if (tg::model_kc(model_hash) >= 0 && !tg::jit_has(model_hash)) return TG_OK;   // compiled in
+    std::string err;
+    if (int rc = tg::jit_compile(model_hash, struct_name, model_source, include_dir, cache_dir, err))
+        return fail(rc, "tg_model_jit(0x%016llx): %s", (unsigned long long)model_hash, err.c_str());
+    return TG_OK;
+}
+
 int tg_sim_create(const tg_model_desc *m, const tg_sim_params *params, int32_t num_envs, int32_t device,
                   tg_sim **out) {
     if (!m || !params || !out) return fail(TG_ERR_ARG, "tg_sim_create: null argument");
@@ -155,8 +165,8 @@ int tg_sim_create(const tg_model_desc *m, const tg_sim_params *params, int32_t n
     int kc = tg::model_kc(m->model_hash);
     if (kc < 0)
         return fail(TG_ERR_MODEL,
-                    "model hash 0x%016llx has no compiled specialisation in libtgsim.so "
-                    "(rebuild with the model's JSON under thormang_isaacgym_amd/model/compiled/)",
+                    "model hash 0x%016llx has no specialisation in libtgsim.so: compiled-in models are listed by "
+                    "tg_compiled_model_hashes; any other model must first be compiled with tg_model_jit",
                     (unsigned long long)m->model_hash);
     int ndev = 0;
     HIPCHK(hipGetDeviceCount(&ndev));

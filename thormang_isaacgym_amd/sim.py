@@ -33,12 +33,63 @@ def load_model(name: str) -> Model:
         return Model.from_json(f.read())
 
 
+def load_asset(path: str, name: str | None = None, locked=(), extra_shapes=(), mesh_root: str | None = None,
+               shape_friction: dict | None = None) -> Model:
+    """gym.load_asset of a URDF at run time (the reference: tasks/gogoro_new.py:198-213):
+    parse the file, merge fixed and ``locked`` joints into rigid groups.  A
+    ``Sim`` over a model that is not compiled into libtgsim.so compiles its
+    kernels on first use (``ensure_specialisation``), so any URDF runs without
+    a library rebuild."""
+    from .model.urdf import load_urdf
+    m = load_urdf(path, name or os.path.splitext(os.path.basename(path))[0], mesh_root=mesh_root,
+                  extra_shapes=list(extra_shapes), shape_friction=shape_friction)
+    m.build_groups(list(locked))
+    return m
+
+
+def jit_cache_dir() -> str:
+    """Where run-time specialisations are cached (TG_JIT_CACHE, default
+    ~/.cache/thormang_isaacgym_amd/jit)."""
+    d = os.environ.get("TG_JIT_CACHE") or os.path.join(os.path.expanduser("~"), ".cache", "thormang_isaacgym_amd",
+                                                        "jit")
+    os.makedirs(d, exist_ok=True)
+    return d
+
+
+def compiled_model_hashes() -> set:
+    n = int(lib().tg_compiled_model_hashes(None, 0))
+    arr = (C.c_uint64 * max(n, 1))()
+    lib().tg_compiled_model_hashes(arr, n)
+    return {int(arr[i]) for i in range(n)}
+
+
+def ensure_specialisation(model: Model, desc: abi.ModelDesc | None = None) -> bool:
+    """Make sure libtgsim can step ``model``: a no-op for a compiled-in model;
+    otherwise the model's constexpr tables (model/codegen.py) are compiled by
+    hipRTC for gfx950 inside the library (tg_model_jit, cached on disk by hash)
+    and registered.  Returns True when a run-time specialisation is used."""
+    from .model import codegen
+    desc = desc or abi.ModelDesc(model)
+    if desc.hash in compiled_model_hashes():
+        return False
+    cname = "Model_jit_%016x" % desc.hash
+    src = codegen.emit(model, cname)
+    check(lib().tg_model_jit(C.c_uint64(desc.hash), cname.encode(), src.encode(), None, jit_cache_dir().encode()),
+          "tg_model_jit (run-time load_asset)")
+    return True
+
+
 def _ptr(t: torch.Tensor | None):
     return None if t is None else C.c_void_p(t.data_ptr())
 
 
 class Sim:
-    def __init__(self, model: Model, params: abi.tg_sim_params, num_envs: int, device: str = "cuda:0"):
+    def __init__(self, model: Model, params: abi.tg_sim_params, num_envs: int, device: str = "cuda:0",
+                 jit_hash: int | None = None):
+        """``jit_hash`` (test hook): register the model under this hash instead
+        of its own, so even a compiled-in model runs on a run-time
+        (tg_model_jit) specialisation -- the JIT path can then be compared
+        with the compiled one on identical inputs."""
         if not device.startswith("cuda"):
             raise RuntimeError(f"libtgsim runs on an MI355X ('cuda:N' device), got {device!r}; "
                                "there is no CPU physics path outside the test oracle")
@@ -46,9 +97,13 @@ class Sim:
         self.model = model
         self.num_envs = N = int(num_envs)
         self.desc = abi.ModelDesc(model)
+        if jit_hash is not None:
+            self.desc.hash = int(jit_hash)
+            self.desc.desc.model_hash = int(jit_hash)
         self.params = params
         self.D, self.G, self.L, self.S = model.num_dof, model.num_groups, model.num_bodies, len(model.shapes)
         torch.cuda.set_device(self.device)
+        self.jit = ensure_specialisation(model, self.desc)
         h = C.c_void_p()
         check(lib().tg_sim_create(C.byref(self.desc.desc), C.byref(params), N, self.device.index or 0, C.byref(h)),
               "tg_sim_create")
