@@ -157,3 +157,36 @@ def test_gpu_gogoro_fused_step_matches_separate_calls():
             assert d <= 1e-4, (what, d)
         n_reset += int(f.reset_buf.sum())
     assert n_reset > 0
+
+
+def test_gpu_cpu_pipeline_config_1_delivers_the_gpu_results_on_the_host():
+    """BASELINE config 1 (reference: Gogoro, 64 envs, sim_device=cpu,
+    rl_device=cpu, pipeline=cpu): the env simulates on the GPU (there is no
+    CPU physics outside the oracle) and hands obs / rew / reset / time_outs to
+    the learner on the CPU -- the same values, bit for bit, as the GPU
+    pipeline with the same seed."""
+    _cuda()
+    import thormang_isaacgym_amd as tia
+    from thormang_isaacgym_amd.cfg import load_task_cfg
+    outs = []
+    for sim_dev, rl_dev, gpu_pipe in (("cpu", "cpu", False), ("cuda:0", "cuda:0", True)):
+        cfg = load_task_cfg("Gogoro", num_envs=64)
+        cfg["sim"]["use_gpu_pipeline"] = gpu_pipe
+        if not gpu_pipe:
+            with pytest.warns(UserWarning, match="CPU pipeline"):
+                env = tia.make(seed=7, task="Gogoro", num_envs=64, sim_device=sim_dev, rl_device=rl_dev, cfg=cfg)
+        else:
+            env = tia.make(seed=7, task="Gogoro", num_envs=64, sim_device=sim_dev, rl_device=rl_dev, cfg=cfg)
+        g = torch.Generator().manual_seed(99)
+        rec = []
+        for _ in range(40):
+            a = torch.rand(64, 1, generator=g) * 2 - 1
+            obs, rew, reset, extras = env.step(a.to(rl_dev))
+            assert obs["obs"].device == torch.device(rl_dev) and rew.device == torch.device(rl_dev)
+            assert reset.device == torch.device(rl_dev) and extras["time_outs"].device == torch.device(rl_dev)
+            rec.append([x.detach().cpu().clone() for x in (obs["obs"], rew, reset, extras["time_outs"])])
+        outs.append(rec)
+        del env
+    for a, b in zip(*outs):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)

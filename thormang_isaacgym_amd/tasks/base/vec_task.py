@@ -20,7 +20,8 @@ semantics, cfg keys) so ``train.py`` + rl_games drive it unchanged:
   (parity unpinned).
 
 Viewer/rendering is out of scope: ``headless=False`` runs
-headless with a warning.
+headless with a warning.  The CPU pipeline runs its physics on the GPU and
+delivers the step tensors on rl_device (``pipeline_device``).
 """
 from __future__ import annotations
 
@@ -58,19 +59,33 @@ def _space(low, high):
         return _Box(low, high)
 
 
+def pipeline_device(config: Dict[str, Any], sim_device: str) -> str:
+    """The GPU the env state and kernels live on.  The reference's GPU pipeline
+    (vec_task.py:66-74: sim_device 'cuda:N', use_gpu_pipeline) maps to cuda:N.
+    Its CPU pipeline (BASELINE config 1: sim_device=cpu, pipeline=cpu) has no
+    CPU physics here -- libtgsim simulates on an MI355X -- so the env runs on
+    cuda:N (N from sim_device, else 0) and VecTask delivers the step tensors
+    on rl_device; without a GPU this raises (the CPU engine under oracle/ is
+    test infrastructure, never a fallback)."""
+    dev_type, _, idx = sim_device.partition(":")
+    gpu_pipeline = bool(config["sim"].get("use_gpu_pipeline", True)) and dev_type.lower() in ("cuda", "gpu")
+    if not gpu_pipeline:
+        if not torch.cuda.is_available():
+            raise RuntimeError("the CPU pipeline runs its physics on an MI355X (libtgsim has no CPU engine) "
+                               "and no GPU is visible")
+        warnings.warn(f"CPU pipeline requested (sim_device={sim_device!r}, use_gpu_pipeline="
+                      f"{config['sim'].get('use_gpu_pipeline', True)}): physics and task kernels run on "
+                      f"cuda:{int(idx) if idx else 0}, step tensors are delivered on rl_device")
+    return f"cuda:{int(idx) if idx else 0}"
+
+
 class Env(abc.ABC):
     def __init__(self, config: Dict[str, Any], rl_device: str, sim_device: str, graphics_device_id: int,
                  headless: bool):
         split_device = sim_device.split(":")
         self.device_type = split_device[0]
         self.device_id = int(split_device[1]) if len(split_device) > 1 else 0
-        self.device = "cpu"
-        if config["sim"].get("use_gpu_pipeline", True):
-            if self.device_type.lower() in ("cuda", "gpu"):
-                self.device = "cuda" + ":" + str(self.device_id)
-            else:
-                print("GPU Pipeline can only be used with GPU simulation. Forcing CPU Pipeline.")
-                config["sim"]["use_gpu_pipeline"] = False
+        self.device = pipeline_device(config, sim_device)
         self.rl_device = rl_device
         self.headless = headless
         enable_camera_sensors = config.get("enableCameraSensors", False)
@@ -149,9 +164,6 @@ class VecTask(Env):
         self.force_render = force_render
         if not headless:
             warnings.warn("thormang_isaacgym_amd has no viewer; running headless")
-        if self.device == "cpu":
-            raise RuntimeError("the CPU pipeline is not provided: libtgsim simulates on an MI355X "
-                               "(sim_device='cuda:N', pipeline='gpu'); the CPU engine exists only as the test oracle")
         if self.cfg.get("physics_engine", "physx") not in ("physx", "flex"):
             raise ValueError(f"Invalid physics engine backend: {self.cfg['physics_engine']}")
         self.sim_params = self._parse_sim_params(self.cfg.get("physics_engine", "physx"), self.cfg["sim"])
@@ -234,6 +246,16 @@ class VecTask(Env):
         if self.num_states > 0:
             self.obs_dict["states"] = self.get_state()
         return self.obs_dict, self.rew_buf.to(self.rl_device), self.reset_buf.to(self.rl_device), self.extras
+
+    def _rl_out(self):
+        """The step's return tuple on rl_device: the live buffers when rl_device
+        is the sim GPU (no copy), copies when it is not (the CPU pipeline)."""
+        if torch.device(self.rl_device) == torch.device(self.device):
+            return self.obs_dict, self.rew_buf, self.reset_buf, self.extras
+        obs = {k: v.to(self.rl_device) for k, v in self.obs_dict.items()}
+        extras = dict(self.extras)
+        extras["time_outs"] = self.extras["time_outs"].to(self.rl_device)
+        return obs, self.rew_buf.to(self.rl_device), self.reset_buf.to(self.rl_device), extras
 
     def zero_actions(self) -> torch.Tensor:
         return torch.zeros([self.num_envs, self.num_actions], dtype=torch.float32, device=self.rl_device)

@@ -33,7 +33,7 @@ import torch
 from .. import abi
 from .._lib import check, lib
 from ..sim import load_model
-from .base.vec_task import VecTask
+from .base.vec_task import VecTask, pipeline_device
 from .gogoro_cfg import ASSET_OPTIONS, check_lock_set, gogoro_params, initial_dof_props, thormang_pose
 from .gogoro_draws import post_draws, reset_draws
 from .terrain import Terrain
@@ -56,7 +56,7 @@ class Gogoro(VecTask):
         if not INCREMENTAL_STEER:
             raise NotImplementedError("only the registered INCREMENTAL_STEER=True behaviour is fused")
         self.curent_step = 0
-        self.device = rl_device
+        self.device = pipeline_device(cfg, sim_device)   # the sim GPU (also for the CPU pipeline)
         self.n_envs = cfg["env"]["numEnvs"]
         self.max_episode_length = torch.tensor(cfg["env"]["max_steps"])
         self.randomization_params = cfg["task"]["randomization_params"]
@@ -78,7 +78,7 @@ class Gogoro(VecTask):
         self.steering_offset = nz["steering_offset"]
         self.speed_sensor_offset = nz["speed_sensor_offset"]
         n = self.n_envs
-        dev = rl_device
+        dev = self.device
         self.imu_offsets = torch.zeros(n, device=dev)
         self.steer_offsets = torch.zeros(n, device=dev)
         self.curent_speed_offset = torch.zeros(n, device=dev)
@@ -104,8 +104,6 @@ class Gogoro(VecTask):
         super().__init__(config=self.cfg, rl_device=rl_device, sim_device=sim_device,
                          graphics_device_id=graphics_device_id, headless=headless,
                          virtual_screen_capture=virtual_screen_capture, force_render=force_render)
-        if torch.device(rl_device) != torch.device(self.device):
-            raise RuntimeError("rl_device must be the simulation GPU (the task state lives in its HBM)")
         self.dt = self.sim_params["dt"]
         self.root_tensor = self.sim.root_state
         self.state_dof = self.sim.dof_state
@@ -265,7 +263,7 @@ class Gogoro(VecTask):
         self.obs_dict["obs"] = self.obs_buf
         if self.num_states > 0:
             self.obs_dict["states"] = self.get_state()
-        return self.obs_dict, self.rew_buf, self.reset_buf, self.extras
+        return self._rl_out()
 
     # ------------------------------------------------------------ resets / draws
     def get_randoms(self, shape, bounds):

@@ -39,7 +39,7 @@ from .._lib import check, lib
 from ..abi import (TG_PROP_ARMATURE, TG_PROP_DAMPING, TG_PROP_DRIVE_MODE, TG_PROP_EFFORT, TG_PROP_LOWER,
                    TG_PROP_STIFFNESS, TG_PROP_UPPER, TG_PROP_VELOCITY, default_dof_props)
 from ..sim import load_model
-from .base.vec_task import VecTask
+from .base.vec_task import VecTask, pipeline_device
 from .gogoro_cfg import check_lock_set, lock_window
 from .paper_draws import ctor_draws, post_draws, reset_draws
 
@@ -164,7 +164,7 @@ class Gogoro(VecTask):
             raise NotImplementedError("terrain (paper.py:171-187) is SURVEY §8 f3, not part of this build")
         self.steering_sensitivity = 0.1
         self.curent_step = 0
-        self.device = rl_device
+        self.device = pipeline_device(cfg, sim_device)   # the sim GPU (also for the CPU pipeline)
         self.n_envs = n = cfg["env"]["numEnvs"]
         self.max_episode_length = torch.tensor(cfg["env"]["max_steps"])
         nz = cfg["noises"]
@@ -174,7 +174,7 @@ class Gogoro(VecTask):
                   "speed_freq_update", "yaw_freq_update", "steering_offset", "command_delay"):
             setattr(self, k, nz[k])
         self.dof_props = None
-        dev = rl_device
+        dev = self.device
         self.yaw_command = torch.zeros(n, device=dev)
         self.min_speed, self.max_speed, self.max_steering = 0.0, 10.0, 0.5
         self.draw_source = getattr(self, "draw_source", None)
@@ -213,8 +213,6 @@ class Gogoro(VecTask):
         super().__init__(config=self.cfg, rl_device=rl_device, sim_device=sim_device,
                          graphics_device_id=graphics_device_id, headless=headless,
                          virtual_screen_capture=virtual_screen_capture, force_render=force_render)
-        if torch.device(rl_device) != torch.device(self.device):
-            raise RuntimeError("rl_device must be the simulation GPU (the task state lives in its HBM)")
         self.dt = self.sim_params["dt"]
         self.root_tensor = self.sim.root_state
         self.state_dof = self.sim.dof_state
@@ -328,7 +326,7 @@ class Gogoro(VecTask):
         self.extras["time_outs"] = self.timeout_buf
         self.obs_dict["obs"] = torch.clamp(self.obs_buf, -self.clip_obs, self.clip_obs) \
             if math.isfinite(self.clip_obs) else self.obs_buf
-        return self.obs_dict, self.rew_buf, self.reset_buf, self.extras
+        return self._rl_out()
 
     # ------------------------------------------------------------ resets / draws
     def get_randoms(self, shape, bounds):

@@ -156,7 +156,7 @@ class ThormangWalk(VecTask):
         self._keep, self._keep_post = a, (rd, pd)
         self.extras["time_outs"] = self.timeout_buf
         self.obs_dict["obs"] = self.obs_buf
-        return self.obs_dict, self.rew_buf, self.reset_buf, self.extras
+        return self._rl_out()
 
     def reset_idx(self, env_ids):
         env_ids = torch.as_tensor(env_ids, device=self.device)
