@@ -57,8 +57,9 @@ int launch_par(const StepArgs &a, hipStream_t stream, const typename P::Args &pa
 }
 
 template <class M> int launch_model(const StepArgs &a, hipStream_t stream, hipEvent_t ev_begin, hipEvent_t ev_end) {
-    hipLaunchKernelGGL(compose_kernel<M>, dim3((a.N + COMPOSE_WPB - 1) / COMPOSE_WPB), dim3(64 * COMPOSE_WPB), 0, stream,
-                       a);
+    if (!a.skip_compose)
+        hipLaunchKernelGGL(compose_kernel<M>, dim3((a.N + COMPOSE_WPB - 1) / COMPOSE_WPB), dim3(64 * COMPOSE_WPB), 0,
+                           stream, a);
     if (ev_begin && hipEventRecord(ev_begin, stream) != hipSuccess) return TG_ERR_HIP;
     if (int rc = a.hf ? launch_par<M, true>(a, stream) : launch_par<M, false>(a, stream)) return rc;
     if (ev_end && hipEventRecord(ev_end, stream) != hipSuccess) return TG_ERR_HIP;
@@ -82,8 +83,9 @@ int launch_model_walk(const StepArgs &a, const WalkPostArgs &pa, hipStream_t str
         return 1;
     } else {
         if (a.hf || pa.p.num_dof != M::ND) return 1;
-        hipLaunchKernelGGL(compose_kernel<M>, dim3((a.N + COMPOSE_WPB - 1) / COMPOSE_WPB), dim3(64 * COMPOSE_WPB), 0,
-                           stream, a);
+        if (!a.skip_compose)
+            hipLaunchKernelGGL(compose_kernel<M>, dim3((a.N + COMPOSE_WPB - 1) / COMPOSE_WPB), dim3(64 * COMPOSE_WPB), 0,
+                               stream, a);
         if (ev_begin && hipEventRecord(ev_begin, stream) != hipSuccess) return TG_ERR_HIP;
         if (int rc = launch_par<M, false, WalkPost>(a, stream, pa)) return rc;
         if (ev_end && hipEventRecord(ev_end, stream) != hipSuccess) return TG_ERR_HIP;
@@ -100,8 +102,9 @@ int launch_model_gogoro(const StepArgs &a, const GogoroPostArgs &pa, hipStream_t
         return 1;
     } else {
         if (pa.p.num_dof != M::ND) return 1;
-        hipLaunchKernelGGL(compose_kernel<M>, dim3((a.N + COMPOSE_WPB - 1) / COMPOSE_WPB), dim3(64 * COMPOSE_WPB), 0,
-                           stream, a);
+        if (!a.skip_compose)
+            hipLaunchKernelGGL(compose_kernel<M>, dim3((a.N + COMPOSE_WPB - 1) / COMPOSE_WPB), dim3(64 * COMPOSE_WPB), 0,
+                               stream, a);
         if (ev_begin && hipEventRecord(ev_begin, stream) != hipSuccess) return TG_ERR_HIP;
         if (int rc = a.hf ? launch_par<M, true, GogoroPost>(a, stream, pa) : launch_par<M, false, GogoroPost>(a, stream, pa))
             return rc;

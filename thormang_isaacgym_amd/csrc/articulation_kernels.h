@@ -76,14 +76,19 @@ constexpr int COMPOSE_WPB = 8;
 // Prologue (tg_walk_step): the walk task's pre_physics_step fused into the
 // compose launch that precedes every step kernel -- the same fp32 operations
 // as walk_task.hip walk_pre_kernel (no contraction: default + scale * a).
-__device__ __forceinline__ void target_prologue(const StepArgs &a, int e, int lane) {
+__device__ __forceinline__ float pm_clamp(const StepArgs &a, float x) {
+    return x < -a.pm_clip ? -a.pm_clip : (x > a.pm_clip ? a.pm_clip : x);
+}
+__device__ __forceinline__ float pm_target(const StepArgs &a, int d, float c) {
 #pragma clang fp contract(off)
+    return a.pm_default[d] + a.pm_scale * c;
+}
+__device__ __forceinline__ void target_prologue(const StepArgs &a, int e, int lane) {
     if (lane >= a.D) return;
     const unsigned i = (unsigned)e * (unsigned)a.D + (unsigned)lane;
-    const float x = a.pm_actions[i];
-    const float c = x < -a.pm_clip ? -a.pm_clip : (x > a.pm_clip ? a.pm_clip : x);
+    const float c = pm_clamp(a, a.pm_actions[i]);
     a.pm_act_out[i] = c;
-    a.pm_tgt_out[i] = a.pm_default[lane] + a.pm_scale * c;
+    a.pm_tgt_out[i] = pm_target(a, lane, c);
 }
 
 // Prologue (tg_gogoro_step): gogoro_task.hip pre_kernel for env e on one lane
@@ -112,7 +117,7 @@ template <class M> __global__ __launch_bounds__(64 * COMPOSE_WPB) void compose_k
     const int wv = threadIdx.x / 64;
     const int e = blockIdx.x * COMPOSE_WPB + wv;
     const bool dirty = e < a.N && a.dirty[e] != 0;   // read before the prologue: one memory latency
-    if (a.pm_actions && e < a.N) target_prologue(a, e, threadIdx.x % 64);
+    if (a.pm_actions && !a.pm_in_step && e < a.N) target_prologue(a, e, threadIdx.x % 64);
     if (a.gp.actions && e < a.N && threadIdx.x % 64 == 0) gogoro_pre_prologue(a.gp, e, a.D);
     if (!dirty) return;
     TG_CPROF_INIT
@@ -608,9 +613,14 @@ struct WalkPost {
                 } else {
                     q[r] = 0.5f * (prop(a, TG_PROP_LOWER, e, d) + prop(a, TG_PROP_UPPER, e, d));
                 }
-                act[r] = b.actions[eD + d];
+                if (a.pm_in_step) {   // the pre-physics ran inside this kernel (pass 2a's targets)
+                    act[r] = pm_clamp(a, a.pm_actions[eD + d]);
+                    pt[r] = pm_target(a, d, act[r]);
+                } else {
+                    act[r] = b.actions[eD + d];
+                    pt[r] = b.pos_target[eD + d];
+                }
                 la[r] = b.last_actions[eD + d];
-                pt[r] = b.pos_target[eD + d];
             }
         }
 #pragma unroll
@@ -667,6 +677,10 @@ struct WalkPost {
                     o[13 + D + d] = clampw(qd[r] * p.dof_vel_scale, -co, co);
                     o[13 + 2 * D + d] = clampw(act[r], -co, co);
                     b.last_actions[eD + d] = act[r];
+                    if (a.pm_in_step) {   // the prologue's outputs (a reset env's actions are 0)
+                        b.actions[eD + d] = act[r];
+                        b.pos_target[eD + d] = pt[r];
+                    }
                 }
                 rate += (act[r] - la[r]) * (act[r] - la[r]);
                 vel2 += qd[r] * qd[r];

@@ -261,9 +261,10 @@ int jit_launch_step(uint64_t hash, const StepArgs &a, hipStream_t stream, hipEve
     if (!L) return TG_ERR_MODEL;
     StepArgs aa = a;
     void *cargs[] = {&aa};
-    if (int rc = launch(L->f[K_COMPOSE], (unsigned)((a.N + JIT_COMPOSE_WPB - 1) / JIT_COMPOSE_WPB),
-                        64 * JIT_COMPOSE_WPB, 0, stream, cargs))
-        return rc;
+    if (!a.skip_compose)
+        if (int rc = launch(L->f[K_COMPOSE], (unsigned)((a.N + JIT_COMPOSE_WPB - 1) / JIT_COMPOSE_WPB),
+                            64 * JIT_COMPOSE_WPB, 0, stream, cargs))
+            return rc;
     if (ev_begin && hipEventRecord(ev_begin, stream) != hipSuccess) return TG_ERR_HIP;
     char pa = 0;   // the step kernel's empty NoPost::Args
     void *sargs[] = {&aa, &pa};

@@ -473,7 +473,8 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         x[5] = PR(TG_PROP_LOWER, d);
         x[6] = PR(TG_PROP_UPPER, d);
         const unsigned ed = (unsigned)e * (unsigned)D + (unsigned)d;
-        x[7] = a.pos_tgt[ed];
+        // the walk pre-physics inside the step (tg_walk_step): the target from the action
+        x[7] = a.pm_in_step ? pm_target(a, d, pm_clamp(a, a.pm_actions[ed])) : a.pos_tgt[ed];
         x[8] = a.vel_tgt[ed];
         x[9] = a.act ? a.act[ed] : 0.f;
     };

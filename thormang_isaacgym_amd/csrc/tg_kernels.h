@@ -57,6 +57,12 @@ struct StepArgs {
     float pm_scale, pm_clip;
     float pm_default[TG_PM_MAX_DOF];
     GogoroPre gp;
+    // pm_in_step: the walk prologue runs inside the step kernel instead (the
+    // drive targets are formed from pm_actions where pass 2a loads them, the
+    // fused WalkPost epilogue writes pm_act_out / pm_tgt_out); skip_compose:
+    // no env can be dirty and no compose prologue is requested, so the
+    // compose launch is left out (tgsim_api.cpp dirty_possible)
+    int pm_in_step, skip_compose;
 };
 
 // tg_walk_step's fused post-physics epilogue (articulation.hip WalkPost)

@@ -49,6 +49,14 @@ struct tg_sim {
     hipStream_t stream = nullptr;
     float gravity[3] = {0, 0, -9.81f};
     bool forces_pending = false;
+    // some env may be dirty (its composite cache stale): set by every call that
+    // can mark envs dirty or change what compose reads (creation, state
+    // binding, tg_refresh -- the contract for writes through the zero-copy
+    // views --, property / mass-scale setters, the Gogoro and paper task
+    // kernels, whose resets rewrite properties), cleared by a compose launch.
+    // While false, a simulate without a compose prologue skips the compose
+    // launch (one launch less per step; ThormangWalk's envs never go dirty)
+    bool dirty_possible = true;
     // device buffers
     float *root = nullptr, *dof = nullptr, *pos_tgt = nullptr, *vel_tgt = nullptr, *act = nullptr;
     float *props = nullptr, *force = nullptr, *mass_scale = nullptr, *shape_mu = nullptr, *comp = nullptr;
@@ -64,6 +72,8 @@ struct tg_sim {
     // kernel timing (tg_set_kernel_timing): event pairs recorded, not yet read
     bool walk_unfused = false;   // tg_walk_step: separate post-physics launch (TG_WALK_UNFUSED=1)
     bool post_unfused = false;   // tg_gogoro_step: separate post-physics launch (TG_POST_UNFUSED=1)
+    bool always_compose = false; // never skip the compose launch (TG_ALWAYS_COMPOSE=1)
+    bool pre_in_compose = false; // tg_walk_step: pre-physics in the compose launch, not the step kernel (TG_PRE_IN_COMPOSE=1)
     int timing = 0;          // period (0: off)
     int64_t timing_count = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending, ev_free;
@@ -176,6 +186,8 @@ int tg_sim_create(const tg_model_desc *m, const tg_sim_params *params, int32_t n
     tg_sim *s = owner.get();
     if (const char *u = getenv("TG_WALK_UNFUSED")) s->walk_unfused = u[0] == '1';
     if (const char *u = getenv("TG_POST_UNFUSED")) s->post_unfused = u[0] == '1';
+    if (const char *u = getenv("TG_ALWAYS_COMPOSE")) s->always_compose = u[0] == '1';
+    if (const char *u = getenv("TG_PRE_IN_COMPOSE")) s->pre_in_compose = u[0] == '1';
     s->device = device;
     s->N = num_envs;
     s->D = m->num_dofs;
@@ -265,10 +277,15 @@ int tg_state_ptrs(tg_sim *s, tg_state_view *v) {
     return TG_OK;
 }
 
-int tg_refresh(tg_sim *s) { return check_sim(s); }
+int tg_refresh(tg_sim *s) {
+    if (int rc = check_sim(s)) return rc;
+    s->dirty_possible = true;   // writes through the zero-copy views (env_dirty, dof_props) take effect
+    return TG_OK;
+}
 
 int tg_bind_state(tg_sim *s, const tg_state_view *v) {
     if (int rc = check_sim(s)) return rc;
+    s->dirty_possible = true;
     if (!v) return fail(TG_ERR_ARG, "null view");
     const size_t N = s->N, D = s->D;
     struct B {
@@ -335,6 +352,7 @@ int tg_set_dof_state_indexed(tg_sim *s, const float *dof, const int32_t *ids, in
 
 int tg_set_dof_properties_indexed(tg_sim *s, int32_t field, const float *vals, const int32_t *ids, int32_t n) {
     if (int rc = check_sim(s)) return rc;
+    s->dirty_possible = true;
     if (int rc = check_ids(s, ids, n)) return rc;
     if (field < 0 || field >= TG_NUM_PROPS) return fail(TG_ERR_ARG, "unknown dof property field %d", field);
     if (!vals) return fail(TG_ERR_ARG, "null property values");
@@ -347,6 +365,7 @@ int tg_set_dof_properties_indexed(tg_sim *s, int32_t field, const float *vals, c
 
 int tg_set_body_mass_scale_indexed(tg_sim *s, const float *scale, const int32_t *ids, int32_t n) {
     if (int rc = check_sim(s)) return rc;
+    s->dirty_possible = true;
     if (int rc = check_ids(s, ids, n)) return rc;
     if (!scale) return fail(TG_ERR_ARG, "null mass scale");
     if (int rc = tg::launch_scatter_rows(s->mass_scale, scale, ids, n, s->L, s->stream)) return fail(rc, "scatter failed");
@@ -421,9 +440,12 @@ struct DeviceGuard {
     }
 };
 
-static int simulate_args(tg_sim *s, const tg::StepArgs &a, const tg::WalkPostArgs *wp = nullptr,
+static int simulate_args(tg_sim *s, const tg::StepArgs &a_in, const tg::WalkPostArgs *wp = nullptr,
                          const tg::GogoroPostArgs *gp = nullptr) {
     DeviceGuard dg(s->device);
+    tg::StepArgs a = a_in;
+    const bool compose_prologue = a.gp.actions || (a.pm_actions && !a.pm_in_step);
+    a.skip_compose = !s->dirty_possible && !compose_prologue && !s->always_compose;
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     const bool timed = s->timing > 0 && s->timing_count % s->timing == 0;
     if (timed) {
@@ -448,6 +470,8 @@ static int simulate_args(tg_sim *s, const tg::StepArgs &a, const tg::WalkPostArg
     if (s->timing > 0) s->timing_count++;
     if (ev.first) s->ev_pending.push_back(ev);
     s->forces_pending = false;   // apply_rigid_body_force_tensors acts for one simulate call
+    if (!a.skip_compose) s->dirty_possible = false;   // the compose launch cleaned every dirty env
+    if (gp) s->dirty_possible = true;                  // the Gogoro epilogue's resets rewrite properties
     return TG_OK;
 }
 
@@ -543,6 +567,7 @@ int tg_rng_fill(tg_sim *s, int32_t kind, uint64_t seed, uint64_t counter, float 
 int tg_gogoro_pre_physics(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_buffers *b, const float *actions,
                           const float *pre_draws, uint64_t counter) {
     if (int rc = check_sim(s)) return rc;
+    s->dirty_possible = true;
     if (!p || !b || !actions) return fail(TG_ERR_ARG, "tg_gogoro_pre_physics: null argument");
     if (p->num_envs != s->N || p->num_dof != s->D) return fail(TG_ERR_ARG, "gogoro params do not match the sim");
     if (int rc = tg::launch_gogoro_pre(*p, *b, actions, pre_draws, counter, s->stream)) return fail(rc, "launch failed");
@@ -552,6 +577,7 @@ int tg_gogoro_pre_physics(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_
 int tg_gogoro_step(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_buffers *b, const float *actions,
                    int32_t n_simulate, uint64_t counter_pre, uint64_t counter_post) {
     if (int rc = check_sim(s)) return rc;
+    s->dirty_possible = true;
     if (!p || !b || !actions) return fail(TG_ERR_ARG, "tg_gogoro_step: null argument");
     if (p->num_envs != s->N || p->num_dof != s->D) return fail(TG_ERR_ARG, "gogoro params do not match the sim");
     if (n_simulate < 1) return fail(TG_ERR_ARG, "tg_gogoro_step: n_simulate %d < 1", n_simulate);
@@ -594,6 +620,7 @@ int tg_gogoro_step(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_buffers
 int tg_gogoro_post_physics(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_buffers *b, const float *reset_draws,
                            const float *obs_draws, const float *speed_draws, const float *yaw_draws, uint64_t counter) {
     if (int rc = check_sim(s)) return rc;
+    s->dirty_possible = true;
     if (!p || !b) return fail(TG_ERR_ARG, "tg_gogoro_post_physics: null argument");
     if (p->num_envs != s->N || p->num_dof != s->D) return fail(TG_ERR_ARG, "gogoro params do not match the sim");
     if ((speed_draws == nullptr) != (yaw_draws == nullptr))
@@ -606,6 +633,7 @@ int tg_gogoro_post_physics(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro
 int tg_gogoro_reset_idx(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_buffers *b, const int32_t *ids,
                         int32_t n, const float *reset_draws, uint64_t counter) {
     if (int rc = check_sim(s)) return rc;
+    s->dirty_possible = true;
     if (int rc = check_ids(s, ids, n)) return rc;
     if (!p || !b) return fail(TG_ERR_ARG, "tg_gogoro_reset_idx: null argument");
     if (p->num_envs != s->N || p->num_dof != s->D) return fail(TG_ERR_ARG, "gogoro params do not match the sim");
@@ -641,6 +669,23 @@ int tg_walk_step(tg_sim *s, const tg_walk_params *p, const tg_walk_buffers *b, c
     if (b->body_force) {   // pre_physics_step: apply_rigid_body_force_tensors(body_force)
         if (int rc = copy_full(s, s->force, b->body_force, (size_t)s->N * s->G * 6)) return rc;
         s->forces_pending = true;
+    }
+    if (n_simulate == 1 && !s->walk_unfused && !s->pre_in_compose) {
+        // one launch per step: pre-physics (drive targets formed from the
+        // actions where pass 2a loads them), physics and post-physics all in
+        // the step kernel; the compose launch runs only if an env may be dirty
+        tg::StepArgs a = step_args(s);
+        a.pm_actions = actions;
+        a.pm_act_out = b->actions;
+        a.pm_tgt_out = b->pos_target;
+        a.pm_scale = p->action_scale;
+        a.pm_clip = p->clip_actions;
+        for (int d = 0; d < p->num_dof; ++d) a.pm_default[d] = p->default_pos[d];
+        a.pm_in_step = 1;
+        const tg::WalkPostArgs wp{*p, *b, reset_draws, push_draws, (uint32_t)counter, (uint32_t)(counter >> 32)};
+        const int rc = simulate_args(s, a, &wp);
+        if (rc <= 0) return rc;
+        // rc == 1: no fused instantiation for this model / ground -- the general path below
     }
     for (int i = 0; i < n_simulate; ++i) {
         tg::StepArgs a = step_args(s);
@@ -703,6 +748,7 @@ int tg_paper_pre_physics(tg_sim *s, const tg_paper_params *p, const tg_paper_buf
                          uint64_t counter) {
     (void)counter;
     if (int rc = check_paper(s, p, b)) return rc;
+    s->dirty_possible = true;
     if (!actions) return fail(TG_ERR_ARG, "paper: null actions");
     if (int rc = tg::launch_paper_pre(*p, *b, actions, s->stream)) return fail(rc, "launch failed");
     return TG_OK;
@@ -712,6 +758,7 @@ int tg_paper_post_physics(tg_sim *s, const tg_paper_params *p, const tg_paper_bu
                           const float *noise_draws, const float *speed_draws, const float *yaw_draws,
                           const float *push_draws, uint64_t counter) {
     if (int rc = check_paper(s, p, b)) return rc;
+    s->dirty_possible = true;
     if (int rc = tg::launch_paper_post(*p, *b, reset_draws, noise_draws, speed_draws, yaw_draws, push_draws, counter,
                                        s->stream))
         return fail(rc, "launch failed");
@@ -721,6 +768,7 @@ int tg_paper_post_physics(tg_sim *s, const tg_paper_params *p, const tg_paper_bu
 int tg_paper_reset_idx(tg_sim *s, const tg_paper_params *p, const tg_paper_buffers *b, const int32_t *ids, int32_t n,
                        const float *reset_draws, uint64_t counter) {
     if (int rc = check_paper(s, p, b)) return rc;
+    s->dirty_possible = true;
     if (int rc = check_ids(s, ids, n)) return rc;
     if (int rc = tg::launch_paper_reset_idx(*p, *b, ids, n, reset_draws, counter, s->stream))
         return fail(rc, "launch failed");
