@@ -1,0 +1,88 @@
+"""Edge cases of the batch shape on the GPU: env counts that do not fill a
+workgroup (the step kernel runs 16 envs per workgroup and the tail lanes redo
+the last env without storing), a single env, the largest batch, empty index
+lists -- each checked against the oracle or against an invariant."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _cuda():
+    if not torch.cuda.is_available():
+        pytest.skip("needs the MI355X")
+
+
+@pytest.mark.parametrize("n", [1, 13, 37])
+def test_gpu_ragged_batches_gogoro_env_matches_oracle(n):
+    _cuda()
+    from tests.gpu_harness import balance_policy, gogoro_env_vs_oracle
+    err = gogoro_env_vs_oracle(num_envs=n, steps=80, seed=50 + n, policy=balance_policy)
+    assert err["obs"] < 1e-3 and err["rew"] < 1e-3, err
+    assert err["reset_equal"] and err["timeout_equal"], err
+
+
+@pytest.mark.parametrize("n", [1, 19])
+def test_gpu_ragged_batches_walk_env_matches_oracle(n):
+    _cuda()
+    from tests.gpu_harness import walk_env_vs_oracle
+    err = walk_env_vs_oracle(num_envs=n, steps=40, seed=60 + n)
+    assert err["obs"] < 1e-3 and err["rew"] < 1e-3, err
+    assert err["reset_equal"] and err["timeout_equal"], err
+
+
+@pytest.mark.parametrize("name", ["thormang", "gogoro"])
+def test_gpu_tail_envs_equal_full_batch(name):
+    """The same 21 env states stepped as a batch of 21 (a partial workgroup)
+    and as the first 21 of a batch of 48: identical results, bit for bit --
+    the tail lanes of a partial workgroup never store."""
+    _cuda()
+    from tests.test_rigid_body_states import random_state
+    from thormang_isaacgym_amd import abi
+    from thormang_isaacgym_amd.sim import Sim, load_model
+    m = load_model(name)
+    root, dof = random_state(m, 48, np.random.default_rng(8))
+    root[:, 2] = 2.0                       # clear of the ground: no contact ordering effects
+    sp = abi.sim_params_from_cfg({"dt": 0.01, "substeps": 2, "gravity": [0, 0, -9.81]}, {}, 48, warn=False)
+    out = []
+    for n in (21, 48):
+        s = Sim(m, sp, n, "cuda:0")
+        s.root_state.copy_(torch.from_numpy(root[:n]))
+        s.dof_state.copy_(torch.from_numpy(dof.reshape(48, -1)[:n].reshape(-1, 2)))
+        s.env_dirty.fill_(1)
+        s.refresh()
+        for _ in range(10):
+            s.simulate()
+        torch.cuda.synchronize()
+        out.append((s.root_state[:21].cpu(), s.dof_state.view(n, -1, 2)[:21].cpu()))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+
+
+def test_gpu_reset_idx_empty_and_full():
+    _cuda()
+    import thormang_isaacgym_amd as tia
+    env = tia.make(seed=3, task="Gogoro", num_envs=64, sim_device="cuda:0", rl_device="cuda:0")
+    before = env.root_tensor.clone()
+    env.reset_idx(torch.zeros(0, dtype=torch.long, device="cuda:0"))   # no-op
+    torch.cuda.synchronize()
+    assert torch.equal(before, env.root_tensor)
+    env.reset_idx(torch.arange(64, device="cuda:0"))
+    torch.cuda.synchronize()
+    assert torch.isfinite(env.root_tensor).all()
+    assert float(env.root_tensor[:, 7:13].abs().max()) == 0.0        # every env re-spawned at rest
+    assert int(env.progress_buf.abs().max()) == 0
+
+
+def test_gpu_walk_32768_envs_runs():
+    """The largest batch in the tests (2x BASELINE config 5's 16384): finite
+    state, resets and timeouts behave, no tail issues."""
+    _cuda()
+    import thormang_isaacgym_amd as tia
+    env = tia.make(seed=5, task="ThormangWalk", num_envs=32768, sim_device="cuda:0", rl_device="cuda:0")
+    g = torch.Generator(device="cuda:0").manual_seed(2)
+    for _ in range(30):
+        obs, rew, reset, extras = env.step(torch.rand(32768, env.num_actions, device="cuda:0", generator=g) * 2 - 1)
+    torch.cuda.synchronize()
+    assert torch.isfinite(obs["obs"]).all() and torch.isfinite(rew).all()
+    assert obs["obs"].shape == (32768, env.num_obs)
