@@ -32,6 +32,19 @@ namespace tg {
 // compose (dirty envs only), then the tree-parallel LDS-resident step,
 // M::EPB envs x M::LPE lanes per workgroup (Thormang: 16 envs, 151 KB of LDS).
 
+// the compose launch before a step kernel: none (no env can be dirty and no
+// prologue), the listed envs of the last fused epilogue (compose_list_kernel),
+// or every dirty env (compose_kernel)
+template <class M> void launch_compose(const StepArgs &a, hipStream_t stream) {
+    if (a.skip_compose) return;
+    if (a.compose_list)
+        hipLaunchKernelGGL(compose_list_kernel<M>, dim3((a.N + COMPOSE_WPB - 1) / COMPOSE_WPB), dim3(64), 0, stream,
+                           a);
+    else
+        hipLaunchKernelGGL(compose_kernel<M>, dim3((a.N + COMPOSE_WPB - 1) / COMPOSE_WPB), dim3(64 * COMPOSE_WPB), 0,
+                           stream, a);
+}
+
 // HF: terrain heightfield present (tg_set_heightfield); the flat-ground
 // instantiation keeps the contact normal a compile-time e_z.
 template <class M, bool HF, class P = NoPost>
@@ -57,9 +70,7 @@ int launch_par(const StepArgs &a, hipStream_t stream, const typename P::Args &pa
 }
 
 template <class M> int launch_model(const StepArgs &a, hipStream_t stream, hipEvent_t ev_begin, hipEvent_t ev_end) {
-    if (!a.skip_compose)
-        hipLaunchKernelGGL(compose_kernel<M>, dim3((a.N + COMPOSE_WPB - 1) / COMPOSE_WPB), dim3(64 * COMPOSE_WPB), 0,
-                           stream, a);
+    launch_compose<M>(a, stream);
     if (ev_begin && hipEventRecord(ev_begin, stream) != hipSuccess) return TG_ERR_HIP;
     if (int rc = a.hf ? launch_par<M, true>(a, stream) : launch_par<M, false>(a, stream)) return rc;
     if (ev_end && hipEventRecord(ev_end, stream) != hipSuccess) return TG_ERR_HIP;
@@ -83,9 +94,7 @@ int launch_model_walk(const StepArgs &a, const WalkPostArgs &pa, hipStream_t str
         return 1;
     } else {
         if (a.hf || pa.p.num_dof != M::ND) return 1;
-        if (!a.skip_compose)
-            hipLaunchKernelGGL(compose_kernel<M>, dim3((a.N + COMPOSE_WPB - 1) / COMPOSE_WPB), dim3(64 * COMPOSE_WPB), 0,
-                               stream, a);
+        launch_compose<M>(a, stream);
         if (ev_begin && hipEventRecord(ev_begin, stream) != hipSuccess) return TG_ERR_HIP;
         if (int rc = launch_par<M, false, WalkPost>(a, stream, pa)) return rc;
         if (ev_end && hipEventRecord(ev_end, stream) != hipSuccess) return TG_ERR_HIP;
@@ -102,9 +111,7 @@ int launch_model_gogoro(const StepArgs &a, const GogoroPostArgs &pa, hipStream_t
         return 1;
     } else {
         if (pa.p.num_dof != M::ND) return 1;
-        if (!a.skip_compose)
-            hipLaunchKernelGGL(compose_kernel<M>, dim3((a.N + COMPOSE_WPB - 1) / COMPOSE_WPB), dim3(64 * COMPOSE_WPB), 0,
-                               stream, a);
+        launch_compose<M>(a, stream);
         if (ev_begin && hipEventRecord(ev_begin, stream) != hipSuccess) return TG_ERR_HIP;
         if (int rc = a.hf ? launch_par<M, true, GogoroPost>(a, stream, pa) : launch_par<M, false, GogoroPost>(a, stream, pa))
             return rc;

@@ -113,28 +113,27 @@ __device__ __forceinline__ void gogoro_pre_prologue(const GogoroPre &g, int e, i
     g.vel_target[(size_t)e * D + g.dof_rear] = g.curent_speed[e];
 }
 
-template <class M> __global__ __launch_bounds__(64 * COMPOSE_WPB) void compose_kernel(StepArgs a) {
-    const int wv = threadIdx.x / 64;
-    const int e = blockIdx.x * COMPOSE_WPB + wv;
-    const bool dirty = e < a.N && a.dirty[e] != 0;   // read before the prologue: one memory latency
-    if (a.pm_actions && !a.pm_in_step && e < a.N) target_prologue(a, e, threadIdx.x % 64);
-    if (a.gp.actions && e < a.N && threadIdx.x % 64 == 0) gogoro_pre_prologue(a.gp, e, a.D);
-    if (!dirty) return;
+// one wavefront's compose scratch
+template <class M> struct ComposeLds {
+    float T[M::NL][12];        // link pose in its group-root frame: R (9), p (3)
+    float LM[M::NL + 1][10];   // link mass, com (group frame), inertia about com; row NL = 0
+    int GL[M::NG][M::MAXGL];   // group links, padded with NL (the zero row): branch-free sums
+};
+
+// compose env e with the 64 lanes of a wavefront (cs: the wave's LDS scratch)
+template <class M> __device__ __forceinline__ void compose_env(const StepArgs &a, int e, int lane, ComposeLds<M> &cs) {
     TG_CPROF_INIT
     using CL = CompLayout<M>;
     static_assert(M::NL <= 64 && M::NG <= 64 && M::NS <= 64, "compose: one lane per link / group / shape");
-    __shared__ float Ts[COMPOSE_WPB][M::NL][12];    // link pose in its group-root frame: R (9), p (3)
-    __shared__ float LMs[COMPOSE_WPB][M::NL + 1][10];   // link mass, com (group frame), inertia about com; row NL = 0
-    __shared__ int GLs[COMPOSE_WPB][M::NG][M::MAXGL];   // group links, padded with NL (the zero row): branch-free sums
-    float(&T)[M::NL][12] = Ts[wv];
-    float(&LM)[M::NL + 1][10] = LMs[wv];
-    int(&GL)[M::NG][M::MAXGL] = GLs[wv];
-    const int lane = threadIdx.x % 64;
+    float(&T)[M::NL][12] = cs.T;
+    float(&LM)[M::NL + 1][10] = cs.LM;
+    int(&GL)[M::NG][M::MAXGL] = cs.GL;
     auto wsync = [] {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
+    wsync();   // a previous compose of this wave is done with the scratch
     auto ldT = [&](int l, M3 &R, V3 &P) {
 #pragma unroll
         for (int k = 0; k < 9; ++k) R.a[k] = T[l][k];
@@ -346,6 +345,35 @@ template <class M> __global__ __launch_bounds__(64 * COMPOSE_WPB) void compose_k
     }
     if (lane == 0) a.dirty[e] = 0;
     TG_CPROF(3)
+}
+
+template <class M> __global__ __launch_bounds__(64 * COMPOSE_WPB) void compose_kernel(StepArgs a) {
+    const int wv = threadIdx.x / 64;
+    const int e = blockIdx.x * COMPOSE_WPB + wv;
+    const bool dirty = e < a.N && a.dirty[e] != 0;   // read before the prologue: one memory latency
+    if (a.cnext && blockIdx.x == 0 && threadIdx.x == 0) *a.cnext = 0;   // the reset list the next epilogue fills
+    if (a.pm_actions && !a.pm_in_step && e < a.N) target_prologue(a, e, threadIdx.x % 64);
+    if (a.gp.actions && e < a.N && threadIdx.x % 64 == 0) gogoro_pre_prologue(a.gp, e, a.D);
+    if (!dirty) return;
+    __shared__ ComposeLds<M> cs[COMPOSE_WPB];
+    compose_env<M>(a, e, threadIdx.x % 64, cs[wv]);
+}
+
+// Compose of the envs a fused task epilogue reset (tg_gogoro_step): the
+// previous step kernel appended their ids to a.clist / *a.ccount, so no wave
+// reads all N dirty flags.  One wavefront per workgroup, COMPOSE_WPB envs per
+// wave: first the task's pre-physics prologue on lanes 0..COMPOSE_WPB-1 (one
+// lane per env), then wave b composes list entry b (b + grid, ... for longer
+// lists); zeroes the count the coming epilogue appends to.
+template <class M> __global__ __launch_bounds__(64) void compose_list_kernel(StepArgs a) {
+    const int lane = threadIdx.x;
+    const int n = a.ccount ? *a.ccount : 0;   // issued first: its latency overlaps the prologue
+    if (a.cnext && blockIdx.x == 0 && lane == 0) *a.cnext = 0;
+    const int e0 = blockIdx.x * COMPOSE_WPB + lane;
+    if (a.gp.actions && lane < COMPOSE_WPB && e0 < a.N) gogoro_pre_prologue(a.gp, e0, a.D);
+    if ((int)blockIdx.x >= n) return;
+    __shared__ ComposeLds<M> cs;
+    for (int i = blockIdx.x; i < n; i += gridDim.x) compose_env<M>(a, a.clist[i], lane, cs);
 }
 
 // ---------------------------------------------------------------- rigid-body states
@@ -866,6 +894,7 @@ struct GogoroPost {
                 prop[TG_PROP_EFFORT * ND + st] = p.steer_effort;
                 prop[TG_PROP_VELOCITY * ND + st] = p.steer_velocity;
                 b.env_dirty[e] = 1;
+                if (pa.reset_list) pa.reset_list[atomicAdd(pa.reset_count, 1)] = e;   // for compose_list_kernel
                 b.curent_command[e] = 0.0f;
 #pragma unroll
                 for (int k = 0; k < 5; ++k) b.action_history[5 * (size_t)e + k] = 0.0f;

@@ -63,6 +63,12 @@ struct StepArgs {
     // no env can be dirty and no compose prologue is requested, so the
     // compose launch is left out (tgsim_api.cpp dirty_possible)
     int pm_in_step, skip_compose;
+    // compose_list: compose only the envs in clist[0, *ccount) (ccount null: none)
+    // -- a fused epilogue's resets -- with compose_list_kernel; cnext (or null):
+    // the reset count the coming epilogue appends to, zeroed by the compose launch
+    int compose_list;
+    const int *clist, *ccount;
+    int *cnext;
 };
 
 // tg_walk_step's fused post-physics epilogue (articulation.hip WalkPost)
@@ -77,6 +83,7 @@ struct GogoroPostArgs {
     tg_gogoro_params p;
     tg_gogoro_buffers b;
     uint32_t c_lo, c_hi;
+    int *reset_list, *reset_count;   // [N] ids of the envs reset (and made dirty) / their count, or null
 };
 #ifndef __HIPCC_RTC__   // host launchers (not part of a hipRTC unit, jit.cpp)
 // compose + step kernel with the Gogoro post-physics fused in; returns 1 when

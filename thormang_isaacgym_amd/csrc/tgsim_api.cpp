@@ -57,6 +57,13 @@ struct tg_sim {
     // While false, a simulate without a compose prologue skips the compose
     // launch (one launch less per step; ThormangWalk's envs never go dirty)
     bool dirty_possible = true;
+    // reset lists of the fused Gogoro epilogue (compose_list_kernel): two
+    // slots of N ids + counts; the epilogue appends to slot list_cur, the next
+    // compose reads the other one and zeroes list_cur's count; list_pending:
+    // the last step kernel had that epilogue (its resets await their compose)
+    int *clist = nullptr, *ccount = nullptr;
+    int list_cur = 0;
+    bool list_pending = false;
     // device buffers
     float *root = nullptr, *dof = nullptr, *pos_tgt = nullptr, *vel_tgt = nullptr, *act = nullptr;
     float *props = nullptr, *force = nullptr, *mass_scale = nullptr, *shape_mu = nullptr, *comp = nullptr;
@@ -213,6 +220,8 @@ int tg_sim_create(const tg_model_desc *m, const tg_sim_params *params, int32_t n
     rc |= s->alloc(&s->env_origin, N * 3);
     rc |= s->alloc(&s->dirty, N);
     rc |= s->alloc(&s->err, 1);
+    rc |= s->alloc(&s->clist, 2 * N);
+    rc |= s->alloc(&s->ccount, 2);
     if (rc) return TG_ERR_HIP;   // g_err holds the failing allocation; owner frees the rest
     // host-side initial values: identity root pose at the env origin grid,
     // unit mass scale, per-shape friction from the model, defaults for props
@@ -238,6 +247,7 @@ int tg_sim_create(const tg_model_desc *m, const tg_sim_params *params, int32_t n
     HIPCHK(hipMemcpy(s->mass_scale, h_ms.data(), h_ms.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(s->shape_mu, h_mu.data(), h_mu.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(s->dirty, h_dirty.data(), N, hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(s->ccount, 0, 2 * sizeof(int)));
     HIPCHK(hipMemcpy(s->props, h_props.data(), h_props.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipDeviceSynchronize());
     *out = owner.release();
@@ -444,8 +454,18 @@ static int simulate_args(tg_sim *s, const tg::StepArgs &a_in, const tg::WalkPost
                          const tg::GogoroPostArgs *gp = nullptr) {
     DeviceGuard dg(s->device);
     tg::StepArgs a = a_in;
-    const bool compose_prologue = a.gp.actions || (a.pm_actions && !a.pm_in_step);
-    a.skip_compose = !s->dirty_possible && !compose_prologue && !s->always_compose;
+    // the compose launch: every dirty env (host-side changes possible), the
+    // last fused epilogue's reset list, the task prologue alone, or none
+    const bool walk_prologue = a.pm_actions && !a.pm_in_step;
+    const bool full = s->dirty_possible || s->always_compose || walk_prologue;
+    a.skip_compose = !full && !s->list_pending && !a.gp.actions;
+    a.compose_list = !full && !a.skip_compose;
+    a.cnext = s->ccount + s->list_cur;
+    if (a.compose_list && s->list_pending) {
+        const int prev = 1 - s->list_cur;
+        a.clist = s->clist + (size_t)prev * s->N;
+        a.ccount = s->ccount + prev;
+    }
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     const bool timed = s->timing > 0 && s->timing_count % s->timing == 0;
     if (timed) {
@@ -470,8 +490,18 @@ static int simulate_args(tg_sim *s, const tg::StepArgs &a_in, const tg::WalkPost
     if (s->timing > 0) s->timing_count++;
     if (ev.first) s->ev_pending.push_back(ev);
     s->forces_pending = false;   // apply_rigid_body_force_tensors acts for one simulate call
-    if (!a.skip_compose) s->dirty_possible = false;   // the compose launch cleaned every dirty env
-    if (gp) s->dirty_possible = true;                  // the Gogoro epilogue's resets rewrite properties
+    if (!a.skip_compose) {   // every dirty env, or every listed one, is composed now
+        if (!a.compose_list) s->dirty_possible = false;
+        s->list_pending = false;
+    }
+    if (gp) {   // the Gogoro epilogue's resets rewrite properties
+        if (gp->reset_list) {   // ... and are listed for the next compose
+            s->list_pending = true;
+            s->list_cur = 1 - s->list_cur;
+        } else {
+            s->dirty_possible = true;
+        }
+    }
     return TG_OK;
 }
 
@@ -577,7 +607,6 @@ int tg_gogoro_pre_physics(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_
 int tg_gogoro_step(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_buffers *b, const float *actions,
                    int32_t n_simulate, uint64_t counter_pre, uint64_t counter_post) {
     if (int rc = check_sim(s)) return rc;
-    s->dirty_possible = true;
     if (!p || !b || !actions) return fail(TG_ERR_ARG, "tg_gogoro_step: null argument");
     if (p->num_envs != s->N || p->num_dof != s->D) return fail(TG_ERR_ARG, "gogoro params do not match the sim");
     if (n_simulate < 1) return fail(TG_ERR_ARG, "tg_gogoro_step: n_simulate %d < 1", n_simulate);
@@ -605,7 +634,8 @@ int tg_gogoro_step(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_buffers
             g.c_hi = (uint32_t)(counter_pre >> 32);
         }
         if (i == n_simulate - 1 && !s->post_unfused) {   // post-physics fused into the last step kernel
-            const tg::GogoroPostArgs gp{*p, *b, (uint32_t)counter_post, (uint32_t)(counter_post >> 32)};
+            const tg::GogoroPostArgs gp{*p, *b, (uint32_t)counter_post, (uint32_t)(counter_post >> 32),
+                                        s->clist + (size_t)s->list_cur * s->N, s->ccount + s->list_cur};
             const int rc = simulate_args(s, a, nullptr, &gp);
             if (rc == 0) return TG_OK;
             if (rc < 0) return rc;
@@ -614,6 +644,7 @@ int tg_gogoro_step(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_buffers
     }
     if (int rc = tg::launch_gogoro_post(*p, *b, nullptr, nullptr, nullptr, nullptr, counter_post, s->stream))
         return fail(rc, "launch failed");
+    s->dirty_possible = true;   // the separate post kernel's resets mark envs dirty
     return TG_OK;
 }
 
