@@ -229,6 +229,14 @@ uint64_t tg_compiled_model_hashes(uint64_t *out, int32_t cap); /* returns count 
 int tg_model_jit(uint64_t model_hash, const char *struct_name, const char *model_source, const char *include_dir,
                  const char *cache_dir);
 
+/* Composite-cache instrumentation (no reference counterpart; tests): copies
+ * the per-env composite cache [N, KC] (the group composites and placements
+ * the step kernel reads, built from the lock windows and mass scales) to the
+ * device buffer out; with recompose != 0 every env is first re-composed from
+ * scratch.  Checks the Gogoro epilogue's in-place seat update against a full
+ * compose. */
+int tg_composite(tg_sim *sim, float *out, int32_t recompose);
+
 /* Random-number instrumentation (no reference counterpart; the task kernels'
  * in-kernel draws replace the reference's torch.rand / torch.randn calls):
  * tg_philox4x32_10 is the library's Philox4x32-10 block function on the host

@@ -129,19 +129,63 @@ def test_gpu_env_step_matches_oracle_along_1000_steps():
     assert err["reset_equal"] and err["timeout_equal"], err
 
 
+def test_gpu_gogoro_inplace_seat_composites_equal_a_full_compose():
+    """The fused epilogue's resets move only the seat locks (base_x/y/z), so it
+    updates the rider group's composite and the placements below the seat in
+    place from stored mass moments (articulation_kernels.h tl_update) instead
+    of re-composing the env.  After 60 steps with hundreds of such resets, the
+    composite cache every env holds equals a from-scratch compose of every env
+    (tg_composite instrumentation) to fp32 rounding."""
+    _cuda()
+    import ctypes as C
+    import thormang_isaacgym_amd as tia
+    from thormang_isaacgym_amd._lib import lib
+    n = 1024
+    env = tia.make(seed=33, task="Gogoro", num_envs=n, sim_device="cuda:0", rl_device="cuda:0")
+    g = torch.Generator(device="cuda:0").manual_seed(4)
+    n_reset = 0
+    for _ in range(60):
+        env.step(torch.rand(n, 1, device="cuda:0", generator=g) * 2 - 1)
+        n_reset += int(env.reset_buf.sum())
+    torch.cuda.synchronize()
+    assert n_reset > 100
+    m = env.sim.model
+    kc_main = 24 * m.num_groups + 12 * len(m.shapes)      # CompLayout::ext(): the part the step kernel reads
+    out = [torch.empty(n * 4096, device="cuda:0") for _ in range(2)]
+    for k, rec in enumerate((0, 1)):
+        assert lib().tg_composite(env.sim.handle, C.c_void_p(out[k].data_ptr()), rec) == 0
+    torch.cuda.synchronize()
+    from thormang_isaacgym_amd import abi
+    from thormang_isaacgym_amd.model import codegen
+    kc = kc_main + codegen.translating_locks(m, abi.ModelDesc(m).arrays)["KX"]
+    a = out[0][: n * kc].view(n, kc)[:, :kc_main]
+    b = out[1][: n * kc].view(n, kc)[:, :kc_main]
+    assert torch.isfinite(a).all() and torch.isfinite(b).all()
+    err = (a - b).abs() / (1.0 + b.abs())
+    assert float(err.max()) < 2e-6, float(err.max())
+
+
 def test_gpu_gogoro_fused_step_matches_separate_calls():
-    """tg_gogoro_step (pre-physics fused into the compose launch) against
+    """tg_gogoro_step (pre-physics and post-physics in the step kernel) against
     tg_gogoro_pre_physics + tg_simulate + tg_gogoro_post_physics (the
     VecTask.step sequence) with in-kernel Philox draws, resets included.  The
-    fused prologue is compiled in the fast-math physics translation unit
-    (its sqrt in the Box-Muller draw may differ in the last bit), so the
-    comparison is to 1e-4 over a free-running horizon; resets and progress
-    must be identical."""
+    two paths run different instantiations of the fast-math step kernel (with
+    and without the epilogue), whose physics rounds differently in the last
+    bit (root state 4e-9 apart after the first step), and random steering
+    amplifies that; so the comparison is the north_star tolerance 1e-3 over 40
+    free-running steps, while resets and progress must be identical."""
     _cuda()
     import thormang_isaacgym_amd as tia
     from thormang_isaacgym_amd.tasks.base.vec_task import VecTask
-    envs = [tia.make(seed=21, task="Gogoro", num_envs=512, sim_device="cuda:0", rl_device="cuda:0")
-            for _ in range(2)]
+    # TG_SEAT_RECOMPOSE: the fused step re-composes its reset envs like the
+    # separate calls do, so the physics is the same on both sides (the
+    # in-place seat update has its own test above)
+    os.environ["TG_SEAT_RECOMPOSE"] = "1"
+    try:
+        envs = [tia.make(seed=21, task="Gogoro", num_envs=512, sim_device="cuda:0", rl_device="cuda:0")
+                for _ in range(2)]
+    finally:
+        del os.environ["TG_SEAT_RECOMPOSE"]
     f, u = envs
     g = torch.Generator(device="cuda:0").manual_seed(9)
     n_reset = 0
@@ -154,7 +198,7 @@ def test_gpu_gogoro_fused_step_matches_separate_calls():
         for x, y, what in ((f.obs_buf, u.obs_buf, "obs"), (f.rew_buf, u.rew_buf, "rew"),
                            (f.root_tensor, u.root_tensor, "root")):
             d = float((x - y).abs().max())
-            assert d <= 1e-4, (what, d)
+            assert d <= 1e-3, (what, d)
         n_reset += int(f.reset_buf.sum())
     assert n_reset > 0
 

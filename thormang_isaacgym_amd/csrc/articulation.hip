@@ -183,6 +183,21 @@ int compiled_hashes(uint64_t *out, int cap) {
     TG_FOR_EACH_MODEL(TG_HASH)
     return n;
 }
+#define TG_COMPOSE_ONLY(MODEL)                                                                            \
+    if (hash == MODEL::hash) {                                                                            \
+        hipLaunchKernelGGL(compose_kernel<MODEL>, dim3((a.N + COMPOSE_WPB - 1) / COMPOSE_WPB),            \
+                           dim3(64 * COMPOSE_WPB), 0, stream, a);                                         \
+        return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;                                          \
+    }
+int launch_compose_only(uint64_t hash, const StepArgs &a, hipStream_t stream) {
+    TG_FOR_EACH_MODEL(TG_COMPOSE_ONLY)
+    return TG_ERR_MODEL;
+}
+#define TG_TL(MODEL) if (hash == MODEL::hash) return MODEL::NTL;
+int model_tl(uint64_t hash) {
+    TG_FOR_EACH_MODEL(TG_TL)
+    return 0;
+}
 int model_kc(uint64_t hash) {
     TG_FOR_EACH_MODEL(TG_KC)
     return jit_kc(hash);

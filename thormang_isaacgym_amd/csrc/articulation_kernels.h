@@ -21,12 +21,25 @@ namespace tg {
 // floats (joint placement R (9) + t (3), then mass, com (3), inertia about the
 // com (6), 2 pad) at 24 g, then 12 floats (R, t) per contact shape.  A lane
 // takes a group's 22 inputs with 6 16-byte loads from one base address.
+// Models with translating locks (codegen translating_locks: the Gogoro seat
+// chain) append an extension at ext(): the lock group's mass moments at the
+// composed lock positions -- mass, first moment S (3), second moment about the
+// group origin Io (6: xx yy zz xy xz yz, rotated link inertias included) --
+// then per lock k (xk): its composed position q0, the mass m_k and first
+// moment S_k of the links below it, its axis w_k in the group frame; then the
+// placement translation t0 (3) of every group hanging below a lock (xag) and of
+// every shape of the lock group below one (xash), as composed.
 template <class M> struct CompLayout {
     static constexpr int GB = 24;
     static constexpr int xtree(int g) { return GB * g; }
     static constexpr int inertia(int g) { return GB * g + 12; }
     static constexpr int shape(int s) { return GB * M::NG + 12 * s; }
-    static_assert(M::KC == GB * M::NG + 12 * M::NS, "codegen KC");
+    static constexpr int ext() { return GB * M::NG + 12 * M::NS; }
+    static constexpr int xk(int k) { return ext() + 10 + 8 * k; }
+    static constexpr int xag(int j) { return ext() + 10 + 8 * M::NTL + 3 * j; }
+    static constexpr int xash(int j) { return ext() + 10 + 8 * M::NTL + 3 * M::NAG + 3 * j; }
+    static_assert(M::KC == GB * M::NG + 12 * M::NS + M::KX, "codegen KC");
+    static_assert(M::NTL == 0 || 10 + 8 * M::NTL + 3 * (M::NAG + M::NASH) <= M::KX, "codegen KX");
 };
 
 __device__ __forceinline__ float prop(const StepArgs &a, int f, int e, int d) {
@@ -94,23 +107,39 @@ __device__ __forceinline__ void target_prologue(const StepArgs &a, int e, int la
 // Prologue (tg_gogoro_step): gogoro_task.hip pre_kernel for env e on one lane
 // -- the same fp32 operations (no contraction / reassociation here either)
 // and the same Philox draw.
-__device__ __forceinline__ void gogoro_pre_prologue(const GogoroPre &g, int e, int D) {
+// the pre-physics values of env e: new action history ah[5], command, steering
+// position target, rear-wheel velocity target (nothing stored)
+__device__ __forceinline__ void gogoro_pre_values(const GogoroPre &g, int e, float *ah, float &cmd, float &tsteer,
+                                                  float &vrear) {
 #pragma clang fp contract(off) reassociate(off)
     const float x = g.actions[e];
     const float a = x < -g.clip_actions ? -g.clip_actions : (x > g.clip_actions ? g.clip_actions : x);
-    float *ah = g.action_history + 5 * (size_t)e;
-    const float h0 = ah[1], h1 = ah[2], h2 = ah[3], h3 = ah[4];
-    ah[0] = h0; ah[1] = h1; ah[2] = h2; ah[3] = h3; ah[4] = a;
+    const float *ah0 = g.action_history + 5 * (size_t)e;
+    ah[0] = ah0[1]; ah[1] = ah0[2]; ah[2] = ah0[3]; ah[3] = ah0[4]; ah[4] = a;
     const float m = g.max_steering_change, ms = g.max_steering;
     float da = a * m;
     da = da < -m ? -m : (da > m ? m : da);
     float c = g.curent_command[e] + da;
     c = c < -ms ? -ms : (c > ms ? ms : c);
-    g.curent_command[e] = c;
+    cmd = c;
     const U4 u = philox(U4{(uint32_t)e, g.c_lo, g.c_hi, 0x50524531u}, g.k0, g.k1);
     const float noise = g.noise_mean + gauss(u.x, u.y) * g.noise_std;
-    g.pos_target[(size_t)e * D + g.dof_steer] = c + g.steer_offsets[e] + noise;
-    g.vel_target[(size_t)e * D + g.dof_rear] = g.curent_speed[e];
+    tsteer = c + g.steer_offsets[e] + noise;
+    vrear = g.curent_speed[e];
+}
+__device__ __forceinline__ void gogoro_pre_store(const GogoroPre &g, int e, int D, const float *ah, float cmd,
+                                                 float tsteer, float vrear) {
+    float *h = g.action_history + 5 * (size_t)e;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) h[k] = ah[k];
+    g.curent_command[e] = cmd;
+    g.pos_target[(size_t)e * D + g.dof_steer] = tsteer;
+    g.vel_target[(size_t)e * D + g.dof_rear] = vrear;
+}
+__device__ __forceinline__ void gogoro_pre_prologue(const GogoroPre &g, int e, int D) {
+    float ah[5], cmd, ts, vr;
+    gogoro_pre_values(g, e, ah, cmd, ts, vr);
+    gogoro_pre_store(g, e, D, ah, cmd, ts, vr);
 }
 
 // one wavefront's compose scratch
@@ -329,6 +358,61 @@ template <class M> __device__ __forceinline__ void compose_env(const StepArgs &a
 #pragma unroll
             for (int k = 0; k < 9; ++k) cx[k] = Rx.a[k];
             cx[9] = t.x; cx[10] = t.y; cx[11] = t.z;
+            if constexpr (M::NTL > 0) {   // composed placement of a group below a translating lock
+#pragma unroll
+                for (int j = 0; j < M::NAG; ++j)
+                    if (M::ag_group[j] == g) {
+                        c[CL::xag(j)] = t.x; c[CL::xag(j) + 1] = t.y; c[CL::xag(j) + 2] = t.z;
+                    }
+            }
+        }
+    }
+    if constexpr (M::NTL > 0) {
+        // translating-lock extension: the lock group's mass moments (pre-Q
+        // group frame) and, per lock, the moments of the links below it
+        constexpr int NV = 10 + 4 * M::NTL;
+        float v[NV];
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[k] = 0.f;
+        if (lact && M::link_group[l] == M::tl_group) {
+            const float ml = LM[l][0];
+            const V3 pc = v3(LM[l][1], LM[l][2], LM[l][3]);
+            const float d2 = dot(pc, pc);
+            v[0] = ml;
+            v[1] = ml * pc.x; v[2] = ml * pc.y; v[3] = ml * pc.z;
+            v[4] = LM[l][4] + ml * (d2 - pc.x * pc.x);
+            v[5] = LM[l][5] + ml * (d2 - pc.y * pc.y);
+            v[6] = LM[l][6] + ml * (d2 - pc.z * pc.z);
+            v[7] = LM[l][7] - ml * pc.x * pc.y;
+            v[8] = LM[l][8] - ml * pc.x * pc.z;
+            v[9] = LM[l][9] - ml * pc.y * pc.z;
+#pragma unroll
+            for (int k = 0; k < M::NTL; ++k)
+                if ((M::link_tl[l] >> k) & 1) {
+                    v[10 + 4 * k] = ml;
+                    v[11 + 4 * k] = ml * pc.x; v[12 + 4 * k] = ml * pc.y; v[13 + 4 * k] = ml * pc.z;
+                }
+        }
+        wave_sum_n<NV>(v);
+        if (lane == 0) {
+            float *x = c + CL::ext();
+#pragma unroll
+            for (int k = 0; k < 10; ++k) x[k] = v[k];
+#pragma unroll
+            for (int k = 0; k < M::NTL; ++k) {
+                const int lk = M::tl_link[k], dk = M::tl_dof[k];
+                M3 Rp;
+                V3 Pp;
+                ldT(M::link_parent[lk], Rp, Pp);
+                const float *o = M::link_origin[lk];
+                const float *ax = M::link_axis[lk];
+                const V3 w = mul(Rp, mul(ld9(o), v3(ax[0], ax[1], ax[2])));
+                float *xk = c + CL::xk(k);
+                xk[0] = 0.5f * (prop(a, TG_PROP_LOWER, e, dk) + prop(a, TG_PROP_UPPER, e, dk));   // as the FK above
+                xk[1] = v[10 + 4 * k];
+                xk[2] = v[11 + 4 * k]; xk[3] = v[12 + 4 * k]; xk[4] = v[13 + 4 * k];
+                xk[5] = w.x; xk[6] = w.y; xk[7] = w.z;
+            }
         }
     }
     TG_CPROF(2)
@@ -342,6 +426,13 @@ template <class M> __device__ __forceinline__ void compose_env(const StepArgs &a
 #pragma unroll
         for (int k = 0; k < 9; ++k) cs[k] = Rx.a[k];
         cs[9] = t.x; cs[10] = t.y; cs[11] = t.z;
+        if constexpr (M::NTL > 0) {   // composed pose of a lock-group shape below a translating lock
+#pragma unroll
+            for (int j = 0; j < M::NASH; ++j)
+                if (M::ash_shape[j] == sh) {
+                    c[CL::xash(j)] = t.x; c[CL::xash(j) + 1] = t.y; c[CL::xash(j) + 2] = t.z;
+                }
+        }
     }
     if (lane == 0) a.dirty[e] = 0;
     TG_CPROF(3)
@@ -353,7 +444,7 @@ template <class M> __global__ __launch_bounds__(64 * COMPOSE_WPB) void compose_k
     const bool dirty = e < a.N && a.dirty[e] != 0;   // read before the prologue: one memory latency
     if (a.cnext && blockIdx.x == 0 && threadIdx.x == 0) *a.cnext = 0;   // the reset list the next epilogue fills
     if (a.pm_actions && !a.pm_in_step && e < a.N) target_prologue(a, e, threadIdx.x % 64);
-    if (a.gp.actions && e < a.N && threadIdx.x % 64 == 0) gogoro_pre_prologue(a.gp, e, a.D);
+    if (a.gp.actions && !a.gp_in_step && e < a.N && threadIdx.x % 64 == 0) gogoro_pre_prologue(a.gp, e, a.D);
     if (!dirty) return;
     __shared__ ComposeLds<M> cs[COMPOSE_WPB];
     compose_env<M>(a, e, threadIdx.x % 64, cs[wv]);
@@ -370,7 +461,7 @@ template <class M> __global__ __launch_bounds__(64) void compose_list_kernel(Ste
     const int n = a.ccount ? *a.ccount : 0;   // issued first: its latency overlaps the prologue
     if (a.cnext && blockIdx.x == 0 && lane == 0) *a.cnext = 0;
     const int e0 = blockIdx.x * COMPOSE_WPB + lane;
-    if (a.gp.actions && lane < COMPOSE_WPB && e0 < a.N) gogoro_pre_prologue(a.gp, e0, a.D);
+    if (a.gp.actions && !a.gp_in_step && lane < COMPOSE_WPB && e0 < a.N) gogoro_pre_prologue(a.gp, e0, a.D);
     if ((int)blockIdx.x >= n) return;
     __shared__ ComposeLds<M> cs;
     for (int i = blockIdx.x; i < n; i += gridDim.x) compose_env<M>(a, a.clist[i], lane, cs);
@@ -785,6 +876,95 @@ struct WalkPost {
     }
 };
 
+// ---------------------------------------------------------------- translating locks
+// The lock group's composite and the placements below its translating locks
+// (CompLayout ext) at new lock positions q[k], from the moments the last
+// compose stored -- what a compose at those positions would write, without
+// re-composing the env.  Moving lock k by dq_k translates the links below it
+// by u_k = dq_k w_k, so with D_l = sum of the u_k above link l:
+//   S'  = S + sum_k m_k u_k
+//   Io' = Io + sum_k [2 (S_k . u_k) E - (S_k u_k^T + u_k S_k^T)]
+//            + sum_{k,k'} m_{max(k,k')} ((u_k . u_k') E - u_k u_k'^T)
+// (nested locks: the links below both are the deeper one's), c' = S'/m,
+// I_com = Io' - m (|c'|^2 E - c' c'^T); placements and shape poses below a lock
+// move by the sum of its u_k, in the joint-aligned frame of the lock group.
+// c: the env's composite cache (written); xe: its extension (read)
+template <class M> __device__ __forceinline__ void tl_update(float *c, const float *xe, const float *q) {
+    using CL = CompLayout<M>;
+    constexpr int gt = M::tl_group;
+    const float *x = xe;
+    auto X = [&](int off) { return xe + (off - CL::ext()); };
+    const float m = x[0];
+    V3 S = v3(x[1], x[2], x[3]);
+    float Io[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) Io[k] = x[4 + k];
+    V3 u[M::NTL];
+    float mk[M::NTL];
+#pragma unroll
+    for (int k = 0; k < M::NTL; ++k) {
+        const float *xk = X(CL::xk(k));
+        const float dq = q[k] - xk[0];
+        mk[k] = xk[1];
+        const V3 Sk = v3(xk[2], xk[3], xk[4]);
+        u[k] = dq * v3(xk[5], xk[6], xk[7]);
+        S = S + mk[k] * u[k];
+        const float su = dot(Sk, u[k]);
+        Io[0] += 2.f * (su - Sk.x * u[k].x);
+        Io[1] += 2.f * (su - Sk.y * u[k].y);
+        Io[2] += 2.f * (su - Sk.z * u[k].z);
+        Io[3] -= Sk.x * u[k].y + u[k].x * Sk.y;
+        Io[4] -= Sk.x * u[k].z + u[k].x * Sk.z;
+        Io[5] -= Sk.y * u[k].z + u[k].y * Sk.z;
+    }
+#pragma unroll
+    for (int k = 0; k < M::NTL; ++k)
+#pragma unroll
+        for (int j = 0; j < M::NTL; ++j) {
+            const float mm = mk[k > j ? k : j];
+            const float uu = dot(u[k], u[j]);
+            Io[0] += mm * (uu - u[k].x * u[j].x);
+            Io[1] += mm * (uu - u[k].y * u[j].y);
+            Io[2] += mm * (uu - u[k].z * u[j].z);
+            Io[3] -= mm * u[k].x * u[j].y;
+            Io[4] -= mm * u[k].x * u[j].z;
+            Io[5] -= mm * u[k].y * u[j].z;
+        }
+    const V3 cc = (m > 0.f ? 1.0f / m : 0.f) * S;
+    const float c2 = dot(cc, cc);
+    float gI[6] = {Io[0] - m * (c2 - cc.x * cc.x), Io[1] - m * (c2 - cc.y * cc.y), Io[2] - m * (c2 - cc.z * cc.z),
+                   Io[3] + m * cc.x * cc.y, Io[4] + m * cc.x * cc.z, Io[5] + m * cc.y * cc.z};
+    const M3 Q = M3{{M::gq[gt][0], M::gq[gt][1], M::gq[gt][2], M::gq[gt][3], M::gq[gt][4], M::gq[gt][5],
+                     M::gq[gt][6], M::gq[gt][7], M::gq[gt][8]}};
+    const V3 cq = mulT(Q, cc);
+    float gIq[6];
+    sym_from(gIq, mul(mul(transpose(Q), sym_to(gI)), Q));
+    float *ci = c + CL::inertia(gt);
+    ci[0] = m;
+    ci[1] = cq.x; ci[2] = cq.y; ci[3] = cq.z;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) ci[4 + k] = gIq[k];
+    auto shift = [&](int mask) {
+        V3 d = v3(0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < M::NTL; ++k)
+            if ((mask >> k) & 1) d = d + u[k];
+        return mulT(Q, d);
+    };
+#pragma unroll
+    for (int j = 0; j < M::NAG; ++j) {
+        const V3 t = v3(X(CL::xag(j))[0], X(CL::xag(j))[1], X(CL::xag(j))[2]) + shift(M::ag_mask[j]);
+        float *cx = c + CL::xtree(M::ag_group[j]);
+        cx[9] = t.x; cx[10] = t.y; cx[11] = t.z;
+    }
+#pragma unroll
+    for (int j = 0; j < M::NASH; ++j) {
+        const V3 t = v3(X(CL::xash(j))[0], X(CL::xash(j))[1], X(CL::xash(j))[2]) + shift(M::ash_mask[j]);
+        float *cs = c + CL::shape(M::ash_shape[j]);
+        cs[9] = t.x; cs[10] = t.y; cs[11] = t.z;
+    }
+}
+
 // ---------------------------------------------------------------- fused Gogoro post-physics
 // tg_gogoro_step's last simulate: gogoro_task.hip post_kernel (progress,
 // masked resets with their property writes and dirty flag, observations,
@@ -810,15 +990,37 @@ struct GogoroPost {
         const tg_gogoro_buffers &b = pa.b;
         const bool lead = sub == 0;
         const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
-        // ---- inputs, one batch
+        // ---- inputs, one batch (with the translating-lock extension a reset
+        // needs: its latency overlaps the draws instead of following them)
+        constexpr int XN = M::NTL > 0 ? M::KX : 1;
+        float xe[XN];
+        if constexpr (M::NTL > 0) {
+            const float *xs = a.comp + (size_t)e * M::KC + CompLayout<M>::ext();
+#pragma unroll
+            for (int k = 0; k < XN; ++k) xe[k] = (lead && pa.tl_inplace) ? xs[k] : 0.f;
+        }
         const int64_t prog1 = b.progress_buf[e] + 1;
         const bool rflag = b.reset_buf[e] != 0;
         float rt[13], ah[5];
 #pragma unroll
         for (int k = 0; k < 13; ++k) rt[k] = rt0[k];
+        float cmdc;
+        if constexpr (ParLayout<M>::TPN > 0) {
+            if (a.gp_in_step) {   // this kernel's pre-physics values (LDS), not yet-unflushed HBM
 #pragma unroll
-        for (int k = 0; k < 5; ++k) ah[k] = b.action_history[5 * (size_t)e + k];
-        float yawc = b.yaw_command[e], cmdc = b.curent_command[e], imu = b.imu_offsets[e];
+                for (int k = 0; k < 5; ++k) ah[k] = s(ParLayout<M>::TP + k);
+                cmdc = s(ParLayout<M>::TP + 5);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 5; ++k) ah[k] = b.action_history[5 * (size_t)e + k];
+                cmdc = b.curent_command[e];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 5; ++k) ah[k] = b.action_history[5 * (size_t)e + k];
+            cmdc = b.curent_command[e];
+        }
+        float yawc = b.yaw_command[e], imu = b.imu_offsets[e];
         // ---- draws: lane l < 8 block l, the lead lane also block 8 (command resample)
         float v[3], v8[3];
         gogoro_post_block(sub < 8 ? sub : 7, e, pa.c_lo, pa.c_hi, k0, k1, v);
@@ -893,8 +1095,25 @@ struct GogoroPost {
                     u_aff(p.steering_damping_range[0], p.steering_damping_range[1], r[10]);
                 prop[TG_PROP_EFFORT * ND + st] = p.steer_effort;
                 prop[TG_PROP_VELOCITY * ND + st] = p.steer_velocity;
-                b.env_dirty[e] = 1;
-                if (pa.reset_list) pa.reset_list[atomicAdd(pa.reset_count, 1)] = e;   // for compose_list_kernel
+                bool inplace = false;
+                if constexpr (M::NTL > 0) inplace = pa.tl_inplace != 0;
+                if (inplace) {
+                    // the new seat windows only translate the rider: update the
+                    // composite in place (tl_update) -- no compose for this env
+                    constexpr int NT = M::NTL > 0 ? M::NTL : 1;
+                    float qn[NT];
+#pragma unroll
+                    for (int k = 0; k < M::NTL; ++k) {
+                        qn[k] = 0.f;
+#pragma unroll
+                        for (int j = 0; j < 3; ++j)
+                            if (seat[j] == M::tl_dof[k]) qn[k] = 0.5f * (cv[j] + (cv[j] + 0.0001f));
+                    }
+                    if constexpr (M::NTL > 0) tl_update<M>(a.comp + (size_t)e * M::KC, xe, qn);
+                } else {
+                    b.env_dirty[e] = 1;
+                    if (pa.reset_list) pa.reset_list[atomicAdd(pa.reset_count, 1)] = e;   // for compose_list_kernel
+                }
                 b.curent_command[e] = 0.0f;
 #pragma unroll
                 for (int k = 0; k < 5; ++k) b.action_history[5 * (size_t)e + k] = 0.0f;

@@ -129,6 +129,11 @@ template <class M> struct ParLayout {
     static constexpr int CGP = SHP + 2 * M::NSA;     // per contact group: world R (9), p (3)
     static constexpr int CGV = CGP + 12 * M::NCG;    // per contact group: free velocity (6)
     static constexpr int FLG = CGV + 6 * M::NCG;     // a drive exceeded its effort limit
+    // the Gogoro pre-physics values computed in the step kernel (models with
+    // the fused Gogoro epilogue): action history (5), command, steering target,
+    // rear-wheel velocity target
+    static constexpr int TPN = (M::FUSED & 2) ? 8 : 0;
+    static constexpr int TP = FLG + 1;
     // per-block ints after the env area
     static constexpr int T_GI = 0;
     static constexpr int T_CPATH = T_GI + M::NG * GIW;                 // [NCG][MAXD]
@@ -140,9 +145,9 @@ template <class M> struct ParLayout {
     // its parent (I^a 21 at +0, p^a 6 at +24) and pass 3 its acceleration (+0)
     // into a separate 32-float block, so pass 1's rigid inertias and bias
     // forces survive and the drive-clamp rerun starts at pass 2
-    static constexpr int CB = (FLG + 1 + 3) & ~3;
+    static constexpr int CB = (TP + TPN + 3) & ~3;
     static constexpr bool SEPC = ((size_t)M::EPB * (CB + 32 * M::NG) + T_TOTAL) * 4 <= 160 * 1024;
-    static constexpr int TOTAL = SEPC ? CB + 32 * M::NG : FLG + 1;
+    static constexpr int TOTAL = SEPC ? CB + 32 * M::NG : TP + TPN;
     static constexpr int ES = (TOTAL + 3) & ~3;      // env stride (16-byte aligned)
     template <int EPB> static constexpr size_t bytes() { return ((size_t)EPB * ES + T_TOTAL) * 4; }
 };
@@ -476,6 +481,12 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         // the walk pre-physics inside the step (tg_walk_step): the target from the action
         x[7] = a.pm_in_step ? pm_target(a, d, pm_clamp(a, a.pm_actions[ed])) : a.pos_tgt[ed];
         x[8] = a.vel_tgt[ed];
+        if constexpr (PL::TPN > 0) {   // the Gogoro pre-physics inside the step (tg_gogoro_step)
+            if (a.gp_in_step) {
+                if (d == a.gp.dof_steer) x[7] = s(PL::TP + 6);
+                if (d == a.gp.dof_rear) x[8] = s(PL::TP + 7);
+            }
+        }
         x[9] = a.act ? a.act[ed] : 0.f;
     };
     // pass 2: the children's contributions of the lane's group, n = the step's
@@ -499,6 +510,18 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
             pA = pA + cv[c];
         }
     };
+    if constexpr (PL::TPN > 0) {
+        if (a.gp_in_step && lead) {   // the Gogoro pre-physics (tg_gogoro_step) on the env's lead lane
+            float ah[5], cmd, ts, vr;
+            gogoro_pre_values(a.gp, e, ah, cmd, ts, vr);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) s(PL::TP + k) = ah[k];
+            s(PL::TP + 5) = cmd;
+            s(PL::TP + 6) = ts;
+            s(PL::TP + 7) = vr;
+            if (owner) gogoro_pre_store(a.gp, e, D, ah, cmd, ts, vr);
+        }
+    }
     TG_SYNC();
     TG_PROF(0)
 

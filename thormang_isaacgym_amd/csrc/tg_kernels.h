@@ -69,6 +69,9 @@ struct StepArgs {
     int compose_list;
     const int *clist, *ccount;
     int *cnext;
+    // gp_in_step: the Gogoro pre-physics (gp) runs at the start of the step
+    // kernel (lead lane; values through the env's LDS) instead of in compose
+    int gp_in_step;
 };
 
 // tg_walk_step's fused post-physics epilogue (articulation.hip WalkPost)
@@ -84,6 +87,7 @@ struct GogoroPostArgs {
     tg_gogoro_buffers b;
     uint32_t c_lo, c_hi;
     int *reset_list, *reset_count;   // [N] ids of the envs reset (and made dirty) / their count, or null
+    int tl_inplace;                  // the epilogue updates a reset env's composite itself (M::NTL > 0)
 };
 #ifndef __HIPCC_RTC__   // host launchers (not part of a hipRTC unit, jit.cpp)
 // compose + step kernel with the Gogoro post-physics fused in; returns 1 when
@@ -104,6 +108,8 @@ int launch_body_states(uint64_t hash, const float *root, const float *dof, int n
 int launch_rb_forces(uint64_t hash, const float *root, const float *dof, int n, const float *mass_scale,
                      const float *forces, const float *torques, int space, float *out, hipStream_t stream);
 int model_kc(uint64_t hash);
+int model_tl(uint64_t hash);
+int launch_compose_only(uint64_t hash, const StepArgs &a, hipStream_t stream);   // every dirty env, no step   // translating locks of a compiled model (codegen translating_locks), 0 otherwise
 
 // run-time compiled models (jit.cpp, tg_model_jit): the launchers above fall
 // through to these when no compiled-in specialisation matches the hash

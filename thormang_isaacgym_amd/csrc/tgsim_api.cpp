@@ -81,6 +81,7 @@ struct tg_sim {
     bool post_unfused = false;   // tg_gogoro_step: separate post-physics launch (TG_POST_UNFUSED=1)
     bool always_compose = false; // never skip the compose launch (TG_ALWAYS_COMPOSE=1)
     bool pre_in_compose = false; // tg_walk_step: pre-physics in the compose launch, not the step kernel (TG_PRE_IN_COMPOSE=1)
+    bool no_inplace = false;     // tg_gogoro_step: reset envs re-composed, not updated in place (TG_SEAT_RECOMPOSE=1)
     int timing = 0;          // period (0: off)
     int64_t timing_count = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending, ev_free;
@@ -195,6 +196,7 @@ int tg_sim_create(const tg_model_desc *m, const tg_sim_params *params, int32_t n
     if (const char *u = getenv("TG_POST_UNFUSED")) s->post_unfused = u[0] == '1';
     if (const char *u = getenv("TG_ALWAYS_COMPOSE")) s->always_compose = u[0] == '1';
     if (const char *u = getenv("TG_PRE_IN_COMPOSE")) s->pre_in_compose = u[0] == '1';
+    if (const char *u = getenv("TG_SEAT_RECOMPOSE")) s->no_inplace = u[0] == '1';
     s->device = device;
     s->N = num_envs;
     s->D = m->num_dofs;
@@ -457,8 +459,9 @@ static int simulate_args(tg_sim *s, const tg::StepArgs &a_in, const tg::WalkPost
     // the compose launch: every dirty env (host-side changes possible), the
     // last fused epilogue's reset list, the task prologue alone, or none
     const bool walk_prologue = a.pm_actions && !a.pm_in_step;
+    const bool gogoro_prologue = a.gp.actions && !a.gp_in_step;
     const bool full = s->dirty_possible || s->always_compose || walk_prologue;
-    a.skip_compose = !full && !s->list_pending && !a.gp.actions;
+    a.skip_compose = !full && !s->list_pending && !gogoro_prologue;
     a.compose_list = !full && !a.skip_compose;
     a.cnext = s->ccount + s->list_cur;
     if (a.compose_list && s->list_pending) {
@@ -494,8 +497,8 @@ static int simulate_args(tg_sim *s, const tg::StepArgs &a_in, const tg::WalkPost
         if (!a.compose_list) s->dirty_possible = false;
         s->list_pending = false;
     }
-    if (gp) {   // the Gogoro epilogue's resets rewrite properties
-        if (gp->reset_list) {   // ... and are listed for the next compose
+    if (gp && !gp->tl_inplace) {   // the Gogoro epilogue's resets rewrite properties
+        if (gp->reset_list) {       // ... and are listed for the next compose
             s->list_pending = true;
             s->list_cur = 1 - s->list_cur;
         } else {
@@ -535,6 +538,22 @@ int tg_rigid_body_states(tg_sim *s, float *out) {
     if (!out) return fail(TG_ERR_ARG, "tg_rigid_body_states: null output");
     if (int rc = tg::launch_body_states(s->hash, s->root, s->dof, (int)s->N, out, s->stream))
         return fail(rc, "rigid-body state launch failed");
+    return TG_OK;
+}
+
+int tg_composite(tg_sim *s, float *out, int32_t recompose) {
+    if (int rc = check_sim(s)) return rc;
+    if (!out) return fail(TG_ERR_ARG, "tg_composite: null output");
+    DeviceGuard dg(s->device);
+    if (recompose) {
+        HIPCHK(hipMemsetAsync(s->dirty, 1, s->N, s->stream));
+        tg::StepArgs a = step_args(s);
+        a.cnext = s->ccount + s->list_cur;
+        if (int rc = tg::launch_compose_only(s->hash, a, s->stream)) return fail(rc, "compose launch failed");
+        s->list_pending = false;
+        s->dirty_possible = false;
+    }
+    HIPCHK(hipMemcpyAsync(out, s->comp, (size_t)s->N * s->KC * sizeof(float), hipMemcpyDeviceToDevice, s->stream));
     return TG_OK;
 }
 
@@ -634,11 +653,18 @@ int tg_gogoro_step(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_buffers
             g.c_hi = (uint32_t)(counter_pre >> 32);
         }
         if (i == n_simulate - 1 && !s->post_unfused) {   // post-physics fused into the last step kernel
+            // models whose resets only move translating locks (the seat chain)
+            // update their composites in the epilogue; others list their resets
+            const bool inplace = tg::model_tl(s->hash) > 0 && !s->no_inplace;
             const tg::GogoroPostArgs gp{*p, *b, (uint32_t)counter_post, (uint32_t)(counter_post >> 32),
-                                        s->clist + (size_t)s->list_cur * s->N, s->ccount + s->list_cur};
+                                        inplace ? nullptr : s->clist + (size_t)s->list_cur * s->N,
+                                        inplace ? nullptr : s->ccount + s->list_cur, inplace ? 1 : 0};
+            // one launch: the pre-physics too runs in the step kernel
+            a.gp_in_step = (n_simulate == 1 && !s->pre_in_compose) ? 1 : 0;
             const int rc = simulate_args(s, a, nullptr, &gp);
             if (rc == 0) return TG_OK;
             if (rc < 0) return rc;
+            a.gp_in_step = 0;   // no fused instantiation: the prologue rides in compose
         }
         if (int rc = simulate_args(s, a)) return rc;
     }

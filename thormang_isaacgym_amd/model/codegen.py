@@ -95,6 +95,47 @@ def fused_tasks(m: Model) -> int:
     return 2 if m.name in FUSED_GOGORO_MODELS else 0
 
 
+def translating_locks(m: Model, a: dict) -> dict:
+    """The locked prismatic joints inside one rigid group whose windows a fused
+    task epilogue moves at every reset (the Gogoro seat offsets base_z ->
+    base_x -> base_y, tasks/gogoro_new.py:562-572): moving such a lock only
+    translates the links below it, so the epilogue updates the group's
+    composite (mass moments) and the placements of the groups hanging below
+    instead of re-composing the env (csrc GogoroPost).  Only for models with
+    the fused Gogoro epilogue; the joints must form one nested chain in one
+    group.  Returns the tables codegen emits (NTL = 0: none)."""
+    none = dict(NTL=0, tl_link=[0], tl_dof=[0], tl_group=0, link_tl=[0] * m.num_bodies,
+                ag=[], ashape=[], KX=0)
+    if not (fused_tasks(m) & 2):
+        return none
+    L = m.num_bodies
+    lpar = [int(x) for x in a["link_parent"]]
+    lgrp = [int(x) for x in a["link_group"]]
+    groot = set(int(x) for x in a["group_root"])
+    tl = [l for l in range(L) if l not in groot and int(a["link_jtype"][l]) == 2 and int(a["link_dof"][l]) >= 0
+          and int(a["dof_locked"][int(a["link_dof"][l])])]
+    if not tl:
+        return none
+    assert len(tl) <= 3 and len({lgrp[l] for l in tl}) == 1, "translating locks: one chain of <= 3 in one group"
+
+    def below(l, j):   # link l in the subtree of link j (inclusive)
+        while l >= 0:
+            if l == j:
+                return True
+            l = lpar[l]
+        return False
+    for i in range(1, len(tl)):
+        assert below(tl[i], tl[i - 1]), "translating locks must be nested"
+    link_tl = [sum(1 << k for k, j in enumerate(tl) if below(l, j)) for l in range(L)]
+    gr = [int(x) for x in a["group_root"]]
+    ag = [(g, link_tl[lpar[gr[g]]]) for g in range(1, m.num_groups) if link_tl[lpar[gr[g]]]]
+    ashape = [(s, link_tl[int(l)]) for s, l in enumerate(a["shape_link"])
+              if link_tl[int(l)] and lgrp[int(l)] == lgrp[tl[0]]]
+    kx = 10 + 8 * len(tl) + 3 * len(ag) + 3 * len(ashape)
+    return dict(NTL=len(tl), tl_link=tl, tl_dof=[int(a["link_dof"][l]) for l in tl], tl_group=lgrp[tl[0]],
+                link_tl=link_tl, ag=ag, ashape=ashape, KX=(kx + 3) & ~3)
+
+
 def emit(m: Model, cname: str) -> str:
     d = ModelDesc(m)
     a = d.arrays
@@ -146,6 +187,7 @@ def emit(m: Model, cname: str) -> str:
         wdepth[l] = 0 if lpar[l] < 0 else wdepth[lpar[l]] + 1
     glinks = [[l for l in range(L) if lgrp[l] == g] for g in range(G)]
     maxgl = max(len(x) for x in glinks)
+    tlc = translating_locks(m, a)
     maxc = max(1, max(len(c) for c in children))
     lines = [
         f"// AUTO-GENERATED by thormang_isaacgym_amd/model/codegen.py from model '{m.name}'. Do not edit.",
@@ -153,7 +195,17 @@ def emit(m: Model, cname: str) -> str:
         f"struct {cname} {{",
         f"  static constexpr unsigned long long hash = 0x{d.hash:016x}ULL;",
         f"  static constexpr int NG = {G}, NL = {L}, ND = {D}, NS = {S > 0 and S or 0}, NSA = {max(S, 1)};",
-        f"  static constexpr int KC = {24 * G + 12 * S};  // per-env composite floats (env-major, csrc CompLayout)",
+        f"  static constexpr int KC = {24 * G + 12 * S + tlc['KX']};  // per-env composite floats (env-major, csrc CompLayout)",
+        f"  static constexpr int KX = {tlc['KX']};  // of which the translating-lock extension (codegen translating_locks)",
+        f"  static constexpr int NTL = {tlc['NTL']}, tl_group = {tlc['tl_group']}, NAG = {len(tlc['ag'])}, "
+        f"NASH = {len(tlc['ashape'])};",
+        f"  static constexpr int tl_link[{max(tlc['NTL'], 1)}] = {_arr(tlc['tl_link'])};",
+        f"  static constexpr int tl_dof[{max(tlc['NTL'], 1)}] = {_arr(tlc['tl_dof'])};",
+        f"  static constexpr int link_tl[{L}] = {_arr(tlc['link_tl'])};",
+        f"  static constexpr int ag_group[{max(len(tlc['ag']), 1)}] = {_arr([x[0] for x in tlc['ag']] or [0])};",
+        f"  static constexpr int ag_mask[{max(len(tlc['ag']), 1)}] = {_arr([x[1] for x in tlc['ag']] or [0])};",
+        f"  static constexpr int ash_shape[{max(len(tlc['ashape']), 1)}] = {_arr([x[0] for x in tlc['ashape']] or [0])};",
+        f"  static constexpr int ash_mask[{max(len(tlc['ashape']), 1)}] = {_arr([x[1] for x in tlc['ashape']] or [0])};",
         f"  static constexpr int NROWS = {sum(n + 3 for n in nrows_n)};  // contact rows (normals + 3 friction per shape)",
         f"  static constexpr int parent[{G}] = {_arr(a['group_parent'])};",
         f"  static constexpr int gdof[{G}] = {_arr(gdof)};",
