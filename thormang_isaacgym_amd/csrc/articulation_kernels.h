@@ -701,13 +701,15 @@ namespace tg {
 // translation unit's (fast-math) ones.
 struct WalkPost {
     static constexpr bool on = true;
+    static constexpr int NPRE = 0;
     using Args = WalkPostArgs;
     static __device__ __forceinline__ float clampw(float x, float lo, float hi) {
         return x < lo ? lo : (x > hi ? hi : x);
     }
     template <class M, int LPE>
     static __device__ __forceinline__ void epilogue(const Args &pa, const StepArgs &a, const LE &s, int e, bool owner,
-                                                    int sub, const float *rt0, float *root, float *dofs) {
+                                                    int sub, const float *rt0, float *root, float *dofs,
+                                                    const float *) {
 #pragma clang fp contract(off) reassociate(off)
         constexpr int D = M::ND;
         constexpr int NR = (D + LPE - 1) / LPE;
@@ -979,9 +981,30 @@ template <class M> __device__ __forceinline__ void tl_update(float *c, const flo
 struct GogoroPost {
     static constexpr bool on = true;
     using Args = GogoroPostArgs;
+    // the translating-lock extension of an env the previous step reset (its
+    // reset happens in this epilogue), LPE lanes x NPRE floats, loaded at
+    // kernel start so its latency hides behind the whole step
+    static constexpr int NPRE = 5;
+    template <class M, int LPE>
+    static __device__ __forceinline__ void prefetch(const Args &pa, const StepArgs &a, int e, int sub, float *x) {
+#pragma unroll
+        for (int k = 0; k < NPRE; ++k) x[k] = 0.f;
+        if constexpr (M::NTL > 0) {
+            static_assert(M::KX <= NPRE * LPE, "extension prefetch: KX <= NPRE x LPE");
+            if (pa.tl_inplace && pa.b.reset_buf[e] != 0) {
+                const float *xs = a.comp + (size_t)e * M::KC + CompLayout<M>::ext();
+#pragma unroll
+                for (int k = 0; k < NPRE; ++k) {
+                    const int i = sub * NPRE + k;
+                    if (i < M::KX) x[k] = xs[i];
+                }
+            }
+        }
+    }
     template <class M, int LPE>
     static __device__ __forceinline__ void epilogue(const Args &pa, const StepArgs &a, const LE &s, int e, bool owner,
-                                                    int sub, const float *rt0, float *root, float *dofs) {
+                                                    int sub, const float *rt0, float *root, float *dofs,
+                                                    const float *xpre) {
 #pragma clang fp contract(off) reassociate(off)
         constexpr int D = M::ND;
         constexpr int NR = (D + LPE - 1) / LPE;
@@ -990,15 +1013,21 @@ struct GogoroPost {
         const tg_gogoro_buffers &b = pa.b;
         const bool lead = sub == 0;
         const uint32_t k0 = (uint32_t)p.seed, k1 = (uint32_t)(p.seed >> 32);
-        // ---- inputs, one batch (with the translating-lock extension a reset
-        // needs: its latency overlaps the draws instead of following them)
-        constexpr int XN = M::NTL > 0 ? M::KX : 1;
-        float xe[XN];
+        // ---- the prefetched extension to the env's dead Delassus slots (read
+        // by the lead lane if the env resets)
         if constexpr (M::NTL > 0) {
-            const float *xs = a.comp + (size_t)e * M::KC + CompLayout<M>::ext();
 #pragma unroll
-            for (int k = 0; k < XN; ++k) xe[k] = (lead && pa.tl_inplace) ? xs[k] : 0.f;
+            for (int k = 0; k < NPRE; ++k) {
+                const int i = sub * NPRE + k;
+                if (i < M::KX) s(ParLayout<M>::W + i) = xpre[k];
+            }
+            static_assert(M::KX <= ParLayout<M>::K * ParLayout<M>::K + 8 * ParLayout<M>::K,
+                          "the extension fits the dead Delassus / row slots");
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // the env's lanes share a wavefront
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
+        // ---- inputs, one batch
         const int64_t prog1 = b.progress_buf[e] + 1;
         const bool rflag = b.reset_buf[e] != 0;
         float rt[13], ah[5];
@@ -1109,7 +1138,7 @@ struct GogoroPost {
                         for (int j = 0; j < 3; ++j)
                             if (seat[j] == M::tl_dof[k]) qn[k] = 0.5f * (cv[j] + (cv[j] + 0.0001f));
                     }
-                    if constexpr (M::NTL > 0) tl_update<M>(a.comp + (size_t)e * M::KC, xe, qn);
+                    if constexpr (M::NTL > 0) tl_update<M>(a.comp + (size_t)e * M::KC, s.b + ParLayout<M>::W, qn);
                 } else {
                     b.env_dirty[e] = 1;
                     if (pa.reset_list) pa.reset_list[atomicAdd(pa.reset_count, 1)] = e;   // for compose_list_kernel

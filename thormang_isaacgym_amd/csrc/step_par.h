@@ -301,6 +301,7 @@ __device__ __forceinline__ float ground_at(const StepArgs &a, float x, float y, 
 struct NoPost {
     struct Args {};
     static constexpr bool on = false;
+    static constexpr int NPRE = 0;   // floats per lane an epilogue prefetches at kernel start
 };
 
 // inverse of the group -> dof map: group of dof d, -1 for a locked dof
@@ -510,6 +511,9 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
             pA = pA + cv[c];
         }
     };
+    // an epilogue's inputs it wants in flight for the whole step (P::prefetch)
+    float xpre[P::NPRE > 0 ? P::NPRE : 1];
+    if constexpr (P::NPRE > 0) P::template prefetch<M, LPE>(pa, a, e, sub, xpre);
     if constexpr (PL::TPN > 0) {
         if (a.gp_in_step && lead) {   // the Gogoro pre-physics (tg_gogoro_step) on the env's lead lane
             float ah[5], cmd, ts, vr;
@@ -1465,7 +1469,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         const V3 wwo = mul(R, v0.w);
         const V3 vco = mul(R, v0.v) + cross(wwo, mul(R, c0));
         const float rt[13] = {pos.x, pos.y, pos.z, qx, qy, qz, qw, vco.x, vco.y, vco.z, wwo.x, wwo.y, wwo.z};
-        P::template epilogue<M, LPE>(pa, a, s, e, owner, sub, rt, root, dofs);
+        P::template epilogue<M, LPE>(pa, a, s, e, owner, sub, rt, root, dofs, xpre);
     } else if (owner) {
         if (lead) {
             const V3 wwo = mul(R, v0.w);
