@@ -1034,7 +1034,7 @@ struct GogoroPost {
 #pragma unroll
         for (int k = 0; k < 13; ++k) rt[k] = rt0[k];
         float cmdc;
-        if constexpr (ParLayout<M>::TPN > 0) {
+        if constexpr (ParLayout<M>::TPON) {
             if (a.gp_in_step) {   // this kernel's pre-physics values (LDS), not yet-unflushed HBM
 #pragma unroll
                 for (int k = 0; k < 5; ++k) ah[k] = s(ParLayout<M>::TP + k);

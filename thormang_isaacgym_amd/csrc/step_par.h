@@ -131,9 +131,12 @@ template <class M> struct ParLayout {
     static constexpr int FLG = CGV + 6 * M::NCG;     // a drive exceeded its effort limit
     // the Gogoro pre-physics values computed in the step kernel (models with
     // the fused Gogoro epilogue): action history (5), command, steering target,
-    // rear-wheel velocity target
-    static constexpr int TPN = (M::FUSED & 2) ? 8 : 0;
-    static constexpr int TP = FLG + 1;
+    // rear-wheel velocity target -- in the root group's U / clamp slots, which
+    // the root never uses (its articulated inertia is solved by the LDL), so
+    // the env stride and with it the LDS bank pattern stay as they were
+    static constexpr bool TPON = (M::FUSED & 2) != 0;
+    static constexpr int TP = F_U;
+    static_assert(F_U + 8 <= GF, "pre-physics values in the root group's slots");
     // per-block ints after the env area
     static constexpr int T_GI = 0;
     static constexpr int T_CPATH = T_GI + M::NG * GIW;                 // [NCG][MAXD]
@@ -145,9 +148,9 @@ template <class M> struct ParLayout {
     // its parent (I^a 21 at +0, p^a 6 at +24) and pass 3 its acceleration (+0)
     // into a separate 32-float block, so pass 1's rigid inertias and bias
     // forces survive and the drive-clamp rerun starts at pass 2
-    static constexpr int CB = (TP + TPN + 3) & ~3;
+    static constexpr int CB = (FLG + 1 + 3) & ~3;
     static constexpr bool SEPC = ((size_t)M::EPB * (CB + 32 * M::NG) + T_TOTAL) * 4 <= 160 * 1024;
-    static constexpr int TOTAL = SEPC ? CB + 32 * M::NG : TP + TPN;
+    static constexpr int TOTAL = SEPC ? CB + 32 * M::NG : FLG + 1;
     static constexpr int ES = (TOTAL + 3) & ~3;      // env stride (16-byte aligned)
     template <int EPB> static constexpr size_t bytes() { return ((size_t)EPB * ES + T_TOTAL) * 4; }
 };
@@ -393,6 +396,20 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
     auto PR = [&](int f, int d) { return a.props[(unsigned)f * ND + pbase + (unsigned)d]; };
     const bool lead = sub == 0;
 
+    // the Gogoro pre-physics (tg_gogoro_step) on the env's lead lane, first of
+    // all so its input latency overlaps the state loads
+    if constexpr (PL::TPON) {
+        if (a.gp_in_step && lead) {   // the Gogoro pre-physics (tg_gogoro_step) on the env's lead lane
+            float ah[5], cmd, ts, vr;
+            gogoro_pre_values(a.gp, e, ah, cmd, ts, vr);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) s(PL::TP + k) = ah[k];
+            s(PL::TP + 5) = cmd;
+            s(PL::TP + 6) = ts;
+            s(PL::TP + 7) = vr;
+            if (owner) gogoro_pre_store(a.gp, e, a.D, ah, cmd, ts, vr);
+        }
+    }
     float *root = a.root + (size_t)e * 13;
     float *dofs = a.dof + (size_t)e * D * 2;
     __syncthreads();   // group tables (shared by both wavefronts)
@@ -482,7 +499,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         // the walk pre-physics inside the step (tg_walk_step): the target from the action
         x[7] = a.pm_in_step ? pm_target(a, d, pm_clamp(a, a.pm_actions[ed])) : a.pos_tgt[ed];
         x[8] = a.vel_tgt[ed];
-        if constexpr (PL::TPN > 0) {   // the Gogoro pre-physics inside the step (tg_gogoro_step)
+        if constexpr (PL::TPON) {   // the Gogoro pre-physics inside the step (tg_gogoro_step)
             if (a.gp_in_step) {
                 if (d == a.gp.dof_steer) x[7] = s(PL::TP + 6);
                 if (d == a.gp.dof_rear) x[8] = s(PL::TP + 7);
@@ -514,18 +531,6 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
     // an epilogue's inputs it wants in flight for the whole step (P::prefetch)
     float xpre[P::NPRE > 0 ? P::NPRE : 1];
     if constexpr (P::NPRE > 0) P::template prefetch<M, LPE>(pa, a, e, sub, xpre);
-    if constexpr (PL::TPN > 0) {
-        if (a.gp_in_step && lead) {   // the Gogoro pre-physics (tg_gogoro_step) on the env's lead lane
-            float ah[5], cmd, ts, vr;
-            gogoro_pre_values(a.gp, e, ah, cmd, ts, vr);
-#pragma unroll
-            for (int k = 0; k < 5; ++k) s(PL::TP + k) = ah[k];
-            s(PL::TP + 5) = cmd;
-            s(PL::TP + 6) = ts;
-            s(PL::TP + 7) = vr;
-            if (owner) gogoro_pre_store(a.gp, e, D, ah, cmd, ts, vr);
-        }
-    }
     TG_SYNC();
     TG_PROF(0)
 
