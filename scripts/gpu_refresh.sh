@@ -25,6 +25,9 @@ run gogoropaper2048 --task GogoroPaper --num-envs 2048 --no-cpu-baseline
 PROF_DIR=$OUT/prof_thormangwalk4096 BENCH_ARGS="--task ThormangWalk --steps 200 --warmup 30" bash scripts/gpu_profile.sh > $OUT/prof_t.log 2>&1 || exit $?
 PROF_DIR=$OUT/prof_gogoro4096 BENCH_ARGS="--task Gogoro --steps 200 --warmup 30" bash scripts/gpu_profile.sh > $OUT/prof_g.log 2>&1 || exit $?
 echo profiles ok
+PROF_DIR=$OUT/sq_thormangwalk4096 BENCH_ARGS="--task ThormangWalk --steps 100 --warmup 20" bash scripts/gpu_pmc_sq.sh > $OUT/sq_t.log 2>&1 || exit $?
+PROF_DIR=$OUT/sq_gogoro4096 BENCH_ARGS="--task Gogoro --steps 100 --warmup 20" bash scripts/gpu_pmc_sq.sh > $OUT/sq_g.log 2>&1 || exit $?
+echo sq ok
 if [ -f thormang_isaacgym_amd/libtgsim_prof.so ]; then
   for t in ThormangWalk Gogoro; do
     TG_LIB_PATH=thormang_isaacgym_amd/libtgsim_prof.so timeout -k 10 120 python scripts/section_prof.py $t > $OUT/section_$t.txt 2>&1 || exit $?

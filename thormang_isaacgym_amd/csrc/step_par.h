@@ -151,7 +151,10 @@ template <class M> struct ParLayout {
     static constexpr int CB = (FLG + 1 + 3) & ~3;
     static constexpr bool SEPC = ((size_t)M::EPB * (CB + 32 * M::NG) + T_TOTAL) * 4 <= 160 * 1024;
     static constexpr int TOTAL = SEPC ? CB + 32 * M::NG : FLG + 1;
-    static constexpr int ES = (TOTAL + 3) & ~3;      // env stride (16-byte aligned)
+#ifndef TG_ES_PAD
+#define TG_ES_PAD 0   // developer experiment: extra floats per env (LDS bank pattern)
+#endif
+    static constexpr int ES = ((TOTAL + 3) & ~3) + TG_ES_PAD;   // env stride (16-byte aligned)
     template <int EPB> static constexpr size_t bytes() { return ((size_t)EPB * ES + T_TOTAL) * 4; }
 };
 
