@@ -67,6 +67,8 @@ typedef struct tg_paper_params {
     float damping_effort, damping_velocity;   /* 200, 1.0  paper.py:697-698 */
     float head_com[3];       /* head_p_link COM in the root-group frame */
     float group0_com[3];     /* root-group COM in its frame (wrench reference point) */
+    int32_t perturbation_stride; /* floats between two envs' rows of b->perturbation (0: 3); the task
+                                    points it at head_p_link's row of its [N, L, 3] perturbation tensor */
     uint64_t seed;
 } tg_paper_params;
 
@@ -84,7 +86,7 @@ typedef struct tg_paper_buffers {
     float *steer_offsets, *curent_speed, *curent_speed_offset, *curent_imu_x_offset, *curent_damping_cfg;
     float *yaw_command;        /* [N] */
     float *speed_no_noise;     /* [N] */
-    float *perturbation;       /* [N, 3] world force on head_p_link */
+    float *perturbation;       /* [N, 3] world force on head_p_link (row stride p->perturbation_stride) */
     float *root_reset;         /* [N, 13] */
     const float *thormang_pose;/* [N, D] */
     float *root;               /* [N, 13] sim root state */

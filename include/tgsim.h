@@ -183,10 +183,12 @@ int tg_apply_body_forces(tg_sim *sim, const float *wrench);
  * [N*L,3], either may be NULL (the reference passes torqueTensor=None), in the
  * world frame (TG_ENV_SPACE, isaacgym's default; envs are translated, not
  * rotated) or each body's own frame (TG_LOCAL_SPACE).  Bodies in model.links
- * order (the order of get_actor_rigid_body_dict).  Reduced on the sim stream,
- * from the current root / dof state, to the group wrenches tg_apply_body_forces
- * takes (world force, torque about the group centre of mass); they act for the
- * next tg_simulate call, as PhysX's applied forces do for one simulate. */
+ * order (the order of get_actor_rigid_body_dict).  They act for the next
+ * tg_simulate call, as PhysX's applied forces do for one simulate: that call
+ * reduces them, from the state it starts from, to the group wrenches
+ * tg_apply_body_forces takes (world force, torque about the group centre of
+ * mass) -- so, unlike the other inputs, the tensors are read by the next
+ * tg_simulate and must stay valid until it has been issued. */
 #define TG_ENV_SPACE 0
 #define TG_LOCAL_SPACE 1
 int tg_apply_rigid_body_force_tensors(tg_sim *sim, const float *forces, const float *torques, int32_t space);

@@ -130,7 +130,8 @@ void oracle_paper_reset_env(const tg_paper_params *p, tg_paper_buffers *b, int e
     b->curent_speed[e] = u_aff(p->speed_range, r[0]);
     b->steer_delay[e] = (int64_t)u_aff(p->command_delay, r[1]);
     b->steer_offsets[e] = u_aff(p->steering_offset, r[2]);
-    b->perturbation[3 * e] = b->perturbation[3 * e + 1] = b->perturbation[3 * e + 2] = 0.0f;
+    float *pz = b->perturbation + (size_t)(p->perturbation_stride ? p->perturbation_stride : 3) * e;
+    pz[0] = pz[1] = pz[2] = 0.0f;
     b->curent_speed_offset[e] = u_aff(p->speed_sensor_offset, r[3]);
     float *root = b->root + 13 * (size_t)e;
     const float *tpl = b->root_reset + 13 * (size_t)e;
@@ -252,9 +253,10 @@ void oracle_paper_post_physics(const tg_paper_params *p, tg_paper_buffers *b, co
             float yaw = b->buffer_obs[(size_t)H * O * e + (H - 1) * O + 1];
             float xf = (push_draws[2 * e] * 2.0f - 1.0f) * p->push_force;
             float zf = -(push_draws[2 * e + 1] * p->push_force);
-            b->perturbation[3 * e] = xf * cosf(yaw + F_PI / 2.0f);
-            b->perturbation[3 * e + 1] = xf * sinf(yaw + F_PI / 2.0f);
-            b->perturbation[3 * e + 2] = zf;
+            float *pe = b->perturbation + (size_t)(p->perturbation_stride ? p->perturbation_stride : 3) * e;
+            pe[0] = xf * cosf(yaw + F_PI / 2.0f);
+            pe[1] = xf * sinf(yaw + F_PI / 2.0f);
+            pe[2] = zf;
         }
     }
     for (int e = 0; e < n; ++e) {

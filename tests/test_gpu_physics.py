@@ -176,6 +176,11 @@ def test_gpu_rigid_body_force_tensors_match_oracle(name, space):
     n, L = 512, m.num_bodies
     rs = np.random.default_rng(21 + space)
     root, dof = random_state(m, n, rs)
+    # locked joints at the centre of their windows, as the composite holds them
+    # (the world-frame reduction takes its moment arms from the composite)
+    props0 = abi.default_dof_props(m, 1)
+    for d in m.locked_dofs:
+        dof.reshape(n, -1, 2)[:, d, 0] = 0.5 * (props0[abi.TG_PROP_LOWER, 0, d] + props0[abi.TG_PROP_UPPER, 0, d])
     f = rs.normal(0, 20.0, (n, L, 3)).astype(np.float32)
     t = rs.normal(0, 2.0, (n, L, 3)).astype(np.float32)
     ms = rs.uniform(0.9, 1.1, (n, L)).astype(np.float32)
@@ -185,17 +190,23 @@ def test_gpu_rigid_body_force_tensors_match_oracle(name, space):
     s.dof_state.copy_(torch.from_numpy(dof))
     ids = torch.arange(n, device="cuda:0")
     s.set_body_mass_scale_indexed(torch.from_numpy(ms).cuda(), ids)
-    assert s.apply_rigid_body_force_tensors(torch.from_numpy(f).cuda().reshape(-1, 3),
-                                            torch.from_numpy(t).cuda().reshape(-1, 3), space)
-    torch.cuda.synchronize()
-    got = s.body_force.cpu().numpy()
-    ref = oracle_wrench(m, root, dof, f, t, space, ms)
-    scale = np.abs(ref).max()
-    np.testing.assert_allclose(got, ref, atol=2e-5 * scale, rtol=1e-4)
-    s.apply_rigid_body_force_tensors(None, torch.from_numpy(t).cuda(), space)
-    torch.cuda.synchronize()
-    ref_t = oracle_wrench(m, root, dof, np.zeros_like(f), t, space, ms)
-    np.testing.assert_allclose(s.body_force.cpu().numpy(), ref_t, atol=2e-5 * scale, rtol=1e-4)
+    # the reduction runs in the next simulate, from the state it starts at:
+    # first inside that simulate's compose launch (the mass scales make every
+    # env dirty), then -- nothing dirty -- by its own kernel
+    ft, tt = torch.from_numpy(f).cuda().reshape(-1, 3), torch.from_numpy(t).cuda().reshape(-1, 3)
+    for case in ("forces+torques", "torques only"):
+        r0 = s.root_state.cpu().numpy().copy()
+        d0 = s.dof_state.cpu().numpy().copy()
+        if case == "forces+torques":
+            assert s.apply_rigid_body_force_tensors(ft, tt, space)
+            ref = oracle_wrench(m, r0, d0, f, t, space, ms)
+            scale = np.abs(ref).max()
+        else:
+            assert s.apply_rigid_body_force_tensors(None, tt, space)
+            ref = oracle_wrench(m, r0, d0, np.zeros_like(f), t, space, ms)
+        s.simulate()
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(s.body_force.cpu().numpy(), ref, atol=2e-5 * scale, rtol=1e-4, err_msg=case)
 
 
 def test_gpu_runtime_loaded_model_matches_oracle():

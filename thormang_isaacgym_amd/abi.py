@@ -101,7 +101,8 @@ class tg_paper_params(C.Structure):
         ("use_steer_delay", C.c_int32), ("random_damping", C.c_int32), ("center_robot", C.c_int32),
         ("push_robot", C.c_int32), ("debug_start_speed", C.c_int32),
         ("damping_stiffness", C.c_float), ("damping_effort", C.c_float), ("damping_velocity", C.c_float),
-        ("head_com", C.c_float * 3), ("group0_com", C.c_float * 3), ("seed", C.c_uint64),
+        ("head_com", C.c_float * 3), ("group0_com", C.c_float * 3), ("perturbation_stride", C.c_int32),
+        ("seed", C.c_uint64),
     ]
 
 

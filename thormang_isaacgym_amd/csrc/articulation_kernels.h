@@ -38,7 +38,9 @@ template <class M> struct CompLayout {
     static constexpr int xk(int k) { return ext() + 10 + 8 * k; }
     static constexpr int xag(int j) { return ext() + 10 + 8 * M::NTL + 3 * j; }
     static constexpr int xash(int j) { return ext() + 10 + 8 * M::NTL + 3 * M::NAG + 3 * j; }
-    static_assert(M::KC == GB * M::NG + 12 * M::NS + M::KX, "codegen KC");
+    // link com block (M::LCOM): com of link l in its group's joint-aligned frame at lcom(l)
+    static constexpr int lcom(int l) { return ext() + M::KX + 3 * l; }
+    static_assert(M::KC == GB * M::NG + 12 * M::NS + M::KX + (M::LCOM ? ((3 * M::NL + 3) & ~3) : 0), "codegen KC");
     static_assert(M::NTL == 0 || 10 + 8 * M::NTL + 3 * (M::NAG + M::NASH) <= M::KX, "codegen KX");
 };
 
@@ -141,6 +143,11 @@ __device__ __forceinline__ void gogoro_pre_prologue(const GogoroPre &g, int e, i
     gogoro_pre_values(g, e, ah, cmd, ts, vr);
     gogoro_pre_store(g, e, D, ah, cmd, ts, vr);
 }
+
+template <class M>
+__device__ __forceinline__ void rb_force_env(const float *root, const float *dof, const float *comp, int e,
+                                             const float *mass_scale, const float *forces, const float *torques,
+                                             int space, float *out, int lane, float (*T)[12], float (*F)[10]);
 
 // one wavefront's compose scratch
 template <class M> struct ComposeLds {
@@ -262,6 +269,12 @@ template <class M> __device__ __forceinline__ void compose_env(const StepArgs &a
         LM[l][1] = cg.x; LM[l][2] = cg.y; LM[l][3] = cg.z;
         LM[l][4] = RI.a[0]; LM[l][5] = RI.a[4]; LM[l][6] = RI.a[8];
         LM[l][7] = RI.a[1]; LM[l][8] = RI.a[2]; LM[l][9] = RI.a[5];
+        if constexpr (M::LCOM) {   // the link's com in its group's joint-aligned frame
+            const float *qg = M::gq[M::link_group[l]];
+            const V3 cq = mulT(M3{{qg[0], qg[1], qg[2], qg[3], qg[4], qg[5], qg[6], qg[7], qg[8]}}, cg);
+            float *lc = a.comp + (size_t)e * M::KC + CL::lcom(l);
+            lc[0] = cq.x; lc[1] = cq.y; lc[2] = cq.z;
+        }
     }
     wsync();
     TG_CPROF(1)
@@ -445,9 +458,11 @@ template <class M> __global__ __launch_bounds__(64 * COMPOSE_WPB) void compose_k
     if (a.cnext && blockIdx.x == 0 && threadIdx.x == 0) *a.cnext = 0;   // the reset list the next epilogue fills
     if (a.pm_actions && !a.pm_in_step && e < a.N) target_prologue(a, e, threadIdx.x % 64);
     if (a.gp.actions && !a.gp_in_step && e < a.N && threadIdx.x % 64 == 0) gogoro_pre_prologue(a.gp, e, a.D);
-    if (!dirty) return;
     __shared__ ComposeLds<M> cs[COMPOSE_WPB];
-    compose_env<M>(a, e, threadIdx.x % 64, cs[wv]);
+    if (dirty) compose_env<M>(a, e, threadIdx.x % 64, cs[wv]);
+    if (a.rbf_forces && e < a.N)   // a pending apply_rigid_body_force_tensors, on the fresh composite
+        rb_force_env<M>(a.root, a.dof, a.comp, e, a.mass_scale, a.rbf_forces, a.rbf_torques, a.rbf_space, a.rbf_out,
+                        threadIdx.x % 64, cs[wv].T, cs[wv].LM);
 }
 
 // Compose of the envs a fused task epilogue reset (tg_gogoro_step): the
@@ -578,14 +593,25 @@ template <class M> __global__ __launch_bounds__(64) void body_state_kernel(const
 // wavefront per env: link poses level by level (lane = link), then lane = group
 // sums its links in link order.  The same function as oracle/physics_ref.c
 // oracle_rigid_body_force_wrench.
-template <class M> __global__ __launch_bounds__(64) void rb_force_kernel(const float *root, const float *dof, int n,
-                                                                         const float *mass_scale, const float *forces,
-                                                                         const float *torques, int space, float *out) {
-    const int e = blockIdx.x;
-    if (e >= n) return;
-    __shared__ float T[M::NL][12];    // R (9), p (3); then com (3), mass, f (3), t (3) per link
-    __shared__ float F[M::NL][10];
-    const int lane = threadIdx.x;
+// env e with the 64 lanes of a wavefront; T, F: the wave's LDS scratch
+template <class M> constexpr int group_depth(int g) {
+    int d = 0;
+    while (M::parent[g] >= 0) {
+        g = M::parent[g];
+        ++d;
+    }
+    return d;
+}
+template <class M> constexpr int max_group_depth() {
+    int d = 0;
+    for (int g = 0; g < M::NG; ++g) d = group_depth<M>(g) > d ? group_depth<M>(g) : d;
+    return d;
+}
+
+template <class M>
+__device__ __forceinline__ void rb_force_env(const float *root, const float *dof, const float *comp, int e,
+                                             const float *mass_scale, const float *forces, const float *torques,
+                                             int space, float *out, int lane, float (*T)[12], float (*F)[10]) {
     const float *r = root + 13 * (size_t)e;
     const float *q = dof + 2 * (size_t)e * M::ND;
     auto wsync = [] {
@@ -593,6 +619,92 @@ template <class M> __global__ __launch_bounds__(64) void rb_force_kernel(const f
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
+    wsync();   // the scratch may have been in use by this wave
+    // an env with no force and no torque on any link gets zero wrenches without
+    // the link kinematics (the paper task pushes only its first 2048 envs)
+    bool any = false;
+    for (int l = lane; l < M::NL; l += 64) {
+        const size_t i = 3 * ((size_t)e * M::NL + l);
+        any = any || forces[i] != 0.f || forces[i + 1] != 0.f || forces[i + 2] != 0.f;
+        if (torques) any = any || torques[i] != 0.f || torques[i + 1] != 0.f || torques[i + 2] != 0.f;
+    }
+    if (!__any(any)) {
+        for (int k = lane; k < 6 * M::NG; k += 64) out[(size_t)e * 6 * M::NG + k] = 0.f;
+        return;
+    }
+    if constexpr (M::LCOM) {
+        if (comp && space == 0) {
+            // world forces: the moment arms from the composite cache -- each
+            // link's com and its group's com in the group's joint-aligned frame
+            // -- rotated by the group's world orientation (group kinematics, a
+            // few levels), no link kinematics: arm_l = W_g (c_l - c_g)
+            using CL = CompLayout<M>;
+            const float *c = comp + (size_t)e * M::KC;
+            float qx = r[3], qy = r[4], qz = r[5], qw = r[6];
+            const float in = rsqrtf(qx * qx + qy * qy + qz * qz + qw * qw);
+            const M3 Rr = quat_to_m3(qx * in, qy * in, qz * in, qw * in);
+            constexpr int GD = max_group_depth<M>();
+            for (int lev = 0; lev <= GD; ++lev) {
+                for (int g = lane; g < M::NG; g += 64) {
+                    if (group_depth<M>(g) != lev) continue;
+                    M3 W;
+                    if (g == 0) {
+                        W = mul(Rr, M3{{M::gq[0][0], M::gq[0][1], M::gq[0][2], M::gq[0][3], M::gq[0][4], M::gq[0][5],
+                                        M::gq[0][6], M::gq[0][7], M::gq[0][8]}});
+                    } else {
+                        M3 Wp, Rpc;
+#pragma unroll
+                        for (int k = 0; k < 9; ++k) {
+                            Wp.a[k] = T[M::parent[g]][k];
+                            Rpc.a[k] = c[CL::xtree(g) + k];
+                        }
+                        if (M::jtype[g] == TG_JOINT_REVOLUTE) {   // Rpc Rz(q), as step pass 1a
+                            float sq, cq;
+                            __sincosf(q[2 * M::gdof[g]], &sq, &cq);
+#pragma unroll
+                            for (int rr = 0; rr < 3; ++rr) {
+                                const float c0 = Rpc.a[3 * rr], c1 = Rpc.a[3 * rr + 1];
+                                Rpc.a[3 * rr] = c0 * cq + c1 * sq;
+                                Rpc.a[3 * rr + 1] = c1 * cq - c0 * sq;
+                            }
+                        }
+                        W = mul(Wp, Rpc);
+                    }
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) T[g][k] = W.a[k];
+                }
+                wsync();
+            }
+            for (int l = lane; l < M::NL; l += 64) {
+                const int g = M::link_group[l];
+                M3 W;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) W.a[k] = T[g][k];
+                const V3 d = v3(c[CL::lcom(l)], c[CL::lcom(l) + 1], c[CL::lcom(l) + 2]) -
+                             v3(c[CL::inertia(g) + 1], c[CL::inertia(g) + 2], c[CL::inertia(g) + 3]);
+                const V3 arm = mul(W, d);
+                const size_t i = (size_t)e * M::NL + l;
+                const V3 f = v3(forces[3 * i], forces[3 * i + 1], forces[3 * i + 2]);
+                const V3 t = torques ? v3(torques[3 * i], torques[3 * i + 1], torques[3 * i + 2]) : v3(0, 0, 0);
+                const V3 tq = t + cross(arm, f);
+                F[l][0] = f.x; F[l][1] = f.y; F[l][2] = f.z;
+                F[l][3] = tq.x; F[l][4] = tq.y; F[l][5] = tq.z;
+            }
+            wsync();
+            for (int g = lane; g < M::NG; g += 64) {
+                V3 fs = v3(0, 0, 0), ts = v3(0, 0, 0);
+                for (int k = 0; k < M::group_nlinks[g]; ++k) {
+                    const int l = M::group_links[g][k];
+                    fs = fs + v3(F[l][0], F[l][1], F[l][2]);
+                    ts = ts + v3(F[l][3], F[l][4], F[l][5]);
+                }
+                float *o = out + ((size_t)e * M::NG + g) * 6;
+                o[0] = fs.x; o[1] = fs.y; o[2] = fs.z;
+                o[3] = ts.x; o[4] = ts.y; o[5] = ts.z;
+            }
+            return;
+        }
+    }
     for (int lev = 0; lev <= M::NDEPTH; ++lev) {
         for (int l = lane; l < M::NL; l += 64) {
             if (M::link_depth[l] != lev) continue;
@@ -666,6 +778,17 @@ template <class M> __global__ __launch_bounds__(64) void rb_force_kernel(const f
         o[0] = fs.x; o[1] = fs.y; o[2] = fs.z;
         o[3] = ts.x; o[4] = ts.y; o[5] = ts.z;
     }
+}
+
+template <class M> __global__ __launch_bounds__(64) void rb_force_kernel(const float *root, const float *dof,
+                                                                         const float *comp, int n,
+                                                                         const float *mass_scale, const float *forces,
+                                                                         const float *torques, int space, float *out) {
+    const int e = blockIdx.x;
+    if (e >= n) return;
+    __shared__ float T[M::NL][12];   // link pose: R (9), p (3)
+    __shared__ float F[M::NL][10];   // link com (3), mass, force (3), torque (3)
+    rb_force_env<M>(root, dof, comp, e, mass_scale, forces, torques, space, out, threadIdx.x, T, F);
 }
 
 // ---------------------------------------------------------------- contact row layout

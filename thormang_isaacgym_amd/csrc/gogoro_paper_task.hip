@@ -103,9 +103,10 @@ __device__ void paper_reset_env(const tg_paper_params &p, const tg_paper_buffers
     b.curent_speed[e] = p_aff(p.speed_range, r[0]);
     b.steer_delay[e] = (int64_t)p_aff(p.command_delay, r[1]);
     b.steer_offsets[e] = p_aff(p.steering_offset, r[2]);
-    b.perturbation[3 * (size_t)e] = 0.0f;
-    b.perturbation[3 * (size_t)e + 1] = 0.0f;
-    b.perturbation[3 * (size_t)e + 2] = 0.0f;
+    float *pz = b.perturbation + (size_t)(p.perturbation_stride ? p.perturbation_stride : 3) * e;
+    pz[0] = 0.0f;
+    pz[1] = 0.0f;
+    pz[2] = 0.0f;
     b.curent_speed_offset[e] = p_aff(p.speed_sensor_offset, r[3]);
     float *root = b.root + 13 * (size_t)e;
     const float *tpl = b.root_reset + 13 * (size_t)e;
@@ -285,7 +286,7 @@ __global__ __launch_bounds__(64) void paper_post_kernel(tg_paper_params p, tg_pa
         yc = yc < -P_PI ? yc + (float)(3.14159265358979323846 * 2) : yc;
         b.yaw_command[e] = yc;
         // pushes on head_p_link (:442-459)
-        float *pert = b.perturbation + 3 * (size_t)e;
+        float *pert = b.perturbation + (size_t)(p.perturbation_stride ? p.perturbation_stride : 3) * e;
         if (p.push_robot && e < p.push_max_envs && (prog + 1) % p.push_interval == 0) {
             const float yaw = last[1];
             const float xf = (p_draw(p, pd, 2, e, 0, c_lo, c_hi, 0x50415055u) * 2.0f - 1.0f) * p.push_force;

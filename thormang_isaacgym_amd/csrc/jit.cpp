@@ -283,11 +283,12 @@ int jit_launch_body_states(uint64_t hash, const float *root, const float *dof, i
     return launch(L->f[K_BODY], (unsigned)n, 64, 0, stream, args);
 }
 
-int jit_launch_rb_forces(uint64_t hash, const float *root, const float *dof, int n, const float *mass_scale,
-                         const float *forces, const float *torques, int space, float *out, hipStream_t stream) {
+int jit_launch_rb_forces(uint64_t hash, const float *root, const float *dof, const float *comp, int n,
+                         const float *mass_scale, const float *forces, const float *torques, int space, float *out,
+                         hipStream_t stream) {
     JitLoaded *L = find(hash);
     if (!L) return TG_ERR_MODEL;
-    void *args[] = {&root, &dof, &n, &mass_scale, &forces, &torques, &space, &out};
+    void *args[] = {&root, &dof, &comp, &n, &mass_scale, &forces, &torques, &space, &out};
     return launch(L->f[K_RBF], (unsigned)n, 64, 0, stream, args);
 }
 

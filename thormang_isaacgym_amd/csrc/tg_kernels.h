@@ -72,6 +72,11 @@ struct StepArgs {
     // gp_in_step: the Gogoro pre-physics (gp) runs at the start of the step
     // kernel (lead lane; values through the env's LDS) instead of in compose
     int gp_in_step;
+    // a pending apply_rigid_body_force_tensors reduced by the (full) compose
+    // launch of this simulate (rbf_forces null: none)
+    const float *rbf_forces, *rbf_torques;
+    int rbf_space;
+    float *rbf_out;
 };
 
 // tg_walk_step's fused post-physics epilogue (articulation.hip WalkPost)
@@ -105,8 +110,9 @@ int launch_step(uint64_t hash, const StepArgs &a, hipStream_t stream, hipEvent_t
 int compiled_hashes(uint64_t *out, int cap);
 int launch_body_states(uint64_t hash, const float *root, const float *dof, int n, float *out, hipStream_t stream);
 // per-link forces / torques [N*L,3] -> group wrenches [N,G,6] (rb_force_kernel)
-int launch_rb_forces(uint64_t hash, const float *root, const float *dof, int n, const float *mass_scale,
-                     const float *forces, const float *torques, int space, float *out, hipStream_t stream);
+int launch_rb_forces(uint64_t hash, const float *root, const float *dof, const float *comp, int n,
+                     const float *mass_scale, const float *forces, const float *torques, int space, float *out,
+                     hipStream_t stream);
 int model_kc(uint64_t hash);
 int model_tl(uint64_t hash);
 int launch_compose_only(uint64_t hash, const StepArgs &a, hipStream_t stream);   // every dirty env, no step   // translating locks of a compiled model (codegen translating_locks), 0 otherwise
@@ -119,8 +125,9 @@ bool jit_has(uint64_t hash);
 int jit_kc(uint64_t hash);
 int jit_launch_step(uint64_t hash, const StepArgs &a, hipStream_t stream, hipEvent_t ev_begin, hipEvent_t ev_end);
 int jit_launch_body_states(uint64_t hash, const float *root, const float *dof, int n, float *out, hipStream_t stream);
-int jit_launch_rb_forces(uint64_t hash, const float *root, const float *dof, int n, const float *mass_scale,
-                         const float *forces, const float *torques, int space, float *out, hipStream_t stream);
+int jit_launch_rb_forces(uint64_t hash, const float *root, const float *dof, const float *comp, int n,
+                         const float *mass_scale, const float *forces, const float *torques, int space, float *out,
+                         hipStream_t stream);
 
 int launch_gogoro_pre(const tg_gogoro_params &p, const tg_gogoro_buffers &b, const float *actions,
                       const float *pre_draws, uint64_t counter, hipStream_t stream);

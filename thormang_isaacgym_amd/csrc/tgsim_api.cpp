@@ -49,6 +49,11 @@ struct tg_sim {
     hipStream_t stream = nullptr;
     float gravity[3] = {0, 0, -9.81f};
     bool forces_pending = false;
+    // apply_rigid_body_force_tensors waiting for the next simulate: reduced to
+    // group wrenches by that simulate's compose launch, or by rb_force_kernel
+    bool rbf_pending = false;
+    const float *rbf_f = nullptr, *rbf_t = nullptr;
+    int rbf_space = 0;
     // some env may be dirty (its composite cache stale): set by every call that
     // can mark envs dirty or change what compose reads (creation, state
     // binding, tg_refresh -- the contract for writes through the zero-copy
@@ -406,6 +411,7 @@ int tg_apply_body_forces(tg_sim *s, const float *wrench) {
     if (!wrench) return fail(TG_ERR_ARG, "null wrench tensor");
     if (int rc = copy_full(s, s->force, wrench, (size_t)s->N * s->G * 6)) return rc;
     s->forces_pending = true;
+    s->rbf_pending = false;   // the group wrenches given here replace a pending per-link tensor
     return TG_OK;
 }
 
@@ -460,7 +466,9 @@ static int simulate_args(tg_sim *s, const tg::StepArgs &a_in, const tg::WalkPost
     // last fused epilogue's reset list, the task prologue alone, or none
     const bool walk_prologue = a.pm_actions && !a.pm_in_step;
     const bool gogoro_prologue = a.gp.actions && !a.gp_in_step;
-    const bool full = s->dirty_possible || s->always_compose || walk_prologue;
+    // (a pending per-link force tensor with listed envs: the full compose, which
+    // reduces it after composing them)
+    const bool full = s->dirty_possible || s->always_compose || walk_prologue || (s->rbf_pending && s->list_pending);
     a.skip_compose = !full && !s->list_pending && !gogoro_prologue;
     a.compose_list = !full && !a.skip_compose;
     a.cnext = s->ccount + s->list_cur;
@@ -468,6 +476,18 @@ static int simulate_args(tg_sim *s, const tg::StepArgs &a_in, const tg::WalkPost
         const int prev = 1 - s->list_cur;
         a.clist = s->clist + (size_t)prev * s->N;
         a.ccount = s->ccount + prev;
+    }
+    if (s->rbf_pending) {   // the pending per-link forces: in the full compose launch, else on their own
+        if (!a.skip_compose && !a.compose_list) {
+            a.rbf_forces = s->rbf_f;
+            a.rbf_torques = s->rbf_t;
+            a.rbf_space = s->rbf_space;
+            a.rbf_out = s->force;
+        } else if (int rc = tg::launch_rb_forces(s->hash, s->root, s->dof, s->comp, (int)s->N, s->mass_scale,
+                                                 s->rbf_f, s->rbf_t, s->rbf_space, s->force, s->stream)) {
+            return fail(rc, "rigid-body force launch failed");
+        }
+        s->rbf_pending = false;
     }
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     const bool timed = s->timing > 0 && s->timing_count % s->timing == 0;
@@ -526,9 +546,13 @@ int tg_apply_rigid_body_force_tensors(tg_sim *s, const float *forces, const floa
         }
         f = s->zero_link3;
     }
-    if (int rc = tg::launch_rb_forces(s->hash, s->root, s->dof, (int)s->N, s->mass_scale, f, torques, space, s->force,
-                                      s->stream))
-        return fail(rc, "rigid-body force launch failed");
+    // reduced when the next simulate runs (PhysX applies the forces during
+    // simulate, at the state it starts from): inside its compose launch if it
+    // has one, else by rb_force_kernel just before the step
+    s->rbf_f = f;
+    s->rbf_t = torques;
+    s->rbf_space = space;
+    s->rbf_pending = true;
     s->forces_pending = true;
     return TG_OK;
 }
@@ -726,6 +750,7 @@ int tg_walk_step(tg_sim *s, const tg_walk_params *p, const tg_walk_buffers *b, c
     if (b->body_force) {   // pre_physics_step: apply_rigid_body_force_tensors(body_force)
         if (int rc = copy_full(s, s->force, b->body_force, (size_t)s->N * s->G * 6)) return rc;
         s->forces_pending = true;
+        s->rbf_pending = false;
     }
     if (n_simulate == 1 && !s->walk_unfused && !s->pre_in_compose) {
         // one launch per step: pre-physics (drive targets formed from the

@@ -188,6 +188,10 @@ def emit(m: Model, cname: str) -> str:
     glinks = [[l for l in range(L) if lgrp[l] == g] for g in range(G)]
     maxgl = max(len(x) for x in glinks)
     tlc = translating_locks(m, a)
+    # link coms in their group's frame (3 per link, padded to 16 bytes): the
+    # rigid-body force reduction's moment arms without link kinematics.  Not
+    # for models whose epilogue moves locks in place (the links would move too)
+    lcom = 0 if tlc["NTL"] else (3 * L + 3) & ~3
     maxc = max(1, max(len(c) for c in children))
     lines = [
         f"// AUTO-GENERATED by thormang_isaacgym_amd/model/codegen.py from model '{m.name}'. Do not edit.",
@@ -195,8 +199,9 @@ def emit(m: Model, cname: str) -> str:
         f"struct {cname} {{",
         f"  static constexpr unsigned long long hash = 0x{d.hash:016x}ULL;",
         f"  static constexpr int NG = {G}, NL = {L}, ND = {D}, NS = {S > 0 and S or 0}, NSA = {max(S, 1)};",
-        f"  static constexpr int KC = {24 * G + 12 * S + tlc['KX']};  // per-env composite floats (env-major, csrc CompLayout)",
+        f"  static constexpr int KC = {24 * G + 12 * S + tlc['KX'] + lcom};  // per-env composite floats (env-major, csrc CompLayout)",
         f"  static constexpr int KX = {tlc['KX']};  // of which the translating-lock extension (codegen translating_locks)",
+        f"  static constexpr int LCOM = {1 if lcom else 0};  // link coms in their group frames (rigid-body force reduction)",
         f"  static constexpr int NTL = {tlc['NTL']}, tl_group = {tlc['tl_group']}, NAG = {len(tlc['ag'])}, "
         f"NASH = {len(tlc['ashape'])};",
         f"  static constexpr int tl_link[{max(tlc['NTL'], 1)}] = {_arr(tlc['tl_link'])};",

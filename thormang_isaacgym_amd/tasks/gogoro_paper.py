@@ -225,12 +225,15 @@ class Gogoro(VecTask):
         self.root_tensor[:, 6] = 1.0
         self.root_reset_tensor = self.root_tensor.clone().detach()
         self.root_reset_tensor[:, 7:13] = 0
-        self.head_perturbation = torch.zeros((n, 3), device=dev)  # curent_perturbations[:, head_p_link]
+        # the reference's [N, L, 3] perturbation tensor (:457); the post kernel
+        # writes head_p_link's rows in place (tg_paper_params.perturbation_stride)
         self._perturbations = torch.zeros((n, self.num_rgbd, 3), device=dev)
         self._head_id = self.rgid_body_to_id["head_p_link"]
+        self.head_perturbation = self._perturbations[:, self._head_id]   # strided view
         self.scratch = torch.zeros(n, device=dev)
         self.current_steering = None
         self.params = paper_params(self.cfg, self.model, n, self.switches, self.seed)
+        self.params.perturbation_stride = 3 * self.num_rgbd
         self._bufs = self._make_buffers()
         self.reset_idx(torch.arange(0, n, device=self.device).type(torch.long))
 
@@ -277,6 +280,9 @@ class Gogoro(VecTask):
         for k, t in pairs.items():
             if t is None:
                 continue
+            if k == "perturbation":   # head_p_link's rows of the [N, L, 3] tensor, stride L*3
+                setattr(b, k, t.data_ptr())
+                continue
             if not t.is_contiguous() or t.device != torch.device(self.device):
                 raise RuntimeError(f"task buffer {k} must be contiguous on {self.device}")
             setattr(b, k, t.data_ptr())
@@ -312,7 +318,6 @@ class Gogoro(VecTask):
         self._keep_post = keep
         self.curent_step += 1
         if self.switches["PUSH_ROBOT"]:   # :449-457, the reference's own [N*L, 3] tensor
-            self._perturbations[:, self._head_id] = self.head_perturbation
             self.sim.apply_rigid_body_force_tensors(torch.flatten(self._perturbations, end_dim=-2), None)
 
     def compute_obs_rwd(self):
