@@ -920,11 +920,7 @@ struct WalkPost {
                     o[13 + d] = clampw((q[r] - p.default_pos[d]) * p.dof_pos_scale, -co, co);
                     o[13 + D + d] = clampw(qd[r] * p.dof_vel_scale, -co, co);
                     o[13 + 2 * D + d] = clampw(act[r], -co, co);
-                    b.last_actions[eD + d] = act[r];
-                    if (a.pm_in_step) {   // the prologue's outputs (a reset env's actions are 0)
-                        b.actions[eD + d] = act[r];
-                        b.pos_target[eD + d] = pt[r];
-                    }
+                    b.last_actions[eD + d] = act[r];   // (pm_in_step: actions / targets stored at kernel start)
                 }
                 rate += (act[r] - la[r]) * (act[r] - la[r]);
                 vel2 += qd[r] * qd[r];

@@ -8,9 +8,10 @@
 //                       (:609-692), observation (:771-808), 20-step clean /
 //                       noisy histories (:503-547), reward terms 1-5, command
 //                       changes, head pushes and the root-group wrench
-//   paper_finish_kernel one workgroup: batch mean of the squared command
-//                       differences (torch.mean without dim, :740, reward term
-//                       7), rewards, resets, VecTask time_outs
+//   paper_finish_kernel batch mean of the squared command differences
+//                       (torch.mean without dim, :740, reward term 7; every
+//                       workgroup sums the whole batch), rewards, resets,
+//                       VecTask time_outs
 // fp32 in the reference's operation order (compiled -ffp-contract=off).
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -33,11 +34,25 @@ __device__ __forceinline__ float p_clamp(float x, float lo, float hi) { return x
 __device__ __forceinline__ float p_aff(const float *b, float u) {
     return b[0] + u * (float)((double)b[1] - (double)b[0]);
 }
+// envs (one wavefront each) per workgroup of the pre / post kernels: N / 8
+// workgroups rather than N, which the dispatcher would issue one by one
+constexpr int PAPER_EPW = 8;
+// an env's lanes are one wavefront: its LDS / memory hand-offs need only a
+// wavefront-scope fence
+__device__ __forceinline__ void p_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 __device__ __forceinline__ float p_wsum(float v) {
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
     return v;
 }
+
+// Philox stream tags of the draw kinds (4 draws per counter block)
+constexpr uint32_t P_TAG_RESET = 0x50415052u, P_TAG_NOISE = 0x50414e5au, P_TAG_SPEED = 0x50415344u,
+                   P_TAG_YAW = 0x50415957u, P_TAG_PUSH = 0x50415055u;
 
 // reset draw k (0..8) of env e: replay array or Philox (4 per counter)
 __device__ __forceinline__ float p_draw(const tg_paper_params &p, const float *arr, int stride, int e, int k,
@@ -48,79 +63,92 @@ __device__ __forceinline__ float p_draw(const tg_paper_params &p, const float *a
     return u01(c);
 }
 
-__global__ __launch_bounds__(64) void paper_pre_kernel(tg_paper_params p, tg_paper_buffers b, const float *actions) {
-    const int e = blockIdx.x, lane = threadIdx.x;
+__global__ __launch_bounds__(64 * PAPER_EPW) void paper_pre_kernel(tg_paper_params p, tg_paper_buffers b,
+                                                                   const float *actions) {
+    // every input in one batch; the shifted history stays in registers (lane =
+    // slot) and the delayed command is taken from its lane
+    static_assert(PC <= 64, "one history slot per lane");
+    const int e = blockIdx.x * PAPER_EPW + threadIdx.x / 64, lane = threadIdx.x % 64;
+    if (e >= p.num_envs) return;
     const int D = p.num_dof;
     float *h = b.command_history + PC * (size_t)e;
-    float hv = 0.f, cmd = 0.f;
-    {
-        const float a = p_clamp(actions[e], -1.0f, 1.0f);
-        cmd = a * p.max_steering;
-        if (lane < PC) hv = lane < PC - 1 ? h[lane + 1] : cmd;
-    }
-    __syncthreads();
+    const float a = p_clamp(actions[e], -1.0f, 1.0f);
+    const float cmd = a * p.max_steering;
+    const float hn = lane < PC - 1 ? h[lane + 1] : 0.0f;
+    const int64_t delay = p.use_steer_delay ? b.steer_delay[e] : 0;
+    const float speed = b.curent_speed[e];
+    const float hv = lane < PC - 1 ? hn : cmd;
+    int idx = PC - 3;
+    if (p.use_steer_delay) idx = delay == 0 ? 0 : (int)(PC - delay);   // command_history[:, -steer_delay]; -0 selects slot 0
+    const float steer = __shfl(hv, idx, 64);
+    p_wave_sync();   // every lane's history read is done before the shifted history is stored
     if (lane < PC) h[lane] = hv;
-    __syncthreads();
     float *pt = b.pos_target + (size_t)D * e, *vt = b.vel_target + (size_t)D * e;
     for (int d = lane; d < D; d += 64) {
-        pt[d] = 0.0f;
-        vt[d] = 0.0f;
+        pt[d] = d == p.dof_steer ? steer : 0.0f;
+        vt[d] = d == p.dof_rear ? speed : 0.0f;
     }
-    __syncthreads();
-    if (lane == 0) {
-        b.curent_command[e] = cmd;
-        int idx = PC - 3;
-        if (p.use_steer_delay) {   // command_history[:, -steer_delay]; -0 selects slot 0
-            const int64_t d = b.steer_delay[e];
-            idx = d == 0 ? 0 : (int)(PC - d);
-        }
-        pt[p.dof_steer] = h[idx];
-        vt[p.dof_rear] = b.curent_speed[e];
-    }
+    if (lane == 0) b.curent_command[e] = cmd;
 }
 
-// reset_idx for env e (:609-692) by one wavefront
-__device__ void paper_reset_env(const tg_paper_params &p, const tg_paper_buffers &b, int e, const float *rd,
-                                uint32_t c_lo, uint32_t c_hi) {
-    const int lane = threadIdx.x;
+// the per-env values the post-physics reads, held by the env's lead lane
+struct PaperLead {
+    float root[13];
+    float speed, speed_off, imu_off, yaw_cmd, cmd;
+    int64_t delay;
+};
+
+// reset_idx for env e (:609-692), lane-parallel part: histories (zero_hist;
+// the fused post kernel rewrites them in full anyway) and dof state
+__device__ void paper_reset_lanes(const tg_paper_params &p, const tg_paper_buffers &b, int e, bool zero_hist) {
+    const int lane = threadIdx.x % 64;
     const int D = p.num_dof;
-    const size_t ND = (size_t)p.num_envs * D;
-    for (int i = lane; i < PHO; i += 64) {
-        b.obs_buf[(size_t)PHO * e + i] = 0.0f;
-        b.buffer_obs[(size_t)PHO * e + i] = 0.0f;
-        b.buffer_obs_noisy[(size_t)PHO * e + i] = 0.0f;
+    if (zero_hist) {
+        for (int i = lane; i < PHO; i += 64) {
+            b.obs_buf[(size_t)PHO * e + i] = 0.0f;
+            b.buffer_obs[(size_t)PHO * e + i] = 0.0f;
+            b.buffer_obs_noisy[(size_t)PHO * e + i] = 0.0f;
+        }
     }
     if (lane < PC) b.command_history[PC * (size_t)e + lane] = 0.0f;
     for (int d = lane; d < D; d += 64) {
         b.dof_state[2 * ((size_t)e * D + d)] = b.thormang_pose[(size_t)e * D + d];
         b.dof_state[2 * ((size_t)e * D + d) + 1] = 0.0f;
     }
-    if (lane != 0) return;
-    const uint32_t tag = 0x50415052u;
-    float r[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) r[k] = p_draw(p, rd, 9, e, k, c_lo, c_hi, tag);
-    b.curent_speed[e] = p_aff(p.speed_range, r[0]);
-    b.steer_delay[e] = (int64_t)p_aff(p.command_delay, r[1]);
+}
+
+// reset_idx for env e, lead-lane part: the draws and the scalar state, written
+// to HBM and returned in L (tpl: the env's root reset template)
+__device__ __forceinline__ void paper_reset_lead(const tg_paper_params &p, const tg_paper_buffers &b, int e,
+                                                 const float *r, const float *tpl, PaperLead &L) {
+    const int D = p.num_dof;
+    const size_t ND = (size_t)p.num_envs * D;
+    L.speed = p_aff(p.speed_range, r[0]);
+    L.delay = (int64_t)p_aff(p.command_delay, r[1]);
+    b.curent_speed[e] = L.speed;
+    b.steer_delay[e] = L.delay;
     b.steer_offsets[e] = p_aff(p.steering_offset, r[2]);
     float *pz = b.perturbation + (size_t)(p.perturbation_stride ? p.perturbation_stride : 3) * e;
     pz[0] = 0.0f;
     pz[1] = 0.0f;
     pz[2] = 0.0f;
-    b.curent_speed_offset[e] = p_aff(p.speed_sensor_offset, r[3]);
+    L.speed_off = p_aff(p.speed_sensor_offset, r[3]);
+    b.curent_speed_offset[e] = L.speed_off;
     float *root = b.root + 13 * (size_t)e;
-    const float *tpl = b.root_reset + 13 * (size_t)e;
 #pragma unroll
-    for (int k = 0; k < 13; ++k) root[k] = tpl[k];
-    root[2] = p.spawn_z;
-    root[3] = 0.0f; root[4] = 0.0f; root[5] = 0.0f; root[6] = 1.0f;
+    for (int k = 0; k < 13; ++k) L.root[k] = tpl[k];
+    L.root[2] = p.spawn_z;
+    L.root[3] = 0.0f; L.root[4] = 0.0f; L.root[5] = 0.0f; L.root[6] = 1.0f;
 #pragma unroll
-    for (int k = 7; k < 13; ++k) root[k] = 0.0f;
+    for (int k = 7; k < 13; ++k) L.root[k] = 0.0f;
     if (p.debug_start_speed) {
-        root[7] = p.start_speed * cosf(0.0f);
-        root[8] = p.start_speed * sinf(0.0f);
+        L.root[7] = p.start_speed * cosf(0.0f);
+        L.root[8] = p.start_speed * sinf(0.0f);
     }
-    b.curent_imu_x_offset[e] = p_aff(p.imu_x_offset, r[4]);
+#pragma unroll
+    for (int k = 0; k < 13; ++k) root[k] = L.root[k];
+    L.imu_off = p_aff(p.imu_x_offset, r[4]);
+    b.curent_imu_x_offset[e] = L.imu_off;
     float *prop = b.dof_props + (size_t)e * D;
     if (p.random_damping) {
         const float damp = p_aff(p.steering_damping_range, r[5]);
@@ -150,10 +178,24 @@ __device__ void paper_reset_env(const tg_paper_params &p, const tg_paper_buffers
     b.curent_command[e] = 0.0f;
     b.yaw_command[e] = 0.0f;
     b.speed_no_noise[e] = 0.0f;
+    L.cmd = 0.0f;
+    L.yaw_cmd = 0.0f;
+}
+
+// reset_idx for env e (:609-692) by one wavefront
+__device__ void paper_reset_env(const tg_paper_params &p, const tg_paper_buffers &b, int e, const float *rd,
+                                uint32_t c_lo, uint32_t c_hi) {
+    paper_reset_lanes(p, b, e, true);
+    if (threadIdx.x % 64 != 0) return;
+    float r[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) r[k] = p_draw(p, rd, 9, e, k, c_lo, c_hi, P_TAG_RESET);
+    PaperLead L;
+    paper_reset_lead(p, b, e, r, b.root_reset + 13 * (size_t)e, L);
 }
 
 // compute_gogoro_observations (:771-808)
-__device__ void paper_observe(const float *root, float desired_yaw, float command, float delay_norm, float *obs) {
+__device__ __forceinline__ void paper_observe(const float *root, float desired_yaw, float command, float delay_norm, float *obs) {
     const float x = root[3], y = root[4], z = root[5], w = root[6];
     float roll = p_rem(atan2f(2.0f * (w * x + y * z), w * w - x * x - y * y + z * z), P_2PI);
     float yaw = p_rem(atan2f(2.0f * (w * z + x * y), w * w + x * x - y * y - z * z), P_2PI);
@@ -183,40 +225,103 @@ __device__ void paper_observe(const float *root, float desired_yaw, float comman
     obs[7] = delay_norm;
 }
 
-__global__ __launch_bounds__(64) void paper_post_kernel(tg_paper_params p, tg_paper_buffers b, const float *rd,
+__global__ __launch_bounds__(64 * PAPER_EPW) void paper_post_kernel(tg_paper_params p, tg_paper_buffers b, const float *rd,
                                                         const float *nd, const float *sd, const float *yd,
                                                         const float *pd, uint32_t c_lo, uint32_t c_hi) {
-    __shared__ float ob[PO], nz[PO];
-    const int e = blockIdx.x, lane = threadIdx.x;
+    // Every HBM input of the env is issued in one batch at the start (the
+    // lead lane's scalars and root-reset template, every lane's history
+    // entries), so the kernel waits on memory once; a reset replaces them by
+    // the reset values in registers.  The histories' command column and the
+    // newest entry go through LDS rather than back through HBM.
+    __shared__ float ob_[PAPER_EPW][PO], nz_[PAPER_EPW][PO], ch_[PAPER_EPW][PH];
+    const int wv = threadIdx.x / 64, lane = threadIdx.x % 64;
+    const int e = blockIdx.x * PAPER_EPW + wv;
+    if (e >= p.num_envs) return;
+    float *ob = ob_[wv], *nz = nz_[wv], *ch = ch_[wv];
+    // the step's 8 Philox blocks, one per lane (reset 3, noise 2, speed, yaw,
+    // push), so the lead lane only looks its draws up
+    __shared__ float dr_[PAPER_EPW][8][4];
+    float(*dr)[4] = dr_[wv];
+    if (lane < 8) {
+        const uint32_t tag = lane < 3 ? P_TAG_RESET + lane : lane < 5 ? P_TAG_NOISE + (lane - 3)
+                           : lane == 5 ? P_TAG_SPEED : lane == 6 ? P_TAG_YAW : P_TAG_PUSH;
+        const U4 x = philox(U4{(uint32_t)e, c_lo, c_hi, tag}, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+        dr[lane][0] = u01(x.x);
+        dr[lane][1] = u01(x.y);
+        dr[lane][2] = u01(x.z);
+        dr[lane][3] = u01(x.w);
+    }
+    // draw k of a kind whose Philox blocks start at blk: replay array or the block
+    auto draw = [&](const float *arr, int stride, int k, int blk) {
+        return arr ? arr[(size_t)stride * e + k] : dr[blk + (k >> 2)][k & 3];
+    };
+    const bool lead = lane == 0;
+    float *bo = b.buffer_obs + (size_t)PHO * e, *bn = b.buffer_obs_noisy + (size_t)PHO * e;
     const bool reset = b.reset_buf[e] != 0;
     const int64_t prog0 = b.progress_buf[e] + 1;
-    __syncthreads();
-    if (lane == 0) b.progress_buf[e] = prog0;
-    if (reset) paper_reset_env(p, b, e, rd, c_lo, c_hi);
-    __syncthreads();
+    float vc[3], vn[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const int i = lane + 64 * j;
+        vc[j] = vn[j] = 0.0f;
+        if (i < PHO - PO) {
+            vc[j] = bo[i + PO];
+            vn[j] = bn[i + PO];
+        }
+    }
+    PaperLead L;
+    float tpl[13], old6 = 0.0f;
+    if (lead) {
+        const float *rt = b.root + 13 * (size_t)e, *tp = b.root_reset + 13 * (size_t)e;
+#pragma unroll
+        for (int k = 0; k < 13; ++k) {
+            L.root[k] = rt[k];
+            tpl[k] = tp[k];
+        }
+        L.speed = b.curent_speed[e];
+        L.speed_off = b.curent_speed_offset[e];
+        L.imu_off = b.curent_imu_x_offset[e];
+        L.yaw_cmd = b.yaw_command[e];
+        L.cmd = b.curent_command[e];
+        L.delay = b.steer_delay[e];
+        old6 = bo[(PH - 1) * PO + 6];
+    }
     const int64_t prog = reset ? 0 : prog0;
-    float *bo = b.buffer_obs + (size_t)PHO * e, *bn = b.buffer_obs_noisy + (size_t)PHO * e;
-    if (lane == 0) {
+    p_wave_sync();   // the Philox blocks
+    if (reset) {
+        paper_reset_lanes(p, b, e, false);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) vc[j] = vn[j] = 0.0f;
+        if (lead) {
+            float r[9];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) r[k] = draw(rd, 9, k, 0);
+            paper_reset_lead(p, b, e, r, tpl, L);
+            old6 = 0.0f;
+        }
+    } else if (lead) {
+        b.progress_buf[e] = prog0;
+    }
+    if (lead) {
         const float dn = (float)((double)p.command_delay[1] - (double)p.command_delay[0]);
-        const float dl = (float)(b.steer_delay[e] - (int64_t)p.command_delay[0]) / dn;
+        const float dl = (float)(L.delay - (int64_t)p.command_delay[0]) / dn;
         float o[PO];
-        paper_observe(b.root + 13 * (size_t)e, b.yaw_command[e], b.curent_command[e], dl, o);
-        const float dcmd = bo[(PH - 1) * PO + 6] - o[6];   // clean[-2][6] - clean[-1][6] after the shift
+        paper_observe(L.root, L.yaw_cmd, L.cmd, dl, o);
+        const float dcmd = old6 - o[6];   // clean[-2][6] - clean[-1][6] after the shift
         // noisy newest entry (:521-542)
-        const uint32_t tag = 0x50414e5au;
         float u[6];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) u[k] = p_draw(p, nd, 6, e, k, c_lo, c_hi, tag);
+        for (int k = 0; k < 6; ++k) u[k] = draw(nd, 6, k, 3);
         float l[PO];
 #pragma unroll
         for (int k = 0; k < PO; ++k) l[k] = o[k];
         l[0] += p_aff(p.imu_filter_noise, u[0]);
         l[1] += p_aff(p.imu_filter_noise, u[1]);
-        l[0] += b.curent_imu_x_offset[e];
+        l[0] += L.imu_off;
         l[2] += p_aff(p.imu_noise, u[2]);
         l[3] += p_aff(p.imu_noise, u[3]);
         l[4] += p_aff(p.speed_sensor_noise, u[4]);
-        l[4] += b.curent_speed_offset[e];
+        l[4] += L.speed_off;
         l[4] = l[4] < 0.0f ? 0.0f : l[4];
         l[5] += p_aff(p.imu_filter_noise, u[5]);
         l[0] /= P_PI;
@@ -233,40 +338,35 @@ __global__ __launch_bounds__(64) void paper_post_kernel(tg_paper_params p, tg_pa
         for (int k = 0; k < PO; ++k) { ob[k] = o[k]; nz[k] = l[k]; }
         b.speed_no_noise[e] = o[4];
     }
-    __syncthreads();
-    // shift both histories by one entry and append
-    float vc[3], vn[3];
+    p_wave_sync();
+    // both histories shifted by one entry, the new one appended
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
         const int i = lane + 64 * j;
         if (i < PHO) {
-            vc[j] = i < PHO - PO ? bo[i + PO] : ob[i - (PHO - PO)];
-            vn[j] = i < PHO - PO ? bn[i + PO] : nz[i - (PHO - PO)];
+            if (i >= PHO - PO) {
+                vc[j] = ob[i - (PHO - PO)];
+                vn[j] = nz[i - (PHO - PO)];
+            }
             if ((i % PO) == 1) vn[j] = 0.0f;   // noisy[:, :, 1] = 0
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        const int i = lane + 64 * j;
-        if (i < PHO) {
+            if ((i % PO) == 6) ch[i / PO] = vc[j];
             bo[i] = vc[j];
             bn[i] = vn[j];
             b.obs_buf[(size_t)PHO * e + i] = vn[j];
         }
     }
-    __syncthreads();
+    p_wave_sync();
     // reward term 7 partial: sum_t (a[t+1] - a[t])^2, a = act / 0.5
     float dsq = 0.0f;
     if (lane < PH - 1) {
-        const float dd = bo[(lane + 1) * PO + 6] / 0.5f - bo[lane * PO + 6] / 0.5f;
+        const float dd = ch[lane + 1] / 0.5f - ch[lane] / 0.5f;
         dsq = dd * dd;
     }
     dsq = p_wsum(dsq);
-    if (lane == 0) {
+    if (lead) {
         b.scratch[e] = dsq;
-        // reward terms 1-5 (:722-746)
-        const float *last = bo + (PH - 1) * PO;
+        // reward terms 1-5 (:722-746) on the newest clean entry
+        const float *last = ob;
         const float tilt_err = p_clamp(last[0] / p.max_tilt, -1.0f, 1.0f);
         const float yaw_err = p_clamp(last[5] / P_PI, -1.0f, 1.0f);
         const float dtilt_err = p_clamp(last[2] / 0.3f, -1.0f, 1.0f);
@@ -279,9 +379,9 @@ __global__ __launch_bounds__(64) void paper_post_kernel(tg_paper_params p, tg_pa
         const float r5 = 1.0f - (act * act) * (tilt_w * dtilt_w);
         b.rew_buf[e] = r1 * 0.45f + r2 * 0.1f + r4 * 0.35f + r5 * 2.0f;
         // command changes (:402-417)
-        if (prog == p.speed_freq_update) b.curent_speed[e] = p_aff(p.speed_range, p_draw(p, sd, 1, e, 0, c_lo, c_hi, 0x50415344u));
-        float yc = b.yaw_command[e];
-        if (prog == p.yaw_freq_update) yc = -P_PI + p_draw(p, yd, 1, e, 0, c_lo, c_hi, 0x50415957u) * (float)(2.0 * 3.14159265358979323846);
+        if (prog == p.speed_freq_update) b.curent_speed[e] = p_aff(p.speed_range, draw(sd, 1, 0, 5));
+        float yc = L.yaw_cmd;
+        if (prog == p.yaw_freq_update) yc = -P_PI + draw(yd, 1, 0, 6) * (float)(2.0 * 3.14159265358979323846);
         yc = yc > P_PI ? yc - (float)(3.14159265358979323846 * 2) : yc;
         yc = yc < -P_PI ? yc + (float)(3.14159265358979323846 * 2) : yc;
         b.yaw_command[e] = yc;
@@ -289,15 +389,14 @@ __global__ __launch_bounds__(64) void paper_post_kernel(tg_paper_params p, tg_pa
         float *pert = b.perturbation + (size_t)(p.perturbation_stride ? p.perturbation_stride : 3) * e;
         if (p.push_robot && e < p.push_max_envs && (prog + 1) % p.push_interval == 0) {
             const float yaw = last[1];
-            const float xf = (p_draw(p, pd, 2, e, 0, c_lo, c_hi, 0x50415055u) * 2.0f - 1.0f) * p.push_force;
-            const float zf = -(p_draw(p, pd, 2, e, 1, c_lo, c_hi, 0x50415055u) * p.push_force);
+            const float xf = (draw(pd, 2, 0, 7) * 2.0f - 1.0f) * p.push_force;
+            const float zf = -(draw(pd, 2, 1, 7) * p.push_force);
             pert[0] = xf * cosf(yaw + P_PI / 2.0f);
             pert[1] = xf * sinf(yaw + P_PI / 2.0f);
             pert[2] = zf;
         }
         if (b.body_force) {   // root-group wrench: force at the head COM
-            const float *q = b.root + 13 * (size_t)e + 3;
-            const float x = q[0], y = q[1], z = q[2], w = q[3];
+            const float x = L.root[3], y = L.root[4], z = L.root[5], w = L.root[6];
             const float R[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w),
                                 2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w),
                                 2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)};
@@ -319,31 +418,49 @@ __global__ __launch_bounds__(64) void paper_post_kernel(tg_paper_params p, tg_pa
     }
 }
 
-// one workgroup: batch mean for reward term 7, rewards, resets, time_outs
-__global__ __launch_bounds__(1024) void paper_finish_kernel(tg_paper_params p, tg_paper_buffers b) {
-    __shared__ double part[1024];
+// batch mean for reward term 7, then rewards, resets, time_outs of the
+// workgroup's FIN_WG envs.  Every workgroup forms the whole batch sum itself
+// (the per-env partials are 4 B/env and L2-resident, and every workgroup adds
+// them in the same order, so all agree bit for bit): no second launch and no
+// single-workgroup tail whose dependent loads run one after another.
+constexpr int FIN_WG = 1024, FIN_UNROLL = 8;
+__global__ __launch_bounds__(FIN_WG) void paper_finish_kernel(tg_paper_params p, tg_paper_buffers b) {
+    __shared__ double part[FIN_WG / 64];
     const int t = threadIdx.x, n = p.num_envs;
+    const int e = blockIdx.x * FIN_WG + t;
+    // the env's own inputs first, so their latency overlaps the sum
+    float tilt = 0.f, rew = 0.f;
+    int64_t prog = 0;
+    if (e < n) {
+        tilt = b.buffer_obs[(size_t)PHO * e + (PH - 1) * PO];
+        prog = b.progress_buf[e];
+        rew = b.rew_buf[e];
+    }
     double s = 0.0;
-    for (int e = t; e < n; e += 1024) s += (double)b.scratch[e];
-    part[t] = s;
+    for (int e0 = t; e0 < n; e0 += FIN_WG * FIN_UNROLL) {
+        float v[FIN_UNROLL];
+#pragma unroll
+        for (int k = 0; k < FIN_UNROLL; ++k) v[k] = e0 + k * FIN_WG < n ? b.scratch[e0 + k * FIN_WG] : 0.f;
+#pragma unroll
+        for (int k = 0; k < FIN_UNROLL; ++k) s += (double)v[k];
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+    if ((t & 63) == 0) part[t >> 6] = s;
     __syncthreads();
-    for (int w = 512; w >= 1; w >>= 1) {
-        if (t < w) part[t] += part[t + w];
-        __syncthreads();
-    }
-    const float r7 = 1.0f - (float)(part[0] / ((double)n * (PH - 1)));
-    for (int e = t; e < n; e += 1024) {
-        const float tilt = b.buffer_obs[(size_t)PHO * e + (PH - 1) * PO];
-        const int64_t prog = b.progress_buf[e];
-        const bool finished = prog >= p.max_episode_length - 1;
-        const bool felt = fabsf(tilt) >= p.max_tilt;
-        float r = b.rew_buf[e] + r7 * 0.2f;
-        r = r < 0.0f ? 0.0f : r;
-        b.rew_buf[e] = felt ? -1.0f : r;
-        const bool rs = finished || felt;
-        b.reset_buf[e] = rs ? 1 : 0;
-        b.timeout_buf[e] = finished && rs;
-    }
+    double tot = 0.0;
+#pragma unroll
+    for (int w = 0; w < FIN_WG / 64; ++w) tot += part[w];
+    if (e >= n) return;
+    const float r7 = 1.0f - (float)(tot / ((double)n * (PH - 1)));
+    const bool finished = prog >= p.max_episode_length - 1;
+    const bool felt = fabsf(tilt) >= p.max_tilt;
+    float r = rew + r7 * 0.2f;
+    r = r < 0.0f ? 0.0f : r;
+    b.rew_buf[e] = felt ? -1.0f : r;
+    const bool rs = finished || felt;
+    b.reset_buf[e] = rs ? 1 : 0;
+    b.timeout_buf[e] = finished && rs;
 }
 
 __global__ __launch_bounds__(64) void paper_reset_idx_kernel(tg_paper_params p, tg_paper_buffers b, const int32_t *ids,
@@ -354,14 +471,16 @@ __global__ __launch_bounds__(64) void paper_reset_idx_kernel(tg_paper_params p, 
 }
 
 int launch_paper_pre(const tg_paper_params &p, const tg_paper_buffers &b, const float *actions, hipStream_t s) {
-    hipLaunchKernelGGL(paper_pre_kernel, dim3(p.num_envs), dim3(64), 0, s, p, b, actions);
+    hipLaunchKernelGGL(paper_pre_kernel, dim3((p.num_envs + PAPER_EPW - 1) / PAPER_EPW), dim3(64 * PAPER_EPW), 0, s, p,
+                       b, actions);
     return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
 }
 int launch_paper_post(const tg_paper_params &p, const tg_paper_buffers &b, const float *rd, const float *nd,
                       const float *sd, const float *yd, const float *pd, uint64_t counter, hipStream_t s) {
-    hipLaunchKernelGGL(paper_post_kernel, dim3(p.num_envs), dim3(64), 0, s, p, b, rd, nd, sd, yd, pd,
+    hipLaunchKernelGGL(paper_post_kernel, dim3((p.num_envs + PAPER_EPW - 1) / PAPER_EPW), dim3(64 * PAPER_EPW), 0, s,
+                       p, b, rd, nd, sd, yd, pd,
                        (uint32_t)counter, (uint32_t)(counter >> 32));
-    hipLaunchKernelGGL(paper_finish_kernel, dim3(1), dim3(1024), 0, s, p, b);
+    hipLaunchKernelGGL(paper_finish_kernel, dim3((p.num_envs + FIN_WG - 1) / FIN_WG), dim3(FIN_WG), 0, s, p, b);
     return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
 }
 int launch_paper_reset_idx(const tg_paper_params &p, const tg_paper_buffers &b, const int32_t *ids, int n,

@@ -413,6 +413,17 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
             if (owner) gogoro_pre_store(a.gp, e, a.D, ah, cmd, ts, vr);
         }
     }
+    // the walk pre-physics (tg_walk_step): the env's clamped actions and drive
+    // targets written once, lane = dof mod LPE; pass 2a reads the targets back
+    // like pos_tgt (the barrier below orders them within the workgroup)
+    if (a.pm_in_step && owner) {
+        for (int d = sub; d < D; d += LPE) {
+            const unsigned ed = (unsigned)e * (unsigned)D + (unsigned)d;
+            const float c = pm_clamp(a, a.pm_actions[ed]);
+            a.pm_act_out[ed] = c;
+            a.pm_tgt_out[ed] = pm_target(a, d, c);
+        }
+    }
     float *root = a.root + (size_t)e * 13;
     float *dofs = a.dof + (size_t)e * D * 2;
     __syncthreads();   // group tables (shared by both wavefronts)
@@ -499,8 +510,8 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         x[5] = PR(TG_PROP_LOWER, d);
         x[6] = PR(TG_PROP_UPPER, d);
         const unsigned ed = (unsigned)e * (unsigned)D + (unsigned)d;
-        // the walk pre-physics inside the step (tg_walk_step): the target from the action
-        x[7] = a.pm_in_step ? pm_target(a, d, pm_clamp(a, a.pm_actions[ed])) : a.pos_tgt[ed];
+        // the walk pre-physics inside the step (tg_walk_step): its targets, written above
+        x[7] = (a.pm_in_step ? a.pm_tgt_out : a.pos_tgt)[ed];
         x[8] = a.vel_tgt[ed];
         if constexpr (PL::TPON) {   // the Gogoro pre-physics inside the step (tg_gogoro_step)
             if (a.gp_in_step) {
