@@ -22,6 +22,7 @@ run thormangwalkdr16384 --task ThormangWalkDR --num-envs 16384 --no-cpu-baseline
 run gogoro4096 --task Gogoro
 run gogoro4096_terrain --task Gogoro --terrain
 run gogoropaper2048 --task GogoroPaper --num-envs 2048 --no-cpu-baseline
+run gogoropaper4096 --task GogoroPaper --no-cpu-baseline
 PROF_DIR=$OUT/prof_thormangwalk4096 BENCH_ARGS="--task ThormangWalk --steps 200 --warmup 30" bash scripts/gpu_profile.sh > $OUT/prof_t.log 2>&1 || exit $?
 PROF_DIR=$OUT/prof_gogoro4096 BENCH_ARGS="--task Gogoro --steps 200 --warmup 30" bash scripts/gpu_profile.sh > $OUT/prof_g.log 2>&1 || exit $?
 echo profiles ok
