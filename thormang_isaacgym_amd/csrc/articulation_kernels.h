@@ -873,13 +873,36 @@ struct WalkPost {
         for (int k = 0; k < 13; ++k) rt[k] = rt0[k];
         const int64_t prog = reset ? 0 : prog1;
         if (reset) {
+            // the env's 4 + 2D reset draws (walk_draw): Philox block j (draws
+            // 4j .. 4j + 3) computed once, on lane j mod LPE, and staged in the
+            // Delassus slots (dead after the contact solve) -- rather than one
+            // block per draw on the lane that uses it
+            using PL = ParLayout<M>;
+            constexpr int NRD = 4 + 2 * D, NB = (NRD + 3) / 4;
+            constexpr bool STAGE = PL::K * PL::K >= 4 * NB;
+            if (STAGE && !pa.reset_draws) {
+                for (int j = sub; j < NB; j += LPE) {
+                    const U4 x = philox(U4{(uint32_t)e, c_lo, c_hi, 0x57524530u + (uint32_t)j}, (uint32_t)p.seed,
+                                        (uint32_t)(p.seed >> 32));
+                    s(PL::W + 4 * j) = u01(x.x);
+                    s(PL::W + 4 * j + 1) = u01(x.y);
+                    s(PL::W + 4 * j + 2) = u01(x.z);
+                    s(PL::W + 4 * j + 3) = u01(x.w);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // the env's lanes share a wavefront
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            auto rdraw = [&](int k) {
+                if (!STAGE || pa.reset_draws) return walk_draw(p, pa.reset_draws, e, k, c_lo, c_hi);
+                return s(PL::W + k);
+            };
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
                 const int d = sub + LPE * r;
                 if (d < D) {
-                    q[r] = p.default_pos[d] +
-                           (walk_draw(p, pa.reset_draws, e, 4 + d, c_lo, c_hi) * 2.0f - 1.0f) * p.joint_noise;
-                    qd[r] = 0.1f * (walk_draw(p, pa.reset_draws, e, 4 + D + d, c_lo, c_hi) * 2.0f - 1.0f);
+                    q[r] = p.default_pos[d] + (rdraw(4 + d) * 2.0f - 1.0f) * p.joint_noise;
+                    qd[r] = 0.1f * (rdraw(4 + D + d) * 2.0f - 1.0f);
                     act[r] = la[r] = 0.f;
                     if (owner) b.actions[eD + d] = 0.f;
                 }
@@ -887,7 +910,7 @@ struct WalkPost {
             if (lead) {
                 float r4[4];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) r4[k] = walk_draw(p, pa.reset_draws, e, k, c_lo, c_hi);
+                for (int k = 0; k < 4; ++k) r4[k] = rdraw(k);
                 cmd[0] = p.cmd_vx[0] + r4[0] * (p.cmd_vx[1] - p.cmd_vx[0]);
                 cmd[1] = p.cmd_vy[0] + r4[1] * (p.cmd_vy[1] - p.cmd_vy[0]);
                 cmd[2] = p.cmd_wz[0] + r4[2] * (p.cmd_wz[1] - p.cmd_wz[0]);
@@ -982,11 +1005,11 @@ struct WalkPost {
         // push wrench for the next simulate (walk_post_kernel)
         float *f = b.body_force + (size_t)6 * p.num_groups * e;
         const bool push = p.push_force > 0.0f && p.push_interval > 0 && prog > 0 && (prog % p.push_interval) == 0;
-        float u[3];
+        float u[3] = {0.5f, 0.5f, 0.5f};
         if (pa.push_draws) {
 #pragma unroll
             for (int k = 0; k < 3; ++k) u[k] = pa.push_draws[3 * (size_t)e + k];
-        } else {
+        } else if (push) {   // (the block only where it is used)
             const U4 xx = philox(U4{(uint32_t)e, c_lo, c_hi, 0x50555348u}, (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
             u[0] = u01(xx.x); u[1] = u01(xx.y); u[2] = u01(xx.z);
         }

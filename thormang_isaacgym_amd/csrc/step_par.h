@@ -162,8 +162,21 @@ struct GInfo {
     int parent, dof, jt;
 };
 
+// the T at a 32-bit byte offset from a uniform base pointer (every per-env
+// buffer is far below 4 GiB)
+template <class T> __device__ __forceinline__ const T &at_u32(const float *base, unsigned byte_off) {
+    return *reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + byte_off);
+}
+
+// a table value known to lie in [lo, hi): lets the compiler form LDS / HBM
+// offsets from it with 24-bit multiplies instead of v_mad_u64_u32
+__device__ __forceinline__ int bounded(int v, int lo, int hi) {
+    __builtin_assume(v >= lo && v < hi);
+    return v;
+}
+
 template <class M> __device__ __forceinline__ GInfo ginfo(const int *gi, int g) {
-    const int *p = gi + g * ParLayout<M>::GIW;
+    const int *p = gi + bounded(g, 0, M::NG) * ParLayout<M>::GIW;
     return GInfo{p[GI_PARENT], p[GI_DOF], p[GI_JT]};
 }
 
@@ -352,7 +365,12 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
     const int *cpath = tab + PL::T_CPATH;
     const int tid = threadIdx.x;
     const int le = tid / LPE, sub = tid % LPE;
-    auto dsc = [&](int t) { return desc[t * LPE + sub]; };
+    auto dsc = [&](int t) {
+        I4 d = desc[t * LPE + sub];
+        d.x = bounded(d.x, 0, M::NG);
+        d.y = bounded(d.y, 0, M::NG);
+        return d;
+    };
     // XCD-aware chunk order: workgroups are dispatched round-robin over the 8
     // XCDs, so workgroup b takes env chunk (b % 8) * (nb / 8) + b / 8 and each
     // XCD's L2 sees a contiguous env range (the [KC][N] composite cache rows
@@ -393,10 +411,12 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
     // per-env inputs through 32-bit element offsets from the uniform base
     // pointers (scalar base + vector offset addressing, no 64-bit address math)
     const unsigned cbase = (unsigned)ein * M::KC;
-    auto CP = [&](int k) { return comp[cbase + (unsigned)k]; };
-    auto CP4 = [&](int k) { return *reinterpret_cast<const float4 *>(comp + (cbase + (unsigned)k)); };
+    // (byte offsets formed in 32 bits: the loads take the scalar-base +
+    // 32-bit vector-offset form, no 64-bit address arithmetic per load)
+    auto CP = [&](int k) { return at_u32<float>(comp, (cbase + (unsigned)k) * 4u); };
+    auto CP4 = [&](int k) { return at_u32<float4>(comp, (cbase + (unsigned)k) * 4u); };
     const unsigned ND = (unsigned)N * (unsigned)D, pbase = (unsigned)ein * (unsigned)D;
-    auto PR = [&](int f, int d) { return a.props[(unsigned)f * ND + pbase + (unsigned)d]; };
+    auto PR = [&](int f, int d) { return at_u32<float>(a.props, ((unsigned)f * ND + pbase + (unsigned)d) * 4u); };
     const bool lead = sub == 0;
 
     // the Gogoro pre-physics (tg_gogoro_step) on the env's lead lane, first of
@@ -428,7 +448,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
     float *dofs = a.dof + (size_t)e * D * 2;
     __syncthreads();   // group tables (shared by both wavefronts)
     for (int g = 1 + sub; g < M::NG; g += LPE) {
-        const int d = gi[g * GIW + GI_DOF];
+        const int d = bounded(gi[g * GIW + GI_DOF], 0, 1 << 16);
         s(g * GF + F_Q) = dofs[2 * d];
         s(g * GF + F_QD) = dofs[2 * d + 1];
     }
@@ -511,15 +531,15 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         x[6] = PR(TG_PROP_UPPER, d);
         const unsigned ed = (unsigned)e * (unsigned)D + (unsigned)d;
         // the walk pre-physics inside the step (tg_walk_step): its targets, written above
-        x[7] = (a.pm_in_step ? a.pm_tgt_out : a.pos_tgt)[ed];
-        x[8] = a.vel_tgt[ed];
+        x[7] = at_u32<float>(a.pm_in_step ? a.pm_tgt_out : a.pos_tgt, ed * 4u);
+        x[8] = at_u32<float>(a.vel_tgt, ed * 4u);
         if constexpr (PL::TPON) {   // the Gogoro pre-physics inside the step (tg_gogoro_step)
             if (a.gp_in_step) {
                 if (d == a.gp.dof_steer) x[7] = s(PL::TP + 6);
                 if (d == a.gp.dof_rear) x[8] = s(PL::TP + 7);
             }
         }
-        x[9] = a.act ? a.act[ed] : 0.f;
+        x[9] = a.act ? at_u32<float>(a.act, ed * 4u) : 0.f;
     };
     // pass 2: the children's contributions of the lane's group, n = the step's
     // largest child count: absent children read the zero block, so every load
@@ -565,7 +585,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
 #pragma unroll
         for (int r = 0; r < (M::NG + LPE - 1) / LPE; ++r) {
             const int g = 1 + sub + r * LPE;
-            vlim[r] = g < M::NG ? PR(TG_PROP_VELOCITY, gi[g * GIW + GI_DOF]) : 0.f;
+            vlim[r] = g < M::NG ? PR(TG_PROP_VELOCITY, bounded(gi[g * GIW + GI_DOF], 0, 1 << 16)) : 0.f;
         }
 #pragma unroll 1
         for (int cp = 0; cp < 2; ++cp) {
@@ -666,7 +686,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
 #pragma unroll
         for (int r = 0; r < NR1; ++r) {
             const int gc = min(max(sub + r * LPE, 1), M::NG - 1);
-            load_drv(gi[gc * GIW + GI_DOF], cdr[r]);
+            load_drv(bounded(gi[gc * GIW + GI_DOF], 0, 1 << 16), cdr[r]);
         }
 #pragma unroll
         for (int r = 0; r < NR1; ++r) {
@@ -703,7 +723,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
             // with D0 = S.I^A.S + armature: D = (1 + be) D0 + Dimp, tau + al D0
             // cb replaces v (dead after pass 1b) in F_V; on a SEPC rerun pass 1
             // was not rerun and F_V already holds cb
-            const SV cbv = crm(ldsv(s, o + F_V), qd * ldS(s, g, gi[g * GIW + GI_JT]));
+            const SV cbv = crm(ldsv(s, o + F_V), qd * ldS(s, g, bounded(gi[g * GIW + GI_JT], 0, 4)));
             if (valid) {
                 if (cp == 0) {
                     s(o + F_CL) = cl0;
@@ -723,7 +743,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
             const int g = sub + r * LPE;
             if (g > 0 && g < M::NG) {
                 const int o = g * GF;
-                const int d = gi[g * GIW + GI_DOF];
+                const int d = bounded(gi[g * GIW + GI_DOF], 0, 1 << 16);
                 float cd[10];
                 load_drv(d, cd);
                 const float q = s(o + F_Q), qd = s(o + F_QD), qdd0 = s(o + F_UU);
@@ -771,7 +791,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                 // with D0 = S.I^A.S + armature: D = (1 + be) D0 + Dimp, tau + al D0
                 // cb replaces v (dead after pass 1b) in F_V; on a SEPC rerun pass 1
                 // was not rerun and F_V already holds cb
-                if (!SEPC || cp == 0) stsv(s, o + F_V, crm(ldsv(s, o + F_V), qd * ldS(s, g, gi[g * GIW + GI_JT])));
+                if (!SEPC || cp == 0) stsv(s, o + F_V, crm(ldsv(s, o + F_V), qd * ldS(s, g, bounded(gi[g * GIW + GI_JT], 0, 4))));
                 s(o + F_DINV) = (1.f + be) * cd[0] + Dimp;
                 s(o + F_UU) = tau + al * cd[0];
                 s(o + F_QDS) = al;
@@ -1010,7 +1030,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                 stv3(s, PL::CGP + 12 * c + 9, pos + mul(R, ldv3(s, cg * GF + F_P)));
                 SV v = v0s;   // root frame: the root velocity plus the path's joint terms
                 for (int i = 0; i < M::cpath_len[c]; ++i) {
-                    const int hg = cpath[c * M::MAXD + i];
+                    const int hg = bounded(cpath[c * M::MAXD + i], -1, M::NG);
                     v = v + s(hg * GF + F_QDS) * ldS(s, hg, ginfo<M>(gi, hg).jt);
                 }
                 stsv(s, PL::CGV + 6 * c, v);
@@ -1366,7 +1386,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
 #pragma unroll
                         for (int j = 0; j < K; ++j)
                             if (M::shape_cg[row_shape<M>(j)] == c) acc += s(PL::LAM + j) * s(scr(j * SW + i));
-                        s(cpath[c * M::MAXD + i] * GF + F_UU) += acc;
+                        s(bounded(cpath[c * M::MAXD + i], -1, M::NG) * GF + F_UU) += acc;
                     }
                     TG_SYNC();
                 }
@@ -1499,7 +1519,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
             root[10] = wwo.x; root[11] = wwo.y; root[12] = wwo.z;
         }
         for (int g = 1 + sub; g < M::NG; g += LPE) {
-            const int d = gi[g * GIW + GI_DOF];
+            const int d = bounded(gi[g * GIW + GI_DOF], 0, 1 << 16);
             dofs[2 * d] = s(g * GF + F_Q);
             dofs[2 * d + 1] = s(g * GF + F_QD);
         }
