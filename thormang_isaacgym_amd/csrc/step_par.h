@@ -562,6 +562,13 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
             pA = pA + cv[c];
         }
     };
+    // one-round trees (the lane's group is g = sub): its drive / limit inputs
+    // are constant over the launch, so they are loaded once here instead of
+    // in every substep and again for the drive-clamp rerun
+    float cd1[10];
+    if constexpr (NR1 == 1) {
+        if (sub > 0 && sub < M::NG) load_drv(bounded(gi[sub * GIW + GI_DOF], 0, 1 << 16), cd1);
+    }
     // an epilogue's inputs it wants in flight for the whole step (P::prefetch)
     float xpre[P::NPRE > 0 ? P::NPRE : 1];
     if constexpr (P::NPRE > 0) P::template prefetch<M, LPE>(pa, a, e, sub, xpre);
@@ -743,9 +750,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
             const int g = sub + r * LPE;
             if (g > 0 && g < M::NG) {
                 const int o = g * GF;
-                const int d = bounded(gi[g * GIW + GI_DOF], 0, 1 << 16);
-                float cd[10];
-                load_drv(d, cd);
+                const float *cd = cd1;   // loaded once per launch (below the prologue)
                 const float q = s(o + F_Q), qd = s(o + F_QD), qdd0 = s(o + F_UU);
                 float Dimp = 0.f, tau = 0.f;
                 const int mode = (int)rintf(cd[1]);
