@@ -565,9 +565,12 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
     // one-round trees (the lane's group is g = sub): its drive / limit inputs
     // are constant over the launch, so they are loaded once here instead of
     // in every substep and again for the drive-clamp rerun
-    float cd1[10];
+    float cd1[10], vlim1 = 0.f, cin1[1][12];
     if constexpr (NR1 == 1) {
         if (sub > 0 && sub < M::NG) load_drv(bounded(gi[sub * GIW + GI_DOF], 0, 1 << 16), cd1);
+        // and the velocity limit of group 1 + sub, the composite of group sub
+        if (1 + sub < M::NG) vlim1 = PR(TG_PROP_VELOCITY, bounded(gi[(1 + sub) * GIW + GI_DOF], 0, 1 << 16));
+        load_inertia(cin1);
     }
     // an epilogue's inputs it wants in flight for the whole step (P::prefetch)
     float xpre[P::NPRE > 0 ? P::NPRE : 1];
@@ -589,10 +592,14 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         // velocity limits of the lane's groups (used by the integration at the
         // end of the substep), issued now so their latency is hidden
         float vlim[(M::NG + LPE - 1) / LPE];
+        if constexpr (NR1 == 1) {
+            vlim[0] = vlim1;
+        } else {
 #pragma unroll
         for (int r = 0; r < (M::NG + LPE - 1) / LPE; ++r) {
             const int g = 1 + sub + r * LPE;
             vlim[r] = g < M::NG ? PR(TG_PROP_VELOCITY, bounded(gi[g * GIW + GI_DOF], 0, 1 << 16)) : 0.f;
+        }
         }
 #pragma unroll 1
         for (int cp = 0; cp < 2; ++cp) {
@@ -612,7 +619,12 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         // which depend on the group's own pose and velocity only
         const V3 gr = mulT(R, grav);   // gravity in the root frame
         float cin[NR1][12];
-        load_inertia(cin);
+        if constexpr (NR1 == 1) {
+#pragma unroll
+            for (int k = 0; k < 12; ++k) cin[0][k] = cin1[0][k];
+        } else {
+            load_inertia(cin);
+        }
         if (lead) stsv(s, F_V, v0);
         TG_SYNC();
         auto body1 = [&](const I4 &dc, const float *ck) {
