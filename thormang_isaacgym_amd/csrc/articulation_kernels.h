@@ -845,11 +845,17 @@ struct WalkPost {
         const int64_t prog1 = b.progress_buf[e] + 1;
         const bool reset = b.reset_buf[e] != 0;
         float q[NR], qd[NR], act[NR], la[NR], pt[NR], cmd[3], rt[13];
+        // (the per-dof constants too: kernel-argument arrays indexed by lane
+        // are memory loads, which would otherwise be issued where they are
+        // used -- inside the reset branch and after it)
+        float dpos[NR], kst[NR];
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
             const int d = sub + LPE * r;
-            q[r] = qd[r] = act[r] = la[r] = pt[r] = 0.f;
+            q[r] = qd[r] = act[r] = la[r] = pt[r] = dpos[r] = kst[r] = 0.f;
             if (d < D) {
+                dpos[r] = p.default_pos[d];
+                kst[r] = p.stiffness[d];
                 const int g = DofGroup<M>::tab.g[d];
                 if (g > 0) {
                     q[r] = s(g * GF + F_Q);
@@ -869,6 +875,11 @@ struct WalkPost {
         }
 #pragma unroll
         for (int k = 0; k < 3; ++k) cmd[k] = b.commands[3 * (size_t)e + k];
+        float tpl[2] = {0.f, 0.f};   // a reset's spawn (x, y)
+        if (lead) {
+            tpl[0] = b.root_reset[13 * (size_t)e];
+            tpl[1] = b.root_reset[13 * (size_t)e + 1];
+        }
 #pragma unroll
         for (int k = 0; k < 13; ++k) rt[k] = rt0[k];
         const int64_t prog = reset ? 0 : prog1;
@@ -901,7 +912,7 @@ struct WalkPost {
             for (int r = 0; r < NR; ++r) {
                 const int d = sub + LPE * r;
                 if (d < D) {
-                    q[r] = p.default_pos[d] + (rdraw(4 + d) * 2.0f - 1.0f) * p.joint_noise;
+                    q[r] = dpos[r] + (rdraw(4 + d) * 2.0f - 1.0f) * p.joint_noise;
                     qd[r] = 0.1f * (rdraw(4 + D + d) * 2.0f - 1.0f);
                     act[r] = la[r] = 0.f;
                     if (owner) b.actions[eD + d] = 0.f;
@@ -915,7 +926,6 @@ struct WalkPost {
                 cmd[1] = p.cmd_vy[0] + r4[1] * (p.cmd_vy[1] - p.cmd_vy[0]);
                 cmd[2] = p.cmd_wz[0] + r4[2] * (p.cmd_wz[1] - p.cmd_wz[0]);
                 const float yaw = (r4[3] * 2.0f - 1.0f) * 3.14159265358979323846f;
-                const float *tpl = b.root_reset + 13 * (size_t)e;
                 rt[0] = tpl[0];
                 rt[1] = tpl[1];
                 rt[2] = p.spawn_height;
@@ -940,14 +950,14 @@ struct WalkPost {
             const int d = sub + LPE * r;
             if (d < D) {
                 if (owner) {
-                    o[13 + d] = clampw((q[r] - p.default_pos[d]) * p.dof_pos_scale, -co, co);
+                    o[13 + d] = clampw((q[r] - dpos[r]) * p.dof_pos_scale, -co, co);
                     o[13 + D + d] = clampw(qd[r] * p.dof_vel_scale, -co, co);
                     o[13 + 2 * D + d] = clampw(act[r], -co, co);
                     b.last_actions[eD + d] = act[r];   // (pm_in_step: actions / targets stored at kernel start)
                 }
                 rate += (act[r] - la[r]) * (act[r] - la[r]);
                 vel2 += qd[r] * qd[r];
-                const float tt = p.stiffness[d] * (pt[r] - q[r]);
+                const float tt = kst[r] * (pt[r] - q[r]);
                 tq += tt * tt;
             }
         }
