@@ -1202,6 +1202,9 @@ struct GogoroPost {
             cmdc = b.curent_command[e];
         }
         float yawc = b.yaw_command[e], imu = b.imu_offsets[e];
+        float tpl[3];   // a reset's spawn (x, y, z), with the other inputs rather than inside the reset branch
+#pragma unroll
+        for (int k = 0; k < 3; ++k) tpl[k] = b.root_reset[13 * (size_t)e + k];
         // ---- draws: lane l < 8 block l, the lead lane also block 8 (command resample)
         float v[3], v8[3];
         gogoro_post_block(sub < 8 ? sub : 7, e, pa.c_lo, pa.c_hi, k0, k1, v);
@@ -1232,7 +1235,6 @@ struct GogoroPost {
             const float target = (r[3] * 2.0f - 1.0f) * F_PI;
             const float rot = target + u_aff(-1.57f, 1.57f, r[4]);
             const float hh = rot / 2.0f;
-            const float *tpl = b.root_reset + 13 * (size_t)e;
             rt[0] = tpl[0];
             rt[1] = tpl[1];
             rt[2] = p.terrain_spawn ? tpl[2] : p.spawn_z;
