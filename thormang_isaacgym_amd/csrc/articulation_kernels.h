@@ -1202,9 +1202,12 @@ struct GogoroPost {
             cmdc = b.curent_command[e];
         }
         float yawc = b.yaw_command[e], imu = b.imu_offsets[e];
-        float tpl[3];   // a reset's spawn (x, y, z), with the other inputs rather than inside the reset branch
+        float tpl[3];   // a reset's spawn (x, y, z) and pose, with the other inputs rather than inside the reset branch
 #pragma unroll
         for (int k = 0; k < 3; ++k) tpl[k] = b.root_reset[13 * (size_t)e + k];
+        float pose[NR];
+#pragma unroll
+        for (int rr = 0; rr < NR; ++rr) pose[rr] = sub + LPE * rr < D ? b.thormang_pose[sub + LPE * rr] : 0.f;
         // ---- draws: lane l < 8 block l, the lead lane also block 8 (command resample)
         float v[3], v8[3];
         gogoro_post_block(sub < 8 ? sub : 7, e, pa.c_lo, pa.c_hi, k0, k1, v);
@@ -1227,7 +1230,7 @@ struct GogoroPost {
                 for (int rr = 0; rr < NR; ++rr) {
                     const int d = sub + LPE * rr;
                     if (d < D) {
-                        dofs[2 * d] = b.thormang_pose[d];
+                        dofs[2 * d] = pose[rr];
                         dofs[2 * d + 1] = 0.0f;
                     }
                 }
