@@ -16,6 +16,10 @@
  *                          changes, head pushes :442-459), then VecTask's
  *                          time_outs (vec_task.py:345)
  *   tg_paper_reset_idx     reset_idx for explicit env ids
+ *   tg_paper_step          the whole VecTask.step (GogoroPaper.step): the
+ *                          pre-physics as the first simulate's compose
+ *                          prologue, n_simulate simulates, the post-physics;
+ *                          the same results as the three calls above
  *
  * The module's debug switches (paper.py:23-34) are parameters with the
  * committed values as defaults: DEBUGFIXBASE (a sim parameter, fix_base),
@@ -107,6 +111,10 @@ int tg_paper_post_physics(tg_sim *sim, const tg_paper_params *p, const tg_paper_
                           const float *push_draws, uint64_t counter);
 int tg_paper_reset_idx(tg_sim *sim, const tg_paper_params *p, const tg_paper_buffers *b, const int32_t *ids,
                        int32_t n, const float *reset_draws, uint64_t counter);
+/* pre_physics_step + n_simulate x simulate + post_physics_step with in-kernel
+ * draws (counter: the post-physics call's) */
+int tg_paper_step(tg_sim *sim, const tg_paper_params *p, const tg_paper_buffers *b, const float *actions,
+                  int32_t n_simulate, uint64_t counter);
 
 #ifdef __cplusplus
 }

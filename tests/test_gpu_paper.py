@@ -161,3 +161,25 @@ def test_gpu_paper_2048_envs_run():
     assert torch.isfinite(obs["obs"]).all() and torch.isfinite(rew).all()
     assert torch.isfinite(env.root_tensor).all()
     assert float(env.head_perturbation.abs().max()) > 0.0   # pushes happened
+
+
+def test_gpu_paper_fused_step_equals_separate_calls(monkeypatch):
+    """tg_paper_step (the pre-physics as the first compose launch's prologue)
+    against the three separate calls (TG_PAPER_UNFUSED=1): the same kernels on
+    the same values, so every buffer agrees bit for bit."""
+    _cuda()
+    import thormang_isaacgym_amd as tia
+    out = []
+    for unfused in ("0", "1"):
+        monkeypatch.setenv("TG_PAPER_UNFUSED", unfused)
+        env = tia.make(seed=11, task="GogoroPaper", num_envs=256, sim_device="cuda:0", rl_device="cuda:0")
+        g = torch.Generator(device="cuda:0").manual_seed(9)
+        for _ in range(150):
+            obs, rew, reset, extras = env.step(torch.rand(256, 1, device="cuda:0", generator=g) * 2 - 1)
+        torch.cuda.synchronize()
+        out.append([t.detach().cpu().clone() for t in (obs["obs"], rew, reset, extras["time_outs"], env.root_tensor,
+                                                        env.sim.dof_pos_target, env.sim.dof_vel_target,
+                                                        env.progress_buf)])
+        assert int(out[-1][2].sum()) >= 0
+    for a, b in zip(*out):
+        assert torch.equal(a, b)

@@ -60,6 +60,8 @@ SIGNATURES = {
                               _VP, _VP, C.c_uint64],
     "tg_paper_reset_idx": [_VP, C.POINTER(abi.tg_paper_params), C.POINTER(abi.tg_paper_buffers), _VP, C.c_int32,
                            _VP, C.c_uint64],
+    "tg_paper_step": [_VP, C.POINTER(abi.tg_paper_params), C.POINTER(abi.tg_paper_buffers), _VP, C.c_int32,
+                      C.c_uint64],
     "tg_walk_pre_physics": [_VP, C.POINTER(abi.tg_walk_params), C.POINTER(abi.tg_walk_buffers), _VP],
     "tg_walk_step": [_VP, C.POINTER(abi.tg_walk_params), C.POINTER(abi.tg_walk_buffers), _VP, C.c_int32, _VP, _VP,
                      C.c_uint64],

@@ -144,6 +144,36 @@ __device__ __forceinline__ void gogoro_pre_prologue(const GogoroPre &g, int e, i
     gogoro_pre_store(g, e, D, ah, cmd, ts, vr);
 }
 
+// the GogoroPaper pre_physics_step (paper_pre_kernel in gogoro_paper_task.hip,
+// the same operations) for env e by its compose wavefront: the command history
+// shifted in registers (lane = slot), the delayed command taken from its lane,
+// the drive target rows written lane-strided
+__device__ __forceinline__ void paper_pre_prologue(const PaperPre &pp, int e, int D, int lane) {
+    constexpr int PC = TG_PAPER_CMD_HIST;
+    static_assert(PC <= 64, "one history slot per lane");
+    float *h = pp.command_history + PC * (size_t)e;
+    const float act = pp.actions[e];
+    const float ac = act < -1.0f ? -1.0f : (act > 1.0f ? 1.0f : act);
+    const float cmd = ac * pp.max_steering;
+    const float hn = lane < PC - 1 ? h[lane + 1] : 0.0f;
+    const int64_t delay = pp.use_steer_delay ? pp.steer_delay[e] : 0;
+    const float speed = pp.curent_speed[e];
+    const float hv = lane < PC - 1 ? hn : cmd;
+    int idx = PC - 3;
+    if (pp.use_steer_delay) idx = delay == 0 ? 0 : (int)(PC - delay);   // command_history[:, -steer_delay]
+    const float steer = __shfl(hv, idx, 64);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // every lane's history read before the stores
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane < PC) h[lane] = hv;
+    float *pt = pp.pos_target + (size_t)D * e, *vt = pp.vel_target + (size_t)D * e;
+    for (int d = lane; d < D; d += 64) {
+        pt[d] = d == pp.dof_steer ? steer : 0.0f;
+        vt[d] = d == pp.dof_rear ? speed : 0.0f;
+    }
+    if (lane == 0) pp.curent_command[e] = cmd;
+}
+
 template <class M>
 __device__ __forceinline__ void rb_force_env(const float *root, const float *dof, const float *comp, int e,
                                              const float *mass_scale, const float *forces, const float *torques,
@@ -458,6 +488,7 @@ template <class M> __global__ __launch_bounds__(64 * COMPOSE_WPB) void compose_k
     if (a.cnext && blockIdx.x == 0 && threadIdx.x == 0) *a.cnext = 0;   // the reset list the next epilogue fills
     if (a.pm_actions && !a.pm_in_step && e < a.N) target_prologue(a, e, threadIdx.x % 64);
     if (a.gp.actions && !a.gp_in_step && e < a.N && threadIdx.x % 64 == 0) gogoro_pre_prologue(a.gp, e, a.D);
+    if (a.pp.actions && e < a.N) paper_pre_prologue(a.pp, e, a.D, threadIdx.x % 64);
     __shared__ ComposeLds<M> cs[COMPOSE_WPB];
     if (dirty) compose_env<M>(a, e, threadIdx.x % 64, cs[wv]);
     if (a.rbf_forces && e < a.N)   // a pending apply_rigid_body_force_tensors, on the fresh composite

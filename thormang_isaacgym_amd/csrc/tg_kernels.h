@@ -26,6 +26,18 @@ struct GogoroPre {
     uint32_t k0, k1, c_lo, c_hi;
 };
 
+// the GogoroPaper pre-physics (paper_pre_kernel) as a compose prologue:
+// one wavefront per env, lane = command-history slot / dof
+struct PaperPre {
+    const float *actions;     // [N] (null: none)
+    float *command_history;   // [N, TG_PAPER_CMD_HIST]
+    const int64_t *steer_delay;
+    const float *curent_speed;
+    float *curent_command, *pos_target, *vel_target;
+    float max_steering;
+    int use_steer_delay, dof_steer, dof_rear;
+};
+
 struct StepArgs {
     int N, D;
     float h;
@@ -57,6 +69,7 @@ struct StepArgs {
     float pm_scale, pm_clip;
     float pm_default[TG_PM_MAX_DOF];
     GogoroPre gp;
+    PaperPre pp;
     // pm_in_step: the walk prologue runs inside the step kernel instead (the
     // drive targets are formed from pm_actions where pass 2a loads them, the
     // fused WalkPost epilogue writes pm_act_out / pm_tgt_out); skip_compose:

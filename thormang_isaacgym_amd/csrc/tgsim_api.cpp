@@ -468,7 +468,9 @@ static int simulate_args(tg_sim *s, const tg::StepArgs &a_in, const tg::WalkPost
     const bool gogoro_prologue = a.gp.actions && !a.gp_in_step;
     // (a pending per-link force tensor with listed envs: the full compose, which
     // reduces it after composing them)
-    const bool full = s->dirty_possible || s->always_compose || walk_prologue || (s->rbf_pending && s->list_pending);
+    const bool paper_prologue = a.pp.actions != nullptr;   // (one wavefront per env: the full compose launch)
+    const bool full = s->dirty_possible || s->always_compose || walk_prologue || paper_prologue ||
+                      (s->rbf_pending && s->list_pending);
     a.skip_compose = !full && !s->list_pending && !gogoro_prologue;
     a.compose_list = !full && !a.skip_compose;
     a.cnext = s->ccount + s->list_cur;
@@ -833,6 +835,35 @@ int tg_paper_pre_physics(tg_sim *s, const tg_paper_params *p, const tg_paper_buf
     s->dirty_possible = true;
     if (!actions) return fail(TG_ERR_ARG, "paper: null actions");
     if (int rc = tg::launch_paper_pre(*p, *b, actions, s->stream)) return fail(rc, "launch failed");
+    return TG_OK;
+}
+
+int tg_paper_step(tg_sim *s, const tg_paper_params *p, const tg_paper_buffers *b, const float *actions,
+                  int32_t n_simulate, uint64_t counter) {
+    if (int rc = check_paper(s, p, b)) return rc;
+    if (!actions) return fail(TG_ERR_ARG, "paper: null actions");
+    if (n_simulate < 1) return fail(TG_ERR_ARG, "tg_paper_step: n_simulate %d < 1", n_simulate);
+    for (int i = 0; i < n_simulate; ++i) {
+        tg::StepArgs a = step_args(s);
+        if (i == 0) {   // pre_physics_step as the first compose launch's prologue
+            tg::PaperPre &q = a.pp;
+            q.actions = actions;
+            q.command_history = b->command_history;
+            q.steer_delay = b->steer_delay;
+            q.curent_speed = b->curent_speed;
+            q.curent_command = b->curent_command;
+            q.pos_target = b->pos_target;
+            q.vel_target = b->vel_target;
+            q.max_steering = p->max_steering;
+            q.use_steer_delay = p->use_steer_delay;
+            q.dof_steer = p->dof_steer;
+            q.dof_rear = p->dof_rear;
+        }
+        if (int rc = simulate_args(s, a)) return rc < 0 ? rc : fail(TG_ERR_STATE, "no step kernel for this model");
+    }
+    if (int rc = tg::launch_paper_post(*p, *b, nullptr, nullptr, nullptr, nullptr, nullptr, counter, s->stream))
+        return fail(rc, "launch failed");
+    s->dirty_possible = true;   // the post kernel's resets rewrite properties and mark envs dirty
     return TG_OK;
 }
 

@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 
 import numpy as np
 import torch
@@ -316,6 +317,9 @@ class Gogoro(VecTask):
         check(lib().tg_paper_post_physics(self.sim.handle, C.byref(self.params), C.byref(self._bufs), _p(rd), _p(nd),
                                           _p(sd), _p(yd), _p(pd), self._counter()), "tg_paper_post_physics")
         self._keep_post = keep
+        self._post_host()
+
+    def _post_host(self):
         self.curent_step += 1
         if self.switches["PUSH_ROBOT"]:   # :449-457, the reference's own [N*L, 3] tensor
             self.sim.apply_rigid_body_force_tensors(torch.flatten(self._perturbations, end_dim=-2), None)
@@ -324,10 +328,22 @@ class Gogoro(VecTask):
         raise NotImplementedError("compute_obs_rwd runs inside the fused post-physics kernel")
 
     def step(self, actions):
-        self.pre_physics_step(actions)
-        for _ in range(self.control_freq_inv):
-            self.simulate()
-        self.post_physics_step()
+        if self.draw_source is None and os.environ.get("TG_PAPER_UNFUSED", "0") != "1":
+            # pre_physics_step + control_freq_inv x simulate + post_physics_step in
+            # one library call (tg_paper_step: the pre-physics rides in the first
+            # simulate's compose launch); the same Philox counters as the separate calls
+            a = actions.to(device=self.device, dtype=torch.float32).contiguous()
+            self._counter()   # the pre-physics call's counter (its kernel draws nothing)
+            check(lib().tg_paper_step(self.sim.handle, C.byref(self.params), C.byref(self._bufs), _p(a),
+                                      self.control_freq_inv, self._counter()), "tg_paper_step")
+            self._keep = a
+            self.frame_count += self.control_freq_inv
+            self._post_host()
+        else:
+            self.pre_physics_step(actions)
+            for _ in range(self.control_freq_inv):
+                self.simulate()
+            self.post_physics_step()
         self.extras["time_outs"] = self.timeout_buf
         self.obs_dict["obs"] = torch.clamp(self.obs_buf, -self.clip_obs, self.clip_obs) \
             if math.isfinite(self.clip_obs) else self.obs_buf
