@@ -218,9 +218,40 @@ def cpu_baseline(task_name: str, num_envs: int, threads: int, terrain_env=None):
         env.step(rs.uniform(-1, 1, shape).astype(np.float32))
         steps += 1
     dt = time.perf_counter() - t0
-    return {"value": num_envs * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{task_name} {num_envs} envs x {steps} steps (oracle/ fp64 physics + C task restatement, "
-                      f"OpenMP {threads} threads) = {dt:.1f} s"}
+    out = {"value": num_envs * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+           "sample": f"{task_name} {num_envs} envs x {steps} steps (oracle/ fp64 physics + C task restatement, "
+                     f"OpenMP {threads} threads) = {dt:.1f} s"}
+    if task_name == "Gogoro":
+        out["post_physics_only"] = post_physics_only(num_envs)
+    return out
+
+
+def post_physics_only(num_envs: int) -> dict:
+    """BASELINE.md's second context figure on this host: the reference's
+    post-physics math alone (compute_gogoro_observations +
+    compute_gogoro_reward, tasks/gogoro_new.py:645-723) -- here as the oracle's
+    C restatement of it (oracle/gogoro_task.c), one thread, no physics."""
+    from tests.oracle_lib import lib, ptr
+    L = lib()
+    rs = np.random.default_rng(7)
+    root = rs.normal(0, 0.3, (num_envs, 13)).astype(np.float32)
+    q = rs.normal(0, 1, (num_envs, 4)).astype(np.float32)
+    root[:, 3:7] = q / np.linalg.norm(q, axis=1, keepdims=True)
+    yaw = rs.uniform(-np.pi, np.pi, num_envs).astype(np.float32)
+    cmd = rs.uniform(-0.5, 0.5, num_envs).astype(np.float32)
+    ah = rs.uniform(-1, 1, (num_envs, 5)).astype(np.float32)
+    prog = rs.integers(0, 1000, num_envs).astype(np.int64)
+    obs = np.zeros((num_envs, 6), np.float32)
+    rew = np.zeros(num_envs, np.float32)
+    rst = np.zeros(num_envs, np.int64)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < 1.0:
+        L.oracle_gogoro_observations(num_envs, ptr(root), ptr(yaw), ptr(cmd), ptr(obs))
+        L.oracle_gogoro_reward(num_envs, ptr(obs), ptr(prog), ptr(ah), 1000, ptr(rew), ptr(rst))
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": num_envs * n / dt, "unit": "env-steps/s", "cores": 1,
+            "sample": f"observations + reward of {num_envs} envs x {n} calls, one thread = {dt:.2f} s"}
 
 
 def main():
