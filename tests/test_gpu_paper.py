@@ -183,3 +183,45 @@ def test_gpu_paper_fused_step_equals_separate_calls(monkeypatch):
         assert int(out[-1][2].sum()) >= 0
     for a, b in zip(*out):
         assert torch.equal(a, b)
+
+
+def test_gpu_paper_inplace_seat_composites_equal_a_full_compose():
+    """GogoroPaper resets draw new seat windows (base_x/y/z, paper.py:681-688);
+    on the V12 model (codegen FUSED bit 4) the post kernel updates the rider's
+    composite in place (tl_update) instead of marking the env for a compose.
+    After 80 steps with many resets the composite every env holds equals a
+    from-scratch compose (tg_composite) to fp32 rounding -- and the in-place
+    path was taken (no env left dirty)."""
+    _cuda()
+    import ctypes as C
+    import thormang_isaacgym_amd as tia
+    from thormang_isaacgym_amd import abi
+    from thormang_isaacgym_amd._lib import lib
+    from thormang_isaacgym_amd.model import codegen
+    n = 512
+    with switches(FLIPPED):   # free base, random seat windows and steering damping
+        env = tia.make(seed=21, task="GogoroPaper", num_envs=n, sim_device="cuda:0", rl_device="cuda:0")
+        m = env.sim.model
+        assert codegen.fused_tasks(m) & 4 and codegen.translating_locks(m, abi.ModelDesc(m).arrays)["NTL"] == 3
+        g = torch.Generator(device="cuda:0").manual_seed(6)
+        n_reset = 0
+        for t in range(80):
+            if t % 8 == 0:   # flag a random quarter of the envs: the next post-physics resets them
+                env.reset_buf[torch.rand(n, device="cuda:0", generator=g) < 0.25] = 1
+            n_reset += int(env.reset_buf.sum())
+            env.step(torch.rand(n, 1, device="cuda:0", generator=g) * 2 - 1)
+        torch.cuda.synchronize()
+    assert n_reset > 20
+    assert int(env.sim.env_dirty.sum()) == 0   # the resets left nothing to compose
+    kc_main = 24 * m.num_groups + 12 * len(m.shapes)
+    out = [torch.empty(n * 4096, device="cuda:0") for _ in range(2)]
+    for k, rec in enumerate((0, 1)):
+        assert lib().tg_composite(env.sim.handle, C.c_void_p(out[k].data_ptr()), rec) == 0
+    torch.cuda.synchronize()
+    t = codegen.translating_locks(m, abi.ModelDesc(m).arrays)
+    kc = kc_main + t["KX"] + ((3 * m.num_bodies + 3) & ~3)   # + the link com block
+    a = out[0][: n * kc].view(n, kc)[:, :kc_main]
+    b = out[1][: n * kc].view(n, kc)[:, :kc_main]
+    assert torch.isfinite(a).all() and torch.isfinite(b).all()
+    err = (a - b).abs() / (1.0 + b.abs())
+    assert float(err.max()) < 2e-6, float(err.max())

@@ -168,15 +168,15 @@ int launch_body_states(uint64_t hash, const float *root, const float *dof, int n
 #define TG_RB_FORCES(MODEL)                                                                               \
     if (hash == MODEL::hash) {                                                                            \
         hipLaunchKernelGGL(rb_force_kernel<MODEL>, dim3(n), dim3(64), 0, stream, root, dof, comp, n,        \
-                           mass_scale, forces, torques, space, out);                                      \
+                           mass_scale, forces, torques, space, out, props);                               \
         return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;                                          \
     }
 
 int launch_rb_forces(uint64_t hash, const float *root, const float *dof, const float *comp, int n,
                      const float *mass_scale, const float *forces, const float *torques, int space, float *out,
-                     hipStream_t stream) {
+                     const float *props, hipStream_t stream) {
     TG_FOR_EACH_MODEL(TG_RB_FORCES)
-    return jit_launch_rb_forces(hash, root, dof, comp, n, mass_scale, forces, torques, space, out, stream);
+    return jit_launch_rb_forces(hash, root, dof, comp, n, mass_scale, forces, torques, space, out, props, stream);
 }
 
 int compiled_hashes(uint64_t *out, int cap) {

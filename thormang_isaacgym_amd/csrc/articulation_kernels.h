@@ -56,7 +56,7 @@ __device__ __forceinline__ float prop(const StepArgs &a, int f, int e, int d) {
 // parallel, then lane g sums group g's links in link order (deterministic, the
 // order of oracle/physics_ref.c) and writes the group's cache rows.
 #ifdef TG_SECTION_PROF
-__device__ unsigned long long tg_cprof_acc[8];   // compose sections, lane 0 of every composed env
+static __device__ unsigned long long tg_cprof_acc[8];   // compose sections, lane 0 of every composed env
 #define TG_CPROF_INIT unsigned long long tg_c0 = clock64();
 #define TG_CPROF(k)                                                              \
     {                                                                            \
@@ -177,7 +177,8 @@ __device__ __forceinline__ void paper_pre_prologue(const PaperPre &pp, int e, in
 template <class M>
 __device__ __forceinline__ void rb_force_env(const float *root, const float *dof, const float *comp, int e,
                                              const float *mass_scale, const float *forces, const float *torques,
-                                             int space, float *out, int lane, float (*T)[12], float (*F)[10]);
+                                             int space, float *out, int lane, float (*T)[12], float (*F)[10],
+                                             const float *props, int N);
 
 // one wavefront's compose scratch
 template <class M> struct ComposeLds {
@@ -493,7 +494,7 @@ template <class M> __global__ __launch_bounds__(64 * COMPOSE_WPB) void compose_k
     if (dirty) compose_env<M>(a, e, threadIdx.x % 64, cs[wv]);
     if (a.rbf_forces && e < a.N)   // a pending apply_rigid_body_force_tensors, on the fresh composite
         rb_force_env<M>(a.root, a.dof, a.comp, e, a.mass_scale, a.rbf_forces, a.rbf_torques, a.rbf_space, a.rbf_out,
-                        threadIdx.x % 64, cs[wv].T, cs[wv].LM);
+                        threadIdx.x % 64, cs[wv].T, cs[wv].LM, a.props, a.N);
 }
 
 // Compose of the envs a fused task epilogue reset (tg_gogoro_step): the
@@ -642,7 +643,8 @@ template <class M> constexpr int max_group_depth() {
 template <class M>
 __device__ __forceinline__ void rb_force_env(const float *root, const float *dof, const float *comp, int e,
                                              const float *mass_scale, const float *forces, const float *torques,
-                                             int space, float *out, int lane, float (*T)[12], float (*F)[10]) {
+                                             int space, float *out, int lane, float (*T)[12], float (*F)[10],
+                                             const float *props, int N) {
     const float *r = root + 13 * (size_t)e;
     const float *q = dof + 2 * (size_t)e * M::ND;
     auto wsync = [] {
@@ -706,13 +708,37 @@ __device__ __forceinline__ void rb_force_env(const float *root, const float *dof
                 }
                 wsync();
             }
+            // models whose resets move translating locks in place (tl_update):
+            // the link coms below a lock are the composed ones shifted by the
+            // lock's displacement since that compose, from the current window
+            V3 ush[M::NTL > 0 ? M::NTL : 1];
+            if constexpr (M::NTL > 0) {
+                const size_t ND = (size_t)N * M::ND;
+#pragma unroll
+                for (int k = 0; k < M::NTL; ++k) {
+                    const size_t i = (size_t)e * M::ND + M::tl_dof[k];
+                    const float qc = 0.5f * (props[TG_PROP_LOWER * ND + i] + props[TG_PROP_UPPER * ND + i]);
+                    const float *xk = c + CL::xk(k);
+                    ush[k] = (qc - xk[0]) * v3(xk[5], xk[6], xk[7]);
+                }
+            }
             for (int l = lane; l < M::NL; l += 64) {
                 const int g = M::link_group[l];
                 M3 W;
 #pragma unroll
                 for (int k = 0; k < 9; ++k) W.a[k] = T[g][k];
-                const V3 d = v3(c[CL::lcom(l)], c[CL::lcom(l) + 1], c[CL::lcom(l) + 2]) -
-                             v3(c[CL::inertia(g) + 1], c[CL::inertia(g) + 2], c[CL::inertia(g) + 3]);
+                V3 lc = v3(c[CL::lcom(l)], c[CL::lcom(l) + 1], c[CL::lcom(l) + 2]);
+                if constexpr (M::NTL > 0) {
+                    if (g == M::tl_group && M::link_tl[l]) {
+                        V3 sh = v3(0, 0, 0);
+#pragma unroll
+                        for (int k = 0; k < M::NTL; ++k)
+                            if ((M::link_tl[l] >> k) & 1) sh = sh + ush[k];
+                        const float *qg = M::gq[g];
+                        lc = lc + mulT(M3{{qg[0], qg[1], qg[2], qg[3], qg[4], qg[5], qg[6], qg[7], qg[8]}}, sh);
+                    }
+                }
+                const V3 d = lc - v3(c[CL::inertia(g) + 1], c[CL::inertia(g) + 2], c[CL::inertia(g) + 3]);
                 const V3 arm = mul(W, d);
                 const size_t i = (size_t)e * M::NL + l;
                 const V3 f = v3(forces[3 * i], forces[3 * i + 1], forces[3 * i + 2]);
@@ -814,12 +840,13 @@ __device__ __forceinline__ void rb_force_env(const float *root, const float *dof
 template <class M> __global__ __launch_bounds__(64) void rb_force_kernel(const float *root, const float *dof,
                                                                          const float *comp, int n,
                                                                          const float *mass_scale, const float *forces,
-                                                                         const float *torques, int space, float *out) {
+                                                                         const float *torques, int space, float *out,
+                                                                         const float *props) {
     const int e = blockIdx.x;
     if (e >= n) return;
     __shared__ float T[M::NL][12];   // link pose: R (9), p (3)
     __shared__ float F[M::NL][10];   // link com (3), mass, force (3), torque (3)
-    rb_force_env<M>(root, dof, comp, e, mass_scale, forces, torques, space, out, threadIdx.x, T, F);
+    rb_force_env<M>(root, dof, comp, e, mass_scale, forces, torques, space, out, threadIdx.x, T, F, props, n);
 }
 
 // ---------------------------------------------------------------- contact row layout

@@ -16,8 +16,12 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <type_traits>
+
 #include "../../include/tg_gogoro_paper.h"
 #include "tg_kernels.h"
+#include "generated/models.inc"
+#include "articulation_kernels.h"   // CompLayout, tl_update: in-place seat composites
 
 namespace tg {
 
@@ -119,8 +123,13 @@ __device__ void paper_reset_lanes(const tg_paper_params &p, const tg_paper_buffe
 
 // reset_idx for env e, lead-lane part: the draws and the scalar state, written
 // to HBM and returned in L (tpl: the env's root reset template)
+// (M: a model whose seat chain is a set of translating locks and comp its
+// composite cache: the new seat windows update the composite in place
+// (tl_update) instead of marking the env for a compose; M = void: mark it)
+template <class M = void>
 __device__ __forceinline__ void paper_reset_lead(const tg_paper_params &p, const tg_paper_buffers &b, int e,
-                                                 const float *r, const float *tpl, PaperLead &L) {
+                                                 const float *r, const float *tpl, PaperLead &L,
+                                                 float *comp = nullptr) {
     const int D = p.num_dof;
     const size_t ND = (size_t)p.num_envs * D;
     L.speed = p_aff(p.speed_range, r[0]);
@@ -159,19 +168,44 @@ __device__ __forceinline__ void paper_reset_lead(const tg_paper_params &p, const
         prop[TG_PROP_DAMPING * ND + st] = damp;
         prop[TG_PROP_EFFORT * ND + st] = p.damping_effort;
         prop[TG_PROP_VELOCITY * ND + st] = p.damping_velocity;
-        b.env_dirty[e] = 1;
+        // (a drive gain: read by the step kernel directly, no compose needed --
+        // but the generic path keeps marking the env)
+        if (!comp) b.env_dirty[e] = 1;
     }
     if (!p.center_robot) {
         const int seat[3] = {p.dof_base_x, p.dof_base_y, p.dof_base_z};
         const float *rg[3] = {p.seat_offset_x_range, p.seat_offset_y_range, p.seat_offset_z_range};
+        float lo[3], hi[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            const float lo = p_aff(rg[k], r[6 + k]);
+            lo[k] = p_aff(rg[k], r[6 + k]);
+            hi[k] = (float)((double)lo[k] + 0.0001);
             prop[TG_PROP_DRIVE_MODE * ND + seat[k]] = 0.0f;
-            prop[TG_PROP_LOWER * ND + seat[k]] = lo;
-            prop[TG_PROP_UPPER * ND + seat[k]] = (float)((double)lo + 0.0001);
+            prop[TG_PROP_LOWER * ND + seat[k]] = lo[k];
+            prop[TG_PROP_UPPER * ND + seat[k]] = hi[k];
         }
-        b.env_dirty[e] = 1;
+        bool inplace = false;
+        if constexpr (!std::is_void<M>::value) {
+            if constexpr (M::NTL > 0) {
+                if (comp) {
+                    // the seat windows only translate the rider: its composite
+                    // from the moments the last compose stored (tl_update) at
+                    // the new window centres, as compose_env pins them
+                    float qn[M::NTL];
+#pragma unroll
+                    for (int k = 0; k < M::NTL; ++k) {
+                        qn[k] = 0.f;
+#pragma unroll
+                        for (int j = 0; j < 3; ++j)
+                            if (seat[j] == M::tl_dof[k]) qn[k] = 0.5f * (lo[j] + hi[j]);
+                    }
+                    float *c = comp + (size_t)e * M::KC;
+                    tl_update<M>(c, c + CompLayout<M>::ext(), qn);
+                    inplace = true;
+                }
+            }
+        }
+        if (!inplace) b.env_dirty[e] = 1;
     }
     b.progress_buf[e] = 0;
     b.reset_buf[e] = 0;
@@ -225,9 +259,12 @@ __device__ __forceinline__ void paper_observe(const float *root, float desired_y
     obs[7] = delay_norm;
 }
 
+// M (comp non-null): the sim's model with in-place seat composites (codegen
+// FUSED bit 4), void: resets mark their envs for a compose
+template <class M>
 __global__ __launch_bounds__(64 * PAPER_EPW) void paper_post_kernel(tg_paper_params p, tg_paper_buffers b, const float *rd,
                                                         const float *nd, const float *sd, const float *yd,
-                                                        const float *pd, uint32_t c_lo, uint32_t c_hi) {
+                                                        const float *pd, uint32_t c_lo, uint32_t c_hi, float *comp) {
     // Every HBM input of the env is issued in one batch at the start (the
     // lead lane's scalars and root-reset template, every lane's history
     // entries), so the kernel waits on memory once; a reset replaces them by
@@ -296,7 +333,7 @@ __global__ __launch_bounds__(64 * PAPER_EPW) void paper_post_kernel(tg_paper_par
             float r[9];
 #pragma unroll
             for (int k = 0; k < 9; ++k) r[k] = draw(rd, 9, k, 0);
-            paper_reset_lead(p, b, e, r, tpl, L);
+            paper_reset_lead<M>(p, b, e, r, tpl, L, comp);
             old6 = 0.0f;
         }
     } else if (lead) {
@@ -476,10 +513,22 @@ int launch_paper_pre(const tg_paper_params &p, const tg_paper_buffers &b, const 
     return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
 }
 int launch_paper_post(const tg_paper_params &p, const tg_paper_buffers &b, const float *rd, const float *nd,
-                      const float *sd, const float *yd, const float *pd, uint64_t counter, hipStream_t s) {
-    hipLaunchKernelGGL(paper_post_kernel, dim3((p.num_envs + PAPER_EPW - 1) / PAPER_EPW), dim3(64 * PAPER_EPW), 0, s,
-                       p, b, rd, nd, sd, yd, pd,
-                       (uint32_t)counter, (uint32_t)(counter >> 32));
+                      const float *sd, const float *yd, const float *pd, uint64_t counter, hipStream_t s,
+                      uint64_t model_hash, float *comp, bool *inplace) {
+    const dim3 grid((p.num_envs + PAPER_EPW - 1) / PAPER_EPW), block(64 * PAPER_EPW);
+    const uint32_t lo = (uint32_t)counter, hi = (uint32_t)(counter >> 32);
+    bool done = false;
+#define TG_PAPER_POST(MODEL)                                                                                  \
+    if constexpr ((MODEL::FUSED & 4) != 0 && MODEL::NTL > 0) {                                              \
+        if (!done && comp && model_hash == MODEL::hash) {                                                    \
+            hipLaunchKernelGGL(paper_post_kernel<MODEL>, grid, block, 0, s, p, b, rd, nd, sd, yd, pd, lo, hi, comp); \
+            done = true;                                                                                     \
+        }                                                                                                    \
+    }
+    TG_FOR_EACH_MODEL(TG_PAPER_POST)
+#undef TG_PAPER_POST
+    if (inplace) *inplace = done;
+    if (!done) hipLaunchKernelGGL(paper_post_kernel<void>, grid, block, 0, s, p, b, rd, nd, sd, yd, pd, lo, hi, nullptr);
     hipLaunchKernelGGL(paper_finish_kernel, dim3((p.num_envs + FIN_WG - 1) / FIN_WG), dim3(FIN_WG), 0, s, p, b);
     return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
 }

@@ -285,10 +285,10 @@ int jit_launch_body_states(uint64_t hash, const float *root, const float *dof, i
 
 int jit_launch_rb_forces(uint64_t hash, const float *root, const float *dof, const float *comp, int n,
                          const float *mass_scale, const float *forces, const float *torques, int space, float *out,
-                         hipStream_t stream) {
+                         const float *props, hipStream_t stream) {
     JitLoaded *L = find(hash);
     if (!L) return TG_ERR_MODEL;
-    void *args[] = {&root, &dof, &comp, &n, &mass_scale, &forces, &torques, &space, &out};
+    void *args[] = {&root, &dof, &comp, &n, &mass_scale, &forces, &torques, &space, &out, &props};
     return launch(L->f[K_RBF], (unsigned)n, 64, 0, stream, args);
 }
 

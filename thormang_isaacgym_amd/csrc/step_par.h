@@ -44,7 +44,7 @@ namespace tg {
 
 #ifdef TG_SECTION_PROF
 // developer build only: per-section cycle counts summed over thread 0 of every block
-__device__ unsigned long long tg_prof_acc[24];   // [16..]: sub-sections (see scripts/section_prof.py)
+static __device__ unsigned long long tg_prof_acc[24];   // [16..]: sub-sections (see scripts/section_prof.py)
 #define TG_PROF_INIT unsigned long long tg_t0 = clock64();
 #define TG_PROF(k)                                                              \
     {                                                                           \

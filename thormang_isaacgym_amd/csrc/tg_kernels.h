@@ -125,7 +125,7 @@ int launch_body_states(uint64_t hash, const float *root, const float *dof, int n
 // per-link forces / torques [N*L,3] -> group wrenches [N,G,6] (rb_force_kernel)
 int launch_rb_forces(uint64_t hash, const float *root, const float *dof, const float *comp, int n,
                      const float *mass_scale, const float *forces, const float *torques, int space, float *out,
-                     hipStream_t stream);
+                     const float *props, hipStream_t stream);
 int model_kc(uint64_t hash);
 int model_tl(uint64_t hash);
 int launch_compose_only(uint64_t hash, const StepArgs &a, hipStream_t stream);   // every dirty env, no step   // translating locks of a compiled model (codegen translating_locks), 0 otherwise
@@ -140,7 +140,7 @@ int jit_launch_step(uint64_t hash, const StepArgs &a, hipStream_t stream, hipEve
 int jit_launch_body_states(uint64_t hash, const float *root, const float *dof, int n, float *out, hipStream_t stream);
 int jit_launch_rb_forces(uint64_t hash, const float *root, const float *dof, const float *comp, int n,
                          const float *mass_scale, const float *forces, const float *torques, int space, float *out,
-                         hipStream_t stream);
+                         const float *props, hipStream_t stream);
 
 int launch_gogoro_pre(const tg_gogoro_params &p, const tg_gogoro_buffers &b, const float *actions,
                       const float *pre_draws, uint64_t counter, hipStream_t stream);
@@ -152,8 +152,11 @@ int launch_gogoro_reset_idx(const tg_gogoro_params &p, const tg_gogoro_buffers &
                             const float *reset_draws, uint64_t counter, hipStream_t stream);
 
 int launch_paper_pre(const tg_paper_params &p, const tg_paper_buffers &b, const float *actions, hipStream_t s);
+// model_hash / comp: the sim's model and composite cache -- a model with
+// in-place seat composites (codegen FUSED bit 4) gets them and *inplace is set
 int launch_paper_post(const tg_paper_params &p, const tg_paper_buffers &b, const float *rd, const float *nd,
-                      const float *sd, const float *yd, const float *pd, uint64_t counter, hipStream_t s);
+                      const float *sd, const float *yd, const float *pd, uint64_t counter, hipStream_t s,
+                      uint64_t model_hash = 0, float *comp = nullptr, bool *inplace = nullptr);
 int launch_paper_reset_idx(const tg_paper_params &p, const tg_paper_buffers &b, const int32_t *ids, int n,
                            const float *rd, uint64_t counter, hipStream_t s);
 int launch_walk_pre(const tg_walk_params &p, const tg_walk_buffers &b, const float *actions, hipStream_t s);

@@ -486,7 +486,7 @@ static int simulate_args(tg_sim *s, const tg::StepArgs &a_in, const tg::WalkPost
             a.rbf_space = s->rbf_space;
             a.rbf_out = s->force;
         } else if (int rc = tg::launch_rb_forces(s->hash, s->root, s->dof, s->comp, (int)s->N, s->mass_scale,
-                                                 s->rbf_f, s->rbf_t, s->rbf_space, s->force, s->stream)) {
+                                                 s->rbf_f, s->rbf_t, s->rbf_space, s->force, s->props, s->stream)) {
             return fail(rc, "rigid-body force launch failed");
         }
         s->rbf_pending = false;
@@ -832,8 +832,7 @@ int tg_paper_pre_physics(tg_sim *s, const tg_paper_params *p, const tg_paper_buf
                          uint64_t counter) {
     (void)counter;
     if (int rc = check_paper(s, p, b)) return rc;
-    s->dirty_possible = true;
-    if (!actions) return fail(TG_ERR_ARG, "paper: null actions");
+    if (!actions) return fail(TG_ERR_ARG, "paper: null actions");   // (targets / history only: nothing to compose)
     if (int rc = tg::launch_paper_pre(*p, *b, actions, s->stream)) return fail(rc, "launch failed");
     return TG_OK;
 }
@@ -861,9 +860,13 @@ int tg_paper_step(tg_sim *s, const tg_paper_params *p, const tg_paper_buffers *b
         }
         if (int rc = simulate_args(s, a)) return rc < 0 ? rc : fail(TG_ERR_STATE, "no step kernel for this model");
     }
-    if (int rc = tg::launch_paper_post(*p, *b, nullptr, nullptr, nullptr, nullptr, nullptr, counter, s->stream))
+    bool inplace = false;
+    if (int rc = tg::launch_paper_post(*p, *b, nullptr, nullptr, nullptr, nullptr, nullptr, counter, s->stream,
+                                       s->hash, s->no_inplace ? nullptr : s->comp, &inplace))
         return fail(rc, "launch failed");
-    s->dirty_possible = true;   // the post kernel's resets rewrite properties and mark envs dirty
+    // the post kernel's resets either update the seat composites in place or
+    // mark their envs for the next compose
+    if (!inplace) s->dirty_possible = true;
     return TG_OK;
 }
 
@@ -871,10 +874,13 @@ int tg_paper_post_physics(tg_sim *s, const tg_paper_params *p, const tg_paper_bu
                           const float *noise_draws, const float *speed_draws, const float *yaw_draws,
                           const float *push_draws, uint64_t counter) {
     if (int rc = check_paper(s, p, b)) return rc;
+    const bool dirty_before = s->dirty_possible;
     s->dirty_possible = true;
+    bool inplace = false;
     if (int rc = tg::launch_paper_post(*p, *b, reset_draws, noise_draws, speed_draws, yaw_draws, push_draws, counter,
-                                       s->stream))
+                                       s->stream, s->hash, s->no_inplace ? nullptr : s->comp, &inplace))
         return fail(rc, "launch failed");
+    if (inplace) s->dirty_possible = dirty_before;
     return TG_OK;
 }
 

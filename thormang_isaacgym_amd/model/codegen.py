@@ -89,10 +89,13 @@ def axis_frame(a) -> np.ndarray:
 #: ThormangWalk -- selected by tree size in articulation.hip; bit 2: the
 #: registered Gogoro task's scooter)
 FUSED_GOGORO_MODELS = ("gogoro",)
+# models whose task (GogoroPaper) moves the seat locks in place at resets
+# (gogoro_paper_task.hip paper_post_kernel<M>): translating locks, link coms kept
+PAPER_MODELS = ("gogoro_v12",)
 
 
 def fused_tasks(m: Model) -> int:
-    return 2 if m.name in FUSED_GOGORO_MODELS else 0
+    return (2 if m.name in FUSED_GOGORO_MODELS else 0) | (4 if m.name in PAPER_MODELS else 0)
 
 
 def translating_locks(m: Model, a: dict) -> dict:
@@ -106,7 +109,7 @@ def translating_locks(m: Model, a: dict) -> dict:
     group.  Returns the tables codegen emits (NTL = 0: none)."""
     none = dict(NTL=0, tl_link=[0], tl_dof=[0], tl_group=0, link_tl=[0] * m.num_bodies,
                 ag=[], ashape=[], KX=0)
-    if not (fused_tasks(m) & 2):
+    if not (fused_tasks(m) & 6):
         return none
     L = m.num_bodies
     lpar = [int(x) for x in a["link_parent"]]
@@ -191,7 +194,10 @@ def emit(m: Model, cname: str) -> str:
     # link coms in their group's frame (3 per link, padded to 16 bytes): the
     # rigid-body force reduction's moment arms without link kinematics.  Not
     # for models whose epilogue moves locks in place (the links would move too)
-    lcom = 0 if tlc["NTL"] else (3 * L + 3) & ~3
+    # link coms for the rigid-body force reduction; the Gogoro epilogue's
+    # in-place seat moves do not maintain them (and its task applies no
+    # per-link forces), the paper's do (rb_force_env shifts them)
+    lcom = 0 if tlc["NTL"] and not fused_tasks(m) & 4 else (3 * L + 3) & ~3
     maxc = max(1, max(len(c) for c in children))
     lines = [
         f"// AUTO-GENERATED by thormang_isaacgym_amd/model/codegen.py from model '{m.name}'. Do not edit.",
@@ -245,7 +251,7 @@ def emit(m: Model, cname: str) -> str:
         f"{_arr([_arr(p) for p in cpaths] or [_arr([0] * maxd)])};",
         f"  static constexpr int shape_cg[{max(S, 1)}] = {_arr(shape_cg or [0])};",
         f"  static constexpr int SL = {SL}, PAIR = {PAIR}, LPE = {LPE}, EPB = {EPB}, NSTEP = {len(sched)}, MAXC = {maxc};",
-        f"  static constexpr int FUSED = {fused_tasks(m)};  // fused task epilogues: 1 walk, 2 Gogoro",
+        f"  static constexpr int FUSED = {fused_tasks(m)};  // fused task epilogues: 1 walk, 2 Gogoro; 4 paper in-place seat",
         f"  static constexpr int sched[{len(sched)}][{SL}] = {_arr([_arr(r) for r in sched])};",
         f"  static constexpr int nchild[{G}] = {_arr([len(c) for c in children])};",
         f"  static constexpr int child[{G}][{maxc}] = {_arr([_arr(c + [-1] * (maxc - len(c))) for c in children])};",
