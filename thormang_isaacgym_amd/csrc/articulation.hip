@@ -167,7 +167,8 @@ int launch_body_states(uint64_t hash, const float *root, const float *dof, int n
 
 #define TG_RB_FORCES(MODEL)                                                                               \
     if (hash == MODEL::hash) {                                                                            \
-        hipLaunchKernelGGL(rb_force_kernel<MODEL>, dim3(n), dim3(64), 0, stream, root, dof, comp, n,        \
+        hipLaunchKernelGGL(rb_force_kernel<MODEL>, dim3((n + COMPOSE_WPB - 1) / COMPOSE_WPB), dim3(64 * COMPOSE_WPB), \
+                           0, stream, root, dof, comp, n,                                                 \
                            mass_scale, forces, torques, space, out, props);                               \
         return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;                                          \
     }
@@ -193,6 +194,11 @@ int compiled_hashes(uint64_t *out, int cap) {
 int launch_compose_only(uint64_t hash, const StepArgs &a, hipStream_t stream) {
     TG_FOR_EACH_MODEL(TG_COMPOSE_ONLY)
     return TG_ERR_MODEL;
+}
+#define TG_FUSED(MODEL) if (hash == MODEL::hash) return MODEL::FUSED;
+int model_fused(uint64_t hash) {
+    TG_FOR_EACH_MODEL(TG_FUSED)
+    return 0;
 }
 #define TG_TL(MODEL) if (hash == MODEL::hash) return MODEL::NTL;
 int model_tl(uint64_t hash) {

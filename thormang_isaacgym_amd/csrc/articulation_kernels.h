@@ -180,6 +180,17 @@ __device__ __forceinline__ void rb_force_env(const float *root, const float *dof
                                              int space, float *out, int lane, float (*T)[12], float (*F)[10],
                                              const float *props, int N);
 
+// a compile-time loop over groups G = B .. E-1: f(GroupC<G>{})
+template <int N> struct GroupC {
+    static constexpr int value = N;
+};
+template <int B, int E, class Fn> __device__ __forceinline__ void rbf_for_groups(Fn &&f) {
+    if constexpr (B < E) {
+        f(GroupC<B>{});
+        rbf_for_groups<B + 1, E>(f);
+    }
+}
+
 // one wavefront's compose scratch
 template <class M> struct ComposeLds {
     float T[M::NL][12];        // link pose in its group-root frame: R (9), p (3)
@@ -489,7 +500,7 @@ template <class M> __global__ __launch_bounds__(64 * COMPOSE_WPB) void compose_k
     if (a.cnext && blockIdx.x == 0 && threadIdx.x == 0) *a.cnext = 0;   // the reset list the next epilogue fills
     if (a.pm_actions && !a.pm_in_step && e < a.N) target_prologue(a, e, threadIdx.x % 64);
     if (a.gp.actions && !a.gp_in_step && e < a.N && threadIdx.x % 64 == 0) gogoro_pre_prologue(a.gp, e, a.D);
-    if (a.pp.actions && e < a.N) paper_pre_prologue(a.pp, e, a.D, threadIdx.x % 64);
+    if (a.pp.actions && !a.pp_in_step && e < a.N) paper_pre_prologue(a.pp, e, a.D, threadIdx.x % 64);
     __shared__ ComposeLds<M> cs[COMPOSE_WPB];
     if (dirty) compose_env<M>(a, e, threadIdx.x % 64, cs[wv]);
     if (a.rbf_forces && e < a.N)   // a pending apply_rigid_body_force_tensors, on the fresh composite
@@ -653,6 +664,119 @@ __device__ __forceinline__ void rb_force_env(const float *root, const float *dof
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
     wsync();   // the scratch may have been in use by this wave
+    if constexpr (M::LCOM && M::NL <= 64 && M::NG <= 64) {
+        if (comp && space == 0) {
+            // world forces, one link and one group per lane: every input of the
+            // env is issued in one batch -- the lane's link force / torque, its
+            // com and its group's com (composite cache), the lane's group
+            // placement and joint position, the root orientation, the lock
+            // windows -- so the wave waits on memory once; then the arms
+            // arm_l = W_g (c_l - c_g) from the group orientations W_g (group
+            // kinematics through LDS, a few levels) and the group sums
+            using CL = CompLayout<M>;
+            const float *c = comp + (size_t)e * M::KC;
+            const bool hl = lane < M::NL;
+            const int l = hl ? lane : 0;
+            const int gl = M::link_group[l];
+            const size_t i = (size_t)e * M::NL + l;
+            V3 f = v3(0, 0, 0), t = v3(0, 0, 0), lc = v3(0, 0, 0), gc = v3(0, 0, 0);
+            if (hl) {
+                f = v3(forces[3 * i], forces[3 * i + 1], forces[3 * i + 2]);
+                if (torques) t = v3(torques[3 * i], torques[3 * i + 1], torques[3 * i + 2]);
+                lc = v3(c[CL::lcom(l)], c[CL::lcom(l) + 1], c[CL::lcom(l) + 2]);
+                gc = v3(c[CL::inertia(gl) + 1], c[CL::inertia(gl) + 2], c[CL::inertia(gl) + 3]);
+            }
+            const bool hg = lane > 0 && lane < M::NG;
+            const int g = hg ? lane : 1 % M::NG;
+            M3 Rpc;
+            float qj = 0.f;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) Rpc.a[k] = hg ? c[CL::xtree(g) + k] : 0.f;
+            if (hg && M::jtype[g] == TG_JOINT_REVOLUTE) qj = q[2 * M::gdof[g]];
+            const float qx = r[3], qy = r[4], qz = r[5], qw = r[6];
+            V3 ush[M::NTL > 0 ? M::NTL : 1];
+            if constexpr (M::NTL > 0) {   // lock displacements since the compose (tl_update, above)
+                const size_t ND = (size_t)N * M::ND;
+#pragma unroll
+                for (int k = 0; k < M::NTL; ++k) {
+                    const size_t id = (size_t)e * M::ND + M::tl_dof[k];
+                    const float qc = 0.5f * (props[TG_PROP_LOWER * ND + id] + props[TG_PROP_UPPER * ND + id]);
+                    const float *xk = c + CL::xk(k);
+                    ush[k] = (qc - xk[0]) * v3(xk[5], xk[6], xk[7]);
+                }
+            }
+            const bool act = f.x != 0.f || f.y != 0.f || f.z != 0.f || t.x != 0.f || t.y != 0.f || t.z != 0.f;
+            if (!__any(act)) {   // no force and no torque on any link: zero wrenches
+                for (int k = lane; k < 6 * M::NG; k += 64) out[(size_t)e * 6 * M::NG + k] = 0.f;
+                return;
+            }
+            if (hg && M::jtype[g] == TG_JOINT_REVOLUTE) {   // Rpc Rz(q), as step pass 1a
+                float sq, cq;
+                __sincosf(qj, &sq, &cq);
+#pragma unroll
+                for (int rr = 0; rr < 3; ++rr) {
+                    const float c0 = Rpc.a[3 * rr], c1 = Rpc.a[3 * rr + 1];
+                    Rpc.a[3 * rr] = c0 * cq + c1 * sq;
+                    Rpc.a[3 * rr + 1] = c1 * cq - c0 * sq;
+                }
+            }
+            constexpr int GD = max_group_depth<M>();
+            for (int lev = 0; lev <= GD; ++lev) {
+                if (lev == 0 && lane == 0) {
+                    const float in = rsqrtf(qx * qx + qy * qy + qz * qz + qw * qw);
+                    const M3 W = mul(quat_to_m3(qx * in, qy * in, qz * in, qw * in),
+                                     M3{{M::gq[0][0], M::gq[0][1], M::gq[0][2], M::gq[0][3], M::gq[0][4],
+                                         M::gq[0][5], M::gq[0][6], M::gq[0][7], M::gq[0][8]}});
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) T[0][k] = W.a[k];
+                } else if (lev > 0 && hg && group_depth<M>(g) == lev) {
+                    M3 Wp;
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) Wp.a[k] = T[M::parent[g]][k];
+                    const M3 W = mul(Wp, Rpc);
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) T[g][k] = W.a[k];
+                }
+                wsync();
+            }
+            if (hl) {
+                M3 W;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) W.a[k] = T[gl][k];
+                if constexpr (M::NTL > 0) {
+                    if (gl == M::tl_group && M::link_tl[l]) {
+                        V3 sh = v3(0, 0, 0);
+#pragma unroll
+                        for (int k = 0; k < M::NTL; ++k)
+                            if ((M::link_tl[l] >> k) & 1) sh = sh + ush[k];
+                        const float *qg = M::gq[gl];
+                        lc = lc + mulT(M3{{qg[0], qg[1], qg[2], qg[3], qg[4], qg[5], qg[6], qg[7], qg[8]}}, sh);
+                    }
+                }
+                const V3 tq = t + cross(mul(W, lc - gc), f);
+                F[l][0] = f.x; F[l][1] = f.y; F[l][2] = f.z;
+                F[l][3] = tq.x; F[l][4] = tq.y; F[l][5] = tq.z;
+            }
+            wsync();
+            // group sums in link order, one lane per (group, component): the
+            // group loop is unrolled at compile time so every link index is an
+            // immediate LDS offset (a lane-indexed walk of the group-link table
+            // would wait on a table load per link)
+            for (int j = lane; j < 6 * M::NG; j += 64) {
+                float acc = 0.f;
+                const int gsel = j / 6, cmp = j % 6;
+                rbf_for_groups<0, M::NG>([&](auto G) {
+                    constexpr int gg = decltype(G)::value;
+                    if (gsel == gg) {
+#pragma unroll
+                        for (int k = 0; k < M::group_nlinks[gg]; ++k) acc += F[M::group_links[gg][k]][cmp];
+                    }
+                });
+                out[(size_t)e * 6 * M::NG + j] = acc;
+            }
+            return;
+        }
+    }
     // an env with no force and no torque on any link gets zero wrenches without
     // the link kinematics (the paper task pushes only its first 2048 envs)
     bool any = false;
@@ -837,16 +961,20 @@ __device__ __forceinline__ void rb_force_env(const float *root, const float *dof
     }
 }
 
-template <class M> __global__ __launch_bounds__(64) void rb_force_kernel(const float *root, const float *dof,
+template <class M> __global__ __launch_bounds__(64 * COMPOSE_WPB) void rb_force_kernel(const float *root, const float *dof,
                                                                          const float *comp, int n,
                                                                          const float *mass_scale, const float *forces,
                                                                          const float *torques, int space, float *out,
                                                                          const float *props) {
-    const int e = blockIdx.x;
+    // COMPOSE_WPB envs per workgroup, one wavefront each (N single-wave
+    // workgroups would be dispatch-bound)
+    const int wv = threadIdx.x / 64;
+    const int e = blockIdx.x * COMPOSE_WPB + wv;
     if (e >= n) return;
-    __shared__ float T[M::NL][12];   // link pose: R (9), p (3)
-    __shared__ float F[M::NL][10];   // link com (3), mass, force (3), torque (3)
-    rb_force_env<M>(root, dof, comp, e, mass_scale, forces, torques, space, out, threadIdx.x, T, F, props, n);
+    __shared__ float T[COMPOSE_WPB][M::NL][12];   // link pose: R (9), p (3)
+    __shared__ float F[COMPOSE_WPB][M::NL][10];   // link com (3), mass, force (3), torque (3)
+    rb_force_env<M>(root, dof, comp, e, mass_scale, forces, torques, space, out, threadIdx.x % 64, T[wv], F[wv],
+                    props, n);
 }
 
 // ---------------------------------------------------------------- contact row layout

@@ -289,7 +289,8 @@ int jit_launch_rb_forces(uint64_t hash, const float *root, const float *dof, con
     JitLoaded *L = find(hash);
     if (!L) return TG_ERR_MODEL;
     void *args[] = {&root, &dof, &comp, &n, &mass_scale, &forces, &torques, &space, &out, &props};
-    return launch(L->f[K_RBF], (unsigned)n, 64, 0, stream, args);
+    return launch(L->f[K_RBF], (unsigned)((n + JIT_COMPOSE_WPB - 1) / JIT_COMPOSE_WPB), 64 * JIT_COMPOSE_WPB, 0, stream,
+                  args);
 }
 
 }  // namespace tg

@@ -134,7 +134,7 @@ template <class M> struct ParLayout {
     // rear-wheel velocity target -- in the root group's U / clamp slots, which
     // the root never uses (its articulated inertia is solved by the LDL), so
     // the env stride and with it the LDS bank pattern stay as they were
-    static constexpr bool TPON = (M::FUSED & 2) != 0;
+    static constexpr bool TPON = (M::FUSED & 6) != 0;
     static constexpr int TP = F_U;
     static_assert(F_U + 8 <= GF, "pre-physics values in the root group's slots");
     // per-block ints after the env area
@@ -432,6 +432,32 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
             s(PL::TP + 7) = vr;
             if (owner) gogoro_pre_store(a.gp, e, a.D, ah, cmd, ts, vr);
         }
+        if (a.pp_in_step && lead) {   // the GogoroPaper pre-physics (tg_paper_step), as paper_pre_prologue
+            const PaperPre &pp = a.pp;
+            constexpr int PC = TG_PAPER_CMD_HIST;
+            float *hh = pp.command_history + PC * (size_t)e;
+            const float act = pp.actions[e];
+            const float ac = act < -1.0f ? -1.0f : (act > 1.0f ? 1.0f : act);
+            const float cmd = ac * pp.max_steering;
+            float hv[PC];
+#pragma unroll
+            for (int k = 0; k < PC - 1; ++k) hv[k] = hh[k + 1];
+            hv[PC - 1] = cmd;
+            const int64_t delay = pp.use_steer_delay ? pp.steer_delay[e] : 0;
+            const float speed = pp.curent_speed[e];
+            int idx = PC - 3;
+            if (pp.use_steer_delay) idx = delay == 0 ? 0 : (int)(PC - delay);   // command_history[:, -steer_delay]
+            float steer = 0.f;
+#pragma unroll
+            for (int k = 0; k < PC; ++k) steer = k == idx ? hv[k] : steer;
+            s(PL::TP + 6) = steer;
+            s(PL::TP + 7) = speed;
+            if (owner) {
+#pragma unroll
+                for (int k = 0; k < PC; ++k) hh[k] = hv[k];
+                pp.curent_command[e] = cmd;
+            }
+        }
     }
     // the walk pre-physics (tg_walk_step): the env's clamped actions and drive
     // targets written once, lane = dof mod LPE; pass 2a reads the targets back
@@ -447,6 +473,15 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
     float *root = a.root + (size_t)e * 13;
     float *dofs = a.dof + (size_t)e * D * 2;
     __syncthreads();   // group tables (shared by both wavefronts)
+    if constexpr (PL::TPON) {
+        if (a.pp_in_step && owner) {   // the paper's drive target rows: steering and rear wheel, 0 elsewhere
+            float *pt = a.pp.pos_target + (size_t)D * e, *vt = a.pp.vel_target + (size_t)D * e;
+            for (int d = sub; d < D; d += LPE) {
+                pt[d] = d == a.pp.dof_steer ? s(PL::TP + 6) : 0.0f;
+                vt[d] = d == a.pp.dof_rear ? s(PL::TP + 7) : 0.0f;
+            }
+        }
+    }
     for (int g = 1 + sub; g < M::NG; g += LPE) {
         const int d = bounded(gi[g * GIW + GI_DOF], 0, 1 << 16);
         s(g * GF + F_Q) = dofs[2 * d];
@@ -537,6 +572,9 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
             if (a.gp_in_step) {
                 if (d == a.gp.dof_steer) x[7] = s(PL::TP + 6);
                 if (d == a.gp.dof_rear) x[8] = s(PL::TP + 7);
+            } else if (a.pp_in_step) {   // the paper zeroes every other target
+                x[7] = d == a.pp.dof_steer ? s(PL::TP + 6) : 0.f;
+                x[8] = d == a.pp.dof_rear ? s(PL::TP + 7) : 0.f;
             }
         }
         x[9] = a.act ? at_u32<float>(a.act, ed * 4u) : 0.f;

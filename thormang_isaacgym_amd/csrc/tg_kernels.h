@@ -85,6 +85,9 @@ struct StepArgs {
     // gp_in_step: the Gogoro pre-physics (gp) runs at the start of the step
     // kernel (lead lane; values through the env's LDS) instead of in compose
     int gp_in_step;
+    // pp_in_step: the GogoroPaper pre-physics (pp) likewise (models with the
+    // pre-physics slots, codegen FUSED bits 2 | 4)
+    int pp_in_step;
     // a pending apply_rigid_body_force_tensors reduced by the (full) compose
     // launch of this simulate (rbf_forces null: none)
     const float *rbf_forces, *rbf_torques;
@@ -128,6 +131,7 @@ int launch_rb_forces(uint64_t hash, const float *root, const float *dof, const f
                      const float *props, hipStream_t stream);
 int model_kc(uint64_t hash);
 int model_tl(uint64_t hash);
+int model_fused(uint64_t hash);   // codegen FUSED bits of a compiled model (0: none / not compiled in)
 int launch_compose_only(uint64_t hash, const StepArgs &a, hipStream_t stream);   // every dirty env, no step   // translating locks of a compiled model (codegen translating_locks), 0 otherwise
 
 // run-time compiled models (jit.cpp, tg_model_jit): the launchers above fall

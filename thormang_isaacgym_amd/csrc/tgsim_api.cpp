@@ -468,7 +468,7 @@ static int simulate_args(tg_sim *s, const tg::StepArgs &a_in, const tg::WalkPost
     const bool gogoro_prologue = a.gp.actions && !a.gp_in_step;
     // (a pending per-link force tensor with listed envs: the full compose, which
     // reduces it after composing them)
-    const bool paper_prologue = a.pp.actions != nullptr;   // (one wavefront per env: the full compose launch)
+    const bool paper_prologue = a.pp.actions && !a.pp_in_step;   // (one wavefront per env: the full compose launch)
     const bool full = s->dirty_possible || s->always_compose || walk_prologue || paper_prologue ||
                       (s->rbf_pending && s->list_pending);
     a.skip_compose = !full && !s->list_pending && !gogoro_prologue;
@@ -857,6 +857,10 @@ int tg_paper_step(tg_sim *s, const tg_paper_params *p, const tg_paper_buffers *b
             q.use_steer_delay = p->use_steer_delay;
             q.dof_steer = p->dof_steer;
             q.dof_rear = p->dof_rear;
+            // in the step kernel itself when it is the only simulate and the
+            // model's kernel has the pre-physics slots; else the compose prologue
+            q.actions = actions;
+            a.pp_in_step = (n_simulate == 1 && (tg::model_fused(s->hash) & 6) && !s->pre_in_compose) ? 1 : 0;
         }
         if (int rc = simulate_args(s, a)) return rc < 0 ? rc : fail(TG_ERR_STATE, "no step kernel for this model");
     }
