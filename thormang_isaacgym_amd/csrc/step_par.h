@@ -422,7 +422,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
     // the Gogoro pre-physics (tg_gogoro_step) on the env's lead lane, first of
     // all so its input latency overlaps the state loads
     if constexpr (PL::TPON) {
-        if (a.gp_in_step && lead) {   // the Gogoro pre-physics (tg_gogoro_step) on the env's lead lane
+        if ((M::FUSED & 2) && a.gp_in_step && lead) {   // the Gogoro pre-physics (tg_gogoro_step) on the env's lead lane
             float ah[5], cmd, ts, vr;
             gogoro_pre_values(a.gp, e, ah, cmd, ts, vr);
 #pragma unroll
@@ -432,7 +432,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
             s(PL::TP + 7) = vr;
             if (owner) gogoro_pre_store(a.gp, e, a.D, ah, cmd, ts, vr);
         }
-        if (a.pp_in_step && lead) {   // the GogoroPaper pre-physics (tg_paper_step), as paper_pre_prologue
+        if ((M::FUSED & 4) && a.pp_in_step && lead) {   // the GogoroPaper pre-physics (tg_paper_step), as paper_pre_prologue
             const PaperPre &pp = a.pp;
             constexpr int PC = TG_PAPER_CMD_HIST;
             float *hh = pp.command_history + PC * (size_t)e;
@@ -474,7 +474,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
     float *dofs = a.dof + (size_t)e * D * 2;
     __syncthreads();   // group tables (shared by both wavefronts)
     if constexpr (PL::TPON) {
-        if (a.pp_in_step && owner) {   // the paper's drive target rows: steering and rear wheel, 0 elsewhere
+        if ((M::FUSED & 4) && a.pp_in_step && owner) {   // the paper's drive target rows: steering and rear wheel, 0 elsewhere
             float *pt = a.pp.pos_target + (size_t)D * e, *vt = a.pp.vel_target + (size_t)D * e;
             for (int d = sub; d < D; d += LPE) {
                 pt[d] = d == a.pp.dof_steer ? s(PL::TP + 6) : 0.0f;
@@ -569,10 +569,10 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         x[7] = at_u32<float>(a.pm_in_step ? a.pm_tgt_out : a.pos_tgt, ed * 4u);
         x[8] = at_u32<float>(a.vel_tgt, ed * 4u);
         if constexpr (PL::TPON) {   // the Gogoro pre-physics inside the step (tg_gogoro_step)
-            if (a.gp_in_step) {
+            if ((M::FUSED & 2) && a.gp_in_step) {
                 if (d == a.gp.dof_steer) x[7] = s(PL::TP + 6);
                 if (d == a.gp.dof_rear) x[8] = s(PL::TP + 7);
-            } else if (a.pp_in_step) {   // the paper zeroes every other target
+            } else if ((M::FUSED & 4) && a.pp_in_step) {   // the paper zeroes every other target
                 x[7] = d == a.pp.dof_steer ? s(PL::TP + 6) : 0.f;
                 x[8] = d == a.pp.dof_rear ? s(PL::TP + 7) : 0.f;
             }
@@ -1080,20 +1080,47 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         if constexpr (M::NS > 0) {
             // contact-group world poses and free velocities (one lane per contact group)
             for (int c = sub; c < M::NCG; c += LPE) {
-                const int cg = M::cgroup[c];
+                // the group and its path (groups, joint types) selected from the
+                // model's constant tables (no table load before the LDS reads),
+                // every path term's LDS reads issued at once
+                int cg = M::cgroup[0], lk = M::cpath_len[0], pk[M::MAXD], pj[M::MAXD];
+#pragma unroll
+                for (int i = 0; i < M::MAXD; ++i) {
+                    pk[i] = M::cpath[0][i] > 0 ? M::cpath[0][i] : 0;
+                    pj[i] = M::jtype[pk[i]];
+                }
+#pragma unroll
+                for (int cc = 1; cc < M::NCG; ++cc) {
+                    const bool on = c == cc;
+                    cg = on ? M::cgroup[cc] : cg;
+                    lk = on ? M::cpath_len[cc] : lk;
+#pragma unroll
+                    for (int i = 0; i < M::MAXD; ++i) {
+                        const int gk = M::cpath[cc][i] > 0 ? M::cpath[cc][i] : 0;
+                        pk[i] = on ? gk : pk[i];
+                        pj[i] = on ? M::jtype[gk] : pj[i];
+                    }
+                }
                 stm3(s, PL::CGP + 12 * c, mul(R, ldR(s, cg)));
                 stv3(s, PL::CGP + 12 * c + 9, pos + mul(R, ldv3(s, cg * GF + F_P)));
                 SV v = v0s;   // root frame: the root velocity plus the path's joint terms
-                for (int i = 0; i < M::cpath_len[c]; ++i) {
-                    const int hg = bounded(cpath[c * M::MAXD + i], -1, M::NG);
-                    v = v + s(hg * GF + F_QDS) * ldS(s, hg, ginfo<M>(gi, hg).jt);
+                float qv[M::MAXD];
+                SV sv[M::MAXD];
+#pragma unroll
+                for (int i = 0; i < M::MAXD; ++i) {
+                    qv[i] = i < lk ? s(pk[i] * GF + F_QDS) : 0.f;
+                    sv[i] = ldS(s, pk[i], pj[i]);
                 }
+#pragma unroll
+                for (int i = 0; i < M::MAXD; ++i) v = v + qv[i] * sv[i];
                 stsv(s, PL::CGV + 6 * c, v);
             }
             TG_SYNC();
             // contact rows (one lane per shape)
             for (int sh = sub; sh < M::NS; sh += LPE) {
-                const int cgi = M::shape_cg[sh];
+                int cgi = M::shape_cg[0];   // (selected from the constant table, no load)
+#pragma unroll
+                for (int k = 1; k < M::NS; ++k) cgi = sh == k ? M::shape_cg[k] : cgi;
                 const int rb = row_base<M>(sh);
                 const M3 Rwg = ldm3(s, PL::CGP + 12 * cgi);
                 const V3 pwg = ldv3(s, PL::CGP + 12 * cgi + 9);
