@@ -987,6 +987,17 @@ template <class M> __device__ __forceinline__ constexpr int row_shape(int i) {
     }
     return 0;
 }
+// the contact group of row i (lane-dependent i): compares and selects against
+// the model's row ranges, no table load
+template <class M> __device__ __forceinline__ int row_cg(int i) {
+    int r = M::shape_cg[0], base = 0;
+#pragma unroll
+    for (int sh = 0; sh < M::NS; ++sh) {
+        r = i >= base ? M::shape_cg[sh] : r;
+        base += M::shape_nrows[sh] + 3;
+    }
+    return r;
+}
 template <class M> __device__ __forceinline__ constexpr int row_base(int s) {
     int base = 0;
     for (int k = 0; k < s; ++k) base += M::shape_nrows[k] + 3;

@@ -1232,7 +1232,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
             auto rvel = [&](int i, const SV &vg) { return dot(ldsv(s, PL::ROW + i * 8), vg); };
             auto rforce = [&](int i, float lam) { return lam * ldsv(s, PL::ROW + i * 8); };
             for (int i = sub; i < K; i += LPE) {
-                s(PL::VFREE + i) = rvel(i, ldsv(s, PL::CGV + 6 * M::shape_cg[row_shape<M>(i)]));
+                s(PL::VFREE + i) = rvel(i, ldsv(s, PL::CGV + 6 * row_cg<M>(i)));
                 s(PL::LAM + i) = 0.f;
             }
             TG_PROF(4)
@@ -1241,7 +1241,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
             // along every contact group's path
 #pragma unroll 1
             for (int j = sub; j < K; j += LPE) {
-                const int ck = M::shape_cg[row_shape<M>(j)];
+                const int ck = row_cg<M>(j);
                 // the path of contact group ck (groups, joint types) selected from
                 // the model's constant tables: no LDS round trip before the walk
                 int lk = M::cpath_len[0], pk[M::MAXD], pj[M::MAXD];
