@@ -1053,7 +1053,7 @@ struct WalkPost {
             if (d < D) {
                 dpos[r] = p.default_pos[d];
                 kst[r] = p.stiffness[d];
-                const int g = DofGroup<M>::tab.g[d];
+                const int g = dof_group<M>(d);
                 if (g > 0) {
                     q[r] = s(g * GF + F_Q);
                     qd[r] = s(g * GF + F_QD);
@@ -1508,7 +1508,7 @@ struct GogoroPost {
             for (int rr = 0; rr < NR; ++rr) {
                 const int d = sub + LPE * rr;
                 if (d < D) {
-                    const int g = DofGroup<M>::tab.g[d];
+                    const int g = dof_group<M>(d);
                     if (g > 0) {
                         dofs[2 * d] = s(g * GF + F_Q);
                         dofs[2 * d + 1] = s(g * GF + F_QD);

@@ -336,6 +336,20 @@ template <class M> struct DofGroup {
     }
     static constexpr Arr tab = make();
 };
+// group of dof d (lane-dependent d): d + OFF when the model numbers its
+// groups that way (an add, no table load), else the table
+template <class M> constexpr int dof_group_offset() {
+    constexpr auto t = DofGroup<M>::make();
+    const int off = M::ND > 0 ? t.g[0] - 0 : 0;
+    for (int d = 0; d < M::ND; ++d)
+        if (t.g[d] != d + off) return -1000;
+    return off;
+}
+template <class M> __device__ __forceinline__ int dof_group(int d) {
+    constexpr int off = dof_group_offset<M>();
+    if constexpr (off != -1000) return d + off;
+    else return DofGroup<M>::tab.g[d];
+}
 
 template <class M, int EPB, bool HF, class P = NoPost>
 __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, typename P::Args pa) {
