@@ -336,6 +336,25 @@ template <class M> struct DofGroup {
     }
     static constexpr Arr tab = make();
 };
+// dof of group g in [1, NG) (lane-dependent g): g + OFF when the model
+// numbers them that way, else a select chain over the model's table
+template <class M> constexpr int group_dof_offset() {
+    const int off = M::NG > 1 ? M::gdof[1] - 1 : 0;
+    for (int g = 1; g < M::NG; ++g)
+        if (M::gdof[g] != g + off) return -1000;
+    return off;
+}
+template <class M> __device__ __forceinline__ int group_dof(int g) {
+    constexpr int off = group_dof_offset<M>();
+    if constexpr (off != -1000) {
+        return g + off;
+    } else {
+        int d = M::gdof[M::NG > 1 ? 1 : 0];
+#pragma unroll
+        for (int k = 2; k < M::NG; ++k) d = g == k ? M::gdof[k] : d;
+        return d;
+    }
+}
 // group of dof d (lane-dependent d): d + OFF when the model numbers its
 // groups that way (an add, no table load), else the table
 template <class M> constexpr int dof_group_offset() {
@@ -486,7 +505,28 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
     }
     float *root = a.root + (size_t)e * 13;
     float *dofs = a.dof + (size_t)e * D * 2;
+    // one-round trees: the env's state issued before the barrier (group ->
+    // dof from the model's constants, not the LDS table) so its latency
+    // overlaps the table fill's (larger trees: measured no gain, more live
+    // registers across the barrier)
+    constexpr int NGR = (M::NG - 1 + LPE - 1) / LPE;
+    constexpr bool EARLY = NGR == 1;
+    float q0 = 0.f, qd0 = 0.f, rt0[13];
+    if constexpr (EARLY) {
+        const int g = 1 + sub;
+        if (g < M::NG) {
+            const int d = group_dof<M>(g);
+            q0 = dofs[2 * d];
+            qd0 = dofs[2 * d + 1];
+        }
+#pragma unroll
+        for (int k = 0; k < 13; ++k) rt0[k] = root[k];
+    }
     __syncthreads();   // group tables (shared by both wavefronts)
+    if constexpr (!EARLY) {
+#pragma unroll
+        for (int k = 0; k < 13; ++k) rt0[k] = root[k];
+    }
     if constexpr (PL::TPON) {
         if ((M::FUSED & 4) && a.pp_in_step && owner) {   // the paper's drive target rows: steering and rear wheel, 0 elsewhere
             float *pt = a.pp.pos_target + (size_t)D * e, *vt = a.pp.vel_target + (size_t)D * e;
@@ -496,25 +536,32 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
             }
         }
     }
-    for (int g = 1 + sub; g < M::NG; g += LPE) {
-        const int d = bounded(gi[g * GIW + GI_DOF], 0, 1 << 16);
-        s(g * GF + F_Q) = dofs[2 * d];
-        s(g * GF + F_QD) = dofs[2 * d + 1];
+    if constexpr (EARLY) {
+        if (1 + sub < M::NG) {
+            s((1 + sub) * GF + F_Q) = q0;
+            s((1 + sub) * GF + F_QD) = qd0;
+        }
+    } else {
+        for (int g = 1 + sub; g < M::NG; g += LPE) {
+            const int d = bounded(gi[g * GIW + GI_DOF], 0, 1 << 16);
+            s(g * GF + F_Q) = dofs[2 * d];
+            s(g * GF + F_QD) = dofs[2 * d + 1];
+        }
     }
     if (sub == 0) {   // the root group's pose in its own frame (never rewritten)
         stR(s, 0, eye3());
         stv3(s, F_P, v3(0, 0, 0));
     }
-    V3 pos = v3(root[0], root[1], root[2]);
-    float qx = root[3], qy = root[4], qz = root[5], qw = root[6];
+    V3 pos = v3(rt0[0], rt0[1], rt0[2]);
+    float qx = rt0[3], qy = rt0[4], qz = rt0[5], qw = rt0[6];
     {
         const float in = rsqrtf(qx * qx + qy * qy + qz * qz + qw * qw);
         qx *= in; qy *= in; qz *= in; qw *= in;
     }
     M3 R = quat_to_m3(qx, qy, qz, qw);
     const V3 c0 = v3(M::root_com[0], M::root_com[1], M::root_com[2]);
-    const V3 ww = v3(root[10], root[11], root[12]);
-    const V3 vo = v3(root[7], root[8], root[9]) - cross(ww, mul(R, c0));
+    const V3 ww = v3(rt0[10], rt0[11], rt0[12]);
+    const V3 vo = v3(rt0[7], rt0[8], rt0[9]) - cross(ww, mul(R, c0));
     SV v0 = fix_base ? sv0() : SV{mulT(R, ww), mulT(R, vo)};
     const V3 grav = v3(a.gx, a.gy, a.gz);
 
