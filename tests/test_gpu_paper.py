@@ -127,6 +127,18 @@ def test_gpu_paper_env_matches_oracle_fixed_base():
     assert err["reset_equal"] and err["timeout_equal"], err
 
 
+def test_gpu_paper_fixed_base_free_running_1000_steps():
+    """north_star's horizon free-running on the paper variant's committed
+    configuration (fixed base): 1000 steps with an episode reset every 60,
+    pushes, command resamples every 25 and the 2-step steering delay."""
+    _cuda()
+    err = _env_vs_oracle({}, steps=1000)
+    print(err)
+    assert err["resets"] >= 64 * 16, err     # every env re-spawned along the way
+    assert err["obs"] < 1e-3 and err["rew"] < 1e-3, err
+    assert err["reset_equal"] and err["timeout_equal"], err
+
+
 FLIPPED = dict(DEBUGFIXBASE=False, USE_STEER_DELAY=True, RANDOM_DAMPING=True, CENTER_ROBOT=False)
 
 
