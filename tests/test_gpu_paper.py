@@ -176,9 +176,11 @@ def test_gpu_paper_2048_envs_run():
 
 
 def test_gpu_paper_fused_step_equals_separate_calls(monkeypatch):
-    """tg_paper_step (the pre-physics as the first compose launch's prologue)
-    against the three separate calls (TG_PAPER_UNFUSED=1): the same kernels on
-    the same values, so every buffer agrees bit for bit."""
+    """tg_paper_step (the pre-physics inside the step kernel, which also forms
+    reward term 7's per-env partials, and a post launch that sums the batch
+    itself) against the three separate calls (TG_PAPER_UNFUSED=1: post kernel
+    partials, finish launch): the same operations in the same order, so every
+    buffer agrees bit for bit."""
     _cuda()
     import thormang_isaacgym_amd as tia
     out = []

@@ -174,6 +174,52 @@ __device__ __forceinline__ void paper_pre_prologue(const PaperPre &pp, int e, in
     if (lane == 0) pp.curent_command[e] = cmd;
 }
 
+// Reward term 7's per-env partial sum_t (a[t+1] - a[t])^2, a = command / 0.5,
+// over the clean history's command column as the post-physics will leave it
+// (the 19 newest entries shifted down, the step's command appended; zero for
+// an env that resets) -- the values paper_post_kernel would form, added in its
+// 64-lane xor-butterfly order with no reassociation or contraction (this unit
+// is compiled -ffast-math), so the post launch can finish the batch mean
+// itself bit for bit (gogoro_realistic_turning_sim_paper.py:740).
+__device__ __forceinline__ float paper_t7_partial(const PaperPre &pp, int e, float cmd) {
+    constexpr int PH = TG_PAPER_HIST, PO = TG_PAPER_OBS;
+    static_assert(PH - 1 <= 32, "partials on the butterfly's lower 32 lanes");
+    const float *bo = pp.buffer_obs + (size_t)PH * PO * e;
+    const bool rs = pp.reset_buf[e] != 0;
+    float ch[PH];
+#pragma unroll
+    for (int t = 0; t < PH - 1; ++t) ch[t] = bo[(t + 1) * PO + 6];
+    ch[PH - 1] = cmd;
+    float v[32];
+    {
+#pragma clang fp reassociate(off) contract(off)
+#pragma unroll
+        for (int l = 0; l < 32; ++l) {
+            if (l < PH - 1) {
+                const float dd = ch[l + 1] / 0.5f - ch[l] / 0.5f;
+                v[l] = dd * dd;
+            } else {
+                v[l] = 0.0f;
+            }
+        }
+#pragma unroll
+        for (int m = 16; m >= 1; m >>= 1)
+#pragma unroll
+            for (int l = 0; l < m; ++l) v[l] = v[l] + v[l + m];
+    }
+    return rs ? 0.0f : v[0];
+}
+// the block's sum of the partials (TG_PAPER_T7_BLK of them, env order, double)
+__device__ __forceinline__ void paper_t7_block(const PaperPre &pp, const float *part, int blk) {
+    double s = 0.0;
+    {
+#pragma clang fp reassociate(off) contract(off)
+#pragma unroll
+        for (int i = 0; i < TG_PAPER_T7_BLK; ++i) s = s + (double)part[i];
+    }
+    pp.t7[blk] = s;
+}
+
 template <class M>
 __device__ __forceinline__ void rb_force_env(const float *root, const float *dof, const float *comp, int e,
                                              const float *mass_scale, const float *forces, const float *torques,

@@ -261,10 +261,56 @@ __device__ __forceinline__ void paper_observe(const float *root, float desired_y
 
 // M (comp non-null): the sim's model with in-place seat composites (codegen
 // FUSED bit 4), void: resets mark their envs for a compose
+// the batch sum of reward term 7 in the canonical order (TG_PAPER_T7_*; a
+// block's sum from blk(c)), by threads 0 .. TG_PAPER_T7_THREADS - 1 of the
+// workgroup; every thread of the workgroup calls it (one barrier)
+constexpr int FIN_WG = 1024, T7T = TG_PAPER_T7_THREADS;
+template <class BLK> __device__ __forceinline__ double t7_batch_sum(int nblk, BLK blk) {
+    __shared__ double wsum[T7T / 64];
+    const int t = threadIdx.x;
+    if (t < T7T) {
+        double s = 0.0;
+        for (int c = t; c < nblk; c += T7T) s += blk(c);
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+        if ((t & 63) == 0) wsum[t >> 6] = s;
+    }
+    __syncthreads();
+    double tot = 0.0;
+#pragma unroll
+    for (int w = 0; w < T7T / 64; ++w) tot += wsum[w];
+    return tot;
+}
+// rewards, resets, time_outs of env e from its reward terms 1-5 and the batch sum
+__device__ __forceinline__ void fin_env(const tg_paper_params &p, const tg_paper_buffers &b, int e, double tot,
+                                        float tilt, int64_t prog, float rew) {
+    const float r7 = 1.0f - (float)(tot / ((double)p.num_envs * (PH - 1)));
+    const bool finished = prog >= p.max_episode_length - 1;
+    const bool felt = fabsf(tilt) >= p.max_tilt;
+    float r = rew + r7 * 0.2f;
+    r = r < 0.0f ? 0.0f : r;
+    b.rew_buf[e] = felt ? -1.0f : r;
+    const bool rs = finished || felt;
+    b.reset_buf[e] = rs ? 1 : 0;
+    b.timeout_buf[e] = finished && rs;
+}
+
+// fin: the step kernel formed the term-7 block sums already (PaperPre.t7, in
+// b.scratch, tg_paper_step), so each workgroup sums the batch first, in the
+// canonical order, and its envs end with their final rewards / resets: no
+// finish launch (the host asks for it only when N is a multiple of
+// PAPER_EPW: no thread returns before the barrier)
 template <class M>
 __global__ __launch_bounds__(64 * PAPER_EPW) void paper_post_kernel(tg_paper_params p, tg_paper_buffers b, const float *rd,
                                                         const float *nd, const float *sd, const float *yd,
-                                                        const float *pd, uint32_t c_lo, uint32_t c_hi, float *comp) {
+                                                        const float *pd, uint32_t c_lo, uint32_t c_hi, float *comp,
+                                                        int fin) {
+    static_assert(64 * PAPER_EPW >= T7T, "the canonical sum's threads");
+    double tot = 0.0;
+    if (fin) {
+        const double *bs = reinterpret_cast<const double *>(b.scratch);
+        tot = t7_batch_sum((p.num_envs + TG_PAPER_T7_BLK - 1) / TG_PAPER_T7_BLK, [&](int c) { return bs[c]; });
+    }
     // Every HBM input of the env is issued in one batch at the start (the
     // lead lane's scalars and root-reset template, every lane's history
     // entries), so the kernel waits on memory once; a reset replaces them by
@@ -401,7 +447,7 @@ __global__ __launch_bounds__(64 * PAPER_EPW) void paper_post_kernel(tg_paper_par
     }
     dsq = p_wsum(dsq);
     if (lead) {
-        b.scratch[e] = dsq;
+        if (!fin) b.scratch[e] = dsq;
         // reward terms 1-5 (:722-746) on the newest clean entry
         const float *last = ob;
         const float tilt_err = p_clamp(last[0] / p.max_tilt, -1.0f, 1.0f);
@@ -414,7 +460,9 @@ __global__ __launch_bounds__(64 * PAPER_EPW) void paper_post_kernel(tg_paper_par
         const float tilt_w = 1.0f - tanhf(50.0f * (tilt_err * tilt_err));
         const float dtilt_w = 1.0f - tanhf(50.0f * (dtilt_err * dtilt_err));
         const float r5 = 1.0f - (act * act) * (tilt_w * dtilt_w);
-        b.rew_buf[e] = r1 * 0.45f + r2 * 0.1f + r4 * 0.35f + r5 * 2.0f;
+        const float rew = r1 * 0.45f + r2 * 0.1f + r4 * 0.35f + r5 * 2.0f;
+        if (fin) fin_env(p, b, e, tot, last[0], prog, rew);
+        else b.rew_buf[e] = rew;
         // command changes (:402-417)
         if (prog == p.speed_freq_update) b.curent_speed[e] = p_aff(p.speed_range, draw(sd, 1, 0, 5));
         float yc = L.yaw_cmd;
@@ -460,9 +508,7 @@ __global__ __launch_bounds__(64 * PAPER_EPW) void paper_post_kernel(tg_paper_par
 // (the per-env partials are 4 B/env and L2-resident, and every workgroup adds
 // them in the same order, so all agree bit for bit): no second launch and no
 // single-workgroup tail whose dependent loads run one after another.
-constexpr int FIN_WG = 1024, FIN_UNROLL = 8;
 __global__ __launch_bounds__(FIN_WG) void paper_finish_kernel(tg_paper_params p, tg_paper_buffers b) {
-    __shared__ double part[FIN_WG / 64];
     const int t = threadIdx.x, n = p.num_envs;
     const int e = blockIdx.x * FIN_WG + t;
     // the env's own inputs first, so their latency overlaps the sum
@@ -473,31 +519,18 @@ __global__ __launch_bounds__(FIN_WG) void paper_finish_kernel(tg_paper_params p,
         prog = b.progress_buf[e];
         rew = b.rew_buf[e];
     }
-    double s = 0.0;
-    for (int e0 = t; e0 < n; e0 += FIN_WG * FIN_UNROLL) {
-        float v[FIN_UNROLL];
+    // the per-env partials of the post kernel, block sums formed here
+    const double tot = t7_batch_sum((n + TG_PAPER_T7_BLK - 1) / TG_PAPER_T7_BLK, [&](int c) {
+        double s = 0.0;
 #pragma unroll
-        for (int k = 0; k < FIN_UNROLL; ++k) v[k] = e0 + k * FIN_WG < n ? b.scratch[e0 + k * FIN_WG] : 0.f;
-#pragma unroll
-        for (int k = 0; k < FIN_UNROLL; ++k) s += (double)v[k];
-    }
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
-    if ((t & 63) == 0) part[t >> 6] = s;
-    __syncthreads();
-    double tot = 0.0;
-#pragma unroll
-    for (int w = 0; w < FIN_WG / 64; ++w) tot += part[w];
+        for (int i = 0; i < TG_PAPER_T7_BLK; ++i) {
+            const int k = c * TG_PAPER_T7_BLK + i;
+            s += (double)(k < n ? b.scratch[k] : 0.0f);
+        }
+        return s;
+    });
     if (e >= n) return;
-    const float r7 = 1.0f - (float)(tot / ((double)n * (PH - 1)));
-    const bool finished = prog >= p.max_episode_length - 1;
-    const bool felt = fabsf(tilt) >= p.max_tilt;
-    float r = rew + r7 * 0.2f;
-    r = r < 0.0f ? 0.0f : r;
-    b.rew_buf[e] = felt ? -1.0f : r;
-    const bool rs = finished || felt;
-    b.reset_buf[e] = rs ? 1 : 0;
-    b.timeout_buf[e] = finished && rs;
+    fin_env(p, b, e, tot, tilt, prog, rew);
 }
 
 __global__ __launch_bounds__(64) void paper_reset_idx_kernel(tg_paper_params p, tg_paper_buffers b, const int32_t *ids,
@@ -514,22 +547,24 @@ int launch_paper_pre(const tg_paper_params &p, const tg_paper_buffers &b, const 
 }
 int launch_paper_post(const tg_paper_params &p, const tg_paper_buffers &b, const float *rd, const float *nd,
                       const float *sd, const float *yd, const float *pd, uint64_t counter, hipStream_t s,
-                      uint64_t model_hash, float *comp, bool *inplace) {
+                      uint64_t model_hash, float *comp, bool *inplace, bool fin) {
     const dim3 grid((p.num_envs + PAPER_EPW - 1) / PAPER_EPW), block(64 * PAPER_EPW);
     const uint32_t lo = (uint32_t)counter, hi = (uint32_t)(counter >> 32);
     bool done = false;
 #define TG_PAPER_POST(MODEL)                                                                                  \
     if constexpr ((MODEL::FUSED & 4) != 0 && MODEL::NTL > 0) {                                              \
         if (!done && comp && model_hash == MODEL::hash) {                                                    \
-            hipLaunchKernelGGL(paper_post_kernel<MODEL>, grid, block, 0, s, p, b, rd, nd, sd, yd, pd, lo, hi, comp); \
+            hipLaunchKernelGGL(paper_post_kernel<MODEL>, grid, block, 0, s, p, b, rd, nd, sd, yd, pd, lo, hi, comp, \
+                               (int)fin);                                                            \
             done = true;                                                                                     \
         }                                                                                                    \
     }
     TG_FOR_EACH_MODEL(TG_PAPER_POST)
 #undef TG_PAPER_POST
     if (inplace) *inplace = done;
-    if (!done) hipLaunchKernelGGL(paper_post_kernel<void>, grid, block, 0, s, p, b, rd, nd, sd, yd, pd, lo, hi, nullptr);
-    hipLaunchKernelGGL(paper_finish_kernel, dim3((p.num_envs + FIN_WG - 1) / FIN_WG), dim3(FIN_WG), 0, s, p, b);
+    if (!done)
+        hipLaunchKernelGGL(paper_post_kernel<void>, grid, block, 0, s, p, b, rd, nd, sd, yd, pd, lo, hi, nullptr, (int)fin);
+    if (!fin) hipLaunchKernelGGL(paper_finish_kernel, dim3((p.num_envs + FIN_WG - 1) / FIN_WG), dim3(FIN_WG), 0, s, p, b);
     return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
 }
 int launch_paper_reset_idx(const tg_paper_params &p, const tg_paper_buffers &b, const int32_t *ids, int n,

@@ -143,7 +143,9 @@ template <class M> struct ParLayout {
     // per (schedule step, lane) descriptor, one int4 (see step_desc)
     static constexpr int T_DESC = (T_CPATH + M::NCG * M::MAXD + 3) & ~3;
     static constexpr int T_ZERO = T_DESC + 4 * M::NSTEP * M::LPE;     // 32 zero floats
-    static constexpr int T_TOTAL = T_ZERO + 32;
+    // GogoroPaper (FUSED bit 4): the envs' reward-term-7 partials
+    static constexpr int T_T7 = T_ZERO + 32;
+    static constexpr int T_TOTAL = T_T7 + ((M::FUSED & 4) ? M::EPB : 0);
     // SEPC (when the LDS has room): pass 2 writes each group's contribution to
     // its parent (I^a 21 at +0, p^a 6 at +24) and pass 3 its acceleration (+0)
     // into a separate 32-float block, so pass 1's rigid inertias and bias
@@ -490,6 +492,10 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                 for (int k = 0; k < PC; ++k) hh[k] = hv[k];
                 pp.curent_command[e] = cmd;
             }
+            if (pp.t7) {   // the env's partial into the workgroup's slots, summed after the barrier
+                static_assert(EPB == TG_PAPER_T7_BLK, "a term-7 block is one workgroup");
+                reinterpret_cast<float *>(tab + PL::T_T7)[le] = owner ? paper_t7_partial(pp, e, cmd) : 0.0f;
+            }
         }
     }
     // the walk pre-physics (tg_walk_step): the env's clamped actions and drive
@@ -523,6 +529,9 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         for (int k = 0; k < 13; ++k) rt0[k] = root[k];
     }
     __syncthreads();   // group tables (shared by both wavefronts)
+    if constexpr ((M::FUSED & 4) != 0) {
+        if (a.pp_in_step && a.pp.t7 && tid == 0) paper_t7_block(a.pp, reinterpret_cast<const float *>(tab + PL::T_T7), chunk);
+    }
     if constexpr (!EARLY) {
 #pragma unroll
         for (int k = 0; k < 13; ++k) rt0[k] = root[k];

@@ -36,7 +36,20 @@ struct PaperPre {
     float *curent_command, *pos_target, *vel_target;
     float max_steering;
     int use_steer_delay, dof_steer, dof_rear;
+    // reward term 7's partials, formed here for a post launch that finishes
+    // the batch itself (t7 null: the post kernel forms them): the sum over
+    // each block of TG_PAPER_T7_BLK envs (one step-kernel workgroup)
+    const float *buffer_obs;   // [N, TG_PAPER_HIST * TG_PAPER_OBS] clean history
+    const int64_t *reset_buf;  // [N]
+    double *t7;                // [ceil(N / TG_PAPER_T7_BLK)] block sums
 };
+// the canonical order of the term-7 batch sum (paper_post_kernel with the
+// finish inline, paper_finish_kernel): per block of TG_PAPER_T7_BLK envs the
+// partials added in env order (double); thread t of TG_PAPER_T7_THREADS adds
+// blocks t, t + TG_PAPER_T7_THREADS, ...; xor-butterfly per wavefront; the
+// wavefront sums in order
+#define TG_PAPER_T7_BLK 16
+#define TG_PAPER_T7_THREADS 512
 
 struct StepArgs {
     int N, D;
@@ -160,7 +173,8 @@ int launch_paper_pre(const tg_paper_params &p, const tg_paper_buffers &b, const 
 // in-place seat composites (codegen FUSED bit 4) gets them and *inplace is set
 int launch_paper_post(const tg_paper_params &p, const tg_paper_buffers &b, const float *rd, const float *nd,
                       const float *sd, const float *yd, const float *pd, uint64_t counter, hipStream_t s,
-                      uint64_t model_hash = 0, float *comp = nullptr, bool *inplace = nullptr);
+                      uint64_t model_hash = 0, float *comp = nullptr, bool *inplace = nullptr,
+                      bool fin = false);
 int launch_paper_reset_idx(const tg_paper_params &p, const tg_paper_buffers &b, const int32_t *ids, int n,
                            const float *rd, uint64_t counter, hipStream_t s);
 int launch_walk_pre(const tg_walk_params &p, const tg_walk_buffers &b, const float *actions, hipStream_t s);

@@ -87,6 +87,7 @@ struct tg_sim {
     bool always_compose = false; // never skip the compose launch (TG_ALWAYS_COMPOSE=1)
     bool pre_in_compose = false; // tg_walk_step: pre-physics in the compose launch, not the step kernel (TG_PRE_IN_COMPOSE=1)
     bool no_inplace = false;     // tg_gogoro_step: reset envs re-composed, not updated in place (TG_SEAT_RECOMPOSE=1)
+    bool paper_finish_launch = false;   // tg_paper_step: term 7 summed by the finish launch (TG_PAPER_FINISH=1)
     int timing = 0;          // period (0: off)
     int64_t timing_count = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending, ev_free;
@@ -202,6 +203,7 @@ int tg_sim_create(const tg_model_desc *m, const tg_sim_params *params, int32_t n
     if (const char *u = getenv("TG_ALWAYS_COMPOSE")) s->always_compose = u[0] == '1';
     if (const char *u = getenv("TG_PRE_IN_COMPOSE")) s->pre_in_compose = u[0] == '1';
     if (const char *u = getenv("TG_SEAT_RECOMPOSE")) s->no_inplace = u[0] == '1';
+    if (const char *u = getenv("TG_PAPER_FINISH")) s->paper_finish_launch = u[0] == '1';
     s->device = device;
     s->N = num_envs;
     s->D = m->num_dofs;
@@ -842,6 +844,7 @@ int tg_paper_step(tg_sim *s, const tg_paper_params *p, const tg_paper_buffers *b
     if (int rc = check_paper(s, p, b)) return rc;
     if (!actions) return fail(TG_ERR_ARG, "paper: null actions");
     if (n_simulate < 1) return fail(TG_ERR_ARG, "tg_paper_step: n_simulate %d < 1", n_simulate);
+    bool fin = false;
     for (int i = 0; i < n_simulate; ++i) {
         tg::StepArgs a = step_args(s);
         if (i == 0) {   // pre_physics_step as the first compose launch's prologue
@@ -861,12 +864,20 @@ int tg_paper_step(tg_sim *s, const tg_paper_params *p, const tg_paper_buffers *b
             // model's kernel has the pre-physics slots; else the compose prologue
             q.actions = actions;
             a.pp_in_step = (n_simulate == 1 && (tg::model_fused(s->hash) & 6) && !s->pre_in_compose) ? 1 : 0;
+            // the step kernel also forms reward term 7's partials, so the post
+            // launch finishes the batch itself (no finish launch)
+            if (a.pp_in_step && !s->paper_finish_launch && p->num_envs % 8 == 0) {   // 8: PAPER_EPW
+                q.buffer_obs = b->buffer_obs;
+                q.reset_buf = b->reset_buf;
+                q.t7 = reinterpret_cast<double *>(b->scratch);   // (N floats hold N / 16 doubles)
+                fin = true;
+            }
         }
         if (int rc = simulate_args(s, a)) return rc < 0 ? rc : fail(TG_ERR_STATE, "no step kernel for this model");
     }
     bool inplace = false;
     if (int rc = tg::launch_paper_post(*p, *b, nullptr, nullptr, nullptr, nullptr, nullptr, counter, s->stream,
-                                       s->hash, s->no_inplace ? nullptr : s->comp, &inplace))
+                                       s->hash, s->no_inplace ? nullptr : s->comp, &inplace, fin))
         return fail(rc, "launch failed");
     // the post kernel's resets either update the seat composites in place or
     // mark their envs for the next compose
