@@ -100,6 +100,12 @@ typedef struct tg_paper_buffers {
     float *body_force;         /* [N, G, 6] or NULL (pushes off) */
     uint8_t *env_dirty;        /* [N] */
     float *scratch;            /* [N] per-env partial sums (reward term 7) */
+    /* [N*L, 3] world-frame per-link forces or NULL: tg_paper_step applies them
+     * to the next simulate exactly as tg_apply_rigid_body_force_tensors(sim,
+     * rb_forces, NULL, TG_ENV_SPACE) right after the call would (the post_physics
+     * pushes write head_p_link's rows first, paper.py:449-457), reduced to the
+     * group wrenches inside the post launch; the separate-call API ignores it */
+    const float *rb_forces;
 } tg_paper_buffers;
 
 typedef struct tg_sim tg_sim;

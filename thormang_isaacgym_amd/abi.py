@@ -112,7 +112,7 @@ class tg_paper_buffers(C.Structure):
         "curent_command", "command_history", "steer_delay", "steer_offsets", "curent_speed", "curent_speed_offset",
         "curent_imu_x_offset", "curent_damping_cfg", "yaw_command", "speed_no_noise", "perturbation", "root_reset",
         "thormang_pose", "root", "dof_state", "pos_target", "vel_target", "dof_props", "body_force", "env_dirty",
-        "scratch")]
+        "scratch", "rb_forces")]
 
 
 TG_WALK_MAX_DOF = 40

@@ -295,6 +295,29 @@ __device__ __forceinline__ void fin_env(const tg_paper_params &p, const tg_paper
     b.timeout_buf[e] = finished && rs;
 }
 
+// rb_out (M with the link-com block): the post-physics' rb_forces reduced to
+// the next simulate's group wrenches by the env's wavefront after its own
+// writes (rb_force_env, as rb_force_kernel would at the next simulate)
+template <class M> constexpr bool paper_rb_fusable() {
+    if constexpr (std::is_void<M>::value) return false;
+    else return M::LCOM != 0 && M::NL <= 64 && M::NG <= 64;
+}
+template <class M, bool ON = paper_rb_fusable<M>()> struct PaperRb {
+    __device__ static void run(const tg_paper_params &, const tg_paper_buffers &, int, float *, float *) {}
+};
+template <class M> struct PaperRb<M, true> {
+    __device__ static void run(const tg_paper_params &p, const tg_paper_buffers &b, int e, float *comp, float *out) {
+        __shared__ float T[PAPER_EPW][M::NL][12], F[PAPER_EPW][M::NL][10];
+        const int wv = threadIdx.x / 64;
+        // this wave's global writes (reset root / dofs / seat windows /
+        // composite, pushes) before its lanes read them back
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        rb_force_env<M>(b.root, b.dof_state, comp, e, nullptr, b.rb_forces, nullptr, TG_ENV_SPACE, out,
+                        threadIdx.x % 64, T[wv], F[wv], b.dof_props, p.num_envs);
+    }
+};
+
 // fin: the step kernel formed the term-7 block sums already (PaperPre.t7, in
 // b.scratch, tg_paper_step), so each workgroup sums the batch first, in the
 // canonical order, and its envs end with their final rewards / resets: no
@@ -304,7 +327,7 @@ template <class M>
 __global__ __launch_bounds__(64 * PAPER_EPW) void paper_post_kernel(tg_paper_params p, tg_paper_buffers b, const float *rd,
                                                         const float *nd, const float *sd, const float *yd,
                                                         const float *pd, uint32_t c_lo, uint32_t c_hi, float *comp,
-                                                        int fin) {
+                                                        int fin, float *rb_out) {
     static_assert(64 * PAPER_EPW >= T7T, "the canonical sum's threads");
     double tot = 0.0;
     if (fin) {
@@ -501,6 +524,7 @@ __global__ __launch_bounds__(64 * PAPER_EPW) void paper_post_kernel(tg_paper_par
         float *wr = b.body_force + (size_t)6 * p.num_groups * e;
         for (int i = 6 + lane; i < 6 * p.num_groups; i += 64) wr[i] = 0.0f;
     }
+    if (rb_out) PaperRb<M>::run(p, b, e, comp, rb_out);
 }
 
 // batch mean for reward term 7, then rewards, resets, time_outs of the
@@ -547,23 +571,28 @@ int launch_paper_pre(const tg_paper_params &p, const tg_paper_buffers &b, const 
 }
 int launch_paper_post(const tg_paper_params &p, const tg_paper_buffers &b, const float *rd, const float *nd,
                       const float *sd, const float *yd, const float *pd, uint64_t counter, hipStream_t s,
-                      uint64_t model_hash, float *comp, bool *inplace, bool fin) {
+                      uint64_t model_hash, float *comp, bool *inplace, bool fin, float *rb_out, bool *rb_done) {
     const dim3 grid((p.num_envs + PAPER_EPW - 1) / PAPER_EPW), block(64 * PAPER_EPW);
     const uint32_t lo = (uint32_t)counter, hi = (uint32_t)(counter >> 32);
     bool done = false;
 #define TG_PAPER_POST(MODEL)                                                                                  \
     if constexpr ((MODEL::FUSED & 4) != 0 && MODEL::NTL > 0) {                                              \
         if (!done && comp && model_hash == MODEL::hash) {                                                    \
+            const bool rb = rb_out && b.rb_forces && paper_rb_fusable<MODEL>();                                \
             hipLaunchKernelGGL(paper_post_kernel<MODEL>, grid, block, 0, s, p, b, rd, nd, sd, yd, pd, lo, hi, comp, \
-                               (int)fin);                                                            \
+                               (int)fin, rb ? rb_out : nullptr);                                     \
+            if (rb_done) *rb_done = rb;                                                                      \
             done = true;                                                                                     \
         }                                                                                                    \
     }
     TG_FOR_EACH_MODEL(TG_PAPER_POST)
 #undef TG_PAPER_POST
     if (inplace) *inplace = done;
-    if (!done)
-        hipLaunchKernelGGL(paper_post_kernel<void>, grid, block, 0, s, p, b, rd, nd, sd, yd, pd, lo, hi, nullptr, (int)fin);
+    if (!done) {
+        if (rb_done) *rb_done = false;
+        hipLaunchKernelGGL(paper_post_kernel<void>, grid, block, 0, s, p, b, rd, nd, sd, yd, pd, lo, hi, nullptr, (int)fin,
+                           nullptr);
+    }
     if (!fin) hipLaunchKernelGGL(paper_finish_kernel, dim3((p.num_envs + FIN_WG - 1) / FIN_WG), dim3(FIN_WG), 0, s, p, b);
     return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
 }

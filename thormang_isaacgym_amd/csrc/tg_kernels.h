@@ -174,7 +174,7 @@ int launch_paper_pre(const tg_paper_params &p, const tg_paper_buffers &b, const 
 int launch_paper_post(const tg_paper_params &p, const tg_paper_buffers &b, const float *rd, const float *nd,
                       const float *sd, const float *yd, const float *pd, uint64_t counter, hipStream_t s,
                       uint64_t model_hash = 0, float *comp = nullptr, bool *inplace = nullptr,
-                      bool fin = false);
+                      bool fin = false, float *rb_out = nullptr, bool *rb_done = nullptr);
 int launch_paper_reset_idx(const tg_paper_params &p, const tg_paper_buffers &b, const int32_t *ids, int n,
                            const float *rd, uint64_t counter, hipStream_t s);
 int launch_walk_pre(const tg_walk_params &p, const tg_walk_buffers &b, const float *actions, hipStream_t s);

@@ -88,6 +88,7 @@ struct tg_sim {
     bool pre_in_compose = false; // tg_walk_step: pre-physics in the compose launch, not the step kernel (TG_PRE_IN_COMPOSE=1)
     bool no_inplace = false;     // tg_gogoro_step: reset envs re-composed, not updated in place (TG_SEAT_RECOMPOSE=1)
     bool paper_finish_launch = false;   // tg_paper_step: term 7 summed by the finish launch (TG_PAPER_FINISH=1)
+    bool paper_rb_launch = false;       // tg_paper_step: rb_forces reduced by rb_force_kernel (TG_PAPER_RB_LAUNCH=1)
     int timing = 0;          // period (0: off)
     int64_t timing_count = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending, ev_free;
@@ -204,6 +205,7 @@ int tg_sim_create(const tg_model_desc *m, const tg_sim_params *params, int32_t n
     if (const char *u = getenv("TG_PRE_IN_COMPOSE")) s->pre_in_compose = u[0] == '1';
     if (const char *u = getenv("TG_SEAT_RECOMPOSE")) s->no_inplace = u[0] == '1';
     if (const char *u = getenv("TG_PAPER_FINISH")) s->paper_finish_launch = u[0] == '1';
+    if (const char *u = getenv("TG_PAPER_RB_LAUNCH")) s->paper_rb_launch = u[0] == '1';
     s->device = device;
     s->N = num_envs;
     s->D = m->num_dofs;
@@ -875,10 +877,19 @@ int tg_paper_step(tg_sim *s, const tg_paper_params *p, const tg_paper_buffers *b
         }
         if (int rc = simulate_args(s, a)) return rc < 0 ? rc : fail(TG_ERR_STATE, "no step kernel for this model");
     }
-    bool inplace = false;
+    bool inplace = false, rb_done = false;
+    const bool rb_fuse = b->rb_forces && !s->paper_rb_launch;
     if (int rc = tg::launch_paper_post(*p, *b, nullptr, nullptr, nullptr, nullptr, nullptr, counter, s->stream,
-                                       s->hash, s->no_inplace ? nullptr : s->comp, &inplace, fin))
+                                       s->hash, s->no_inplace ? nullptr : s->comp, &inplace, fin,
+                                       rb_fuse ? s->force : nullptr, &rb_done))
         return fail(rc, "launch failed");
+    if (b->rb_forces) {   // the next simulate's rigid-body forces: reduced already, or pending as if applied now
+        s->rbf_f = b->rb_forces;
+        s->rbf_t = nullptr;
+        s->rbf_space = TG_ENV_SPACE;
+        s->rbf_pending = !rb_done;
+        s->forces_pending = true;
+    }
     // the post kernel's resets either update the seat composites in place or
     // mark their envs for the next compose
     if (!inplace) s->dirty_possible = true;

@@ -289,6 +289,8 @@ class Gogoro(VecTask):
             setattr(b, k, t.data_ptr())
         if self.obs_buf.shape[1] != NOBS * HIST:
             raise RuntimeError("obs_buf must be [N, 160]")
+        if push:   # tg_paper_step applies the [N*L, 3] tensor to the next simulate itself (:457)
+            b.rb_forces = self._perturbations.data_ptr()
         self._buf_tensors = pairs
         return b
 
@@ -319,9 +321,9 @@ class Gogoro(VecTask):
         self._keep_post = keep
         self._post_host()
 
-    def _post_host(self):
+    def _post_host(self, applied: bool = False):
         self.curent_step += 1
-        if self.switches["PUSH_ROBOT"]:   # :449-457, the reference's own [N*L, 3] tensor
+        if self.switches["PUSH_ROBOT"] and not applied:   # :449-457, the reference's own [N*L, 3] tensor
             self.sim.apply_rigid_body_force_tensors(torch.flatten(self._perturbations, end_dim=-2), None)
 
     def compute_obs_rwd(self):
@@ -338,7 +340,9 @@ class Gogoro(VecTask):
                                       self.control_freq_inv, self._counter()), "tg_paper_step")
             self._keep = a
             self.frame_count += self.control_freq_inv
-            self._post_host()
+            # (tg_paper_step applied rb_forces = the perturbation tensor already,
+            # as apply_rigid_body_force_tensors right after it would)
+            self._post_host(applied=bool(self._bufs.rb_forces))
         else:
             self.pre_physics_step(actions)
             for _ in range(self.control_freq_inv):
