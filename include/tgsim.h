@@ -254,9 +254,12 @@ int tg_rng_fill(tg_sim *sim, int32_t kind, uint64_t seed, uint64_t counter, floa
 /* Benchmark instrumentation (no reference counterpart): with period > 0,
  * tg_simulate brackets every period-th articulation step kernel launch with HIP
  * events on the sim stream (an event pair serialises the queue for ~5 us each
- * side, so sampling keeps the instrumented run's throughput honest); 0 turns
- * timing off.  tg_read_kernel_timing waits for the recorded launches and
- * returns (and resets) the summed kernel time and the timed launch count. */
+ * side, so sampling keeps the instrumented run's throughput honest); with
+ * period = -W < 0 it brackets windows of W consecutive step-kernel launches
+ * with one pair (no event between the kernels it times; a window another
+ * launch of the library falls into is dropped); 0 turns timing off.
+ * tg_read_kernel_timing waits for the recorded launches and returns (and
+ * resets) the summed kernel time and the timed launch count. */
 int tg_set_kernel_timing(tg_sim *sim, int32_t period);
 int tg_read_kernel_timing(tg_sim *sim, double *total_ms, int64_t *launches);
 

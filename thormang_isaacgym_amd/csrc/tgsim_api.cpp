@@ -89,9 +89,16 @@ struct tg_sim {
     bool no_inplace = false;     // tg_gogoro_step: reset envs re-composed, not updated in place (TG_SEAT_RECOMPOSE=1)
     bool paper_finish_launch = false;   // tg_paper_step: term 7 summed by the finish launch (TG_PAPER_FINISH=1)
     bool paper_rb_launch = false;       // tg_paper_step: rb_forces reduced by rb_force_kernel (TG_PAPER_RB_LAUNCH=1)
-    int timing = 0;          // period (0: off)
+    int timing = 0;          // period (0: off; < 0: windows of -timing launches)
     int64_t timing_count = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending, ev_free;
+    std::vector<int> ev_launches;   // step-kernel launches each pending pair brackets
+    // windowed timing (tg_set_kernel_timing with a negative period): one event
+    // pair around -timing consecutive step-kernel launches, dropped when any
+    // other launch of the library falls inside it (win_dirty)
+    std::pair<hipEvent_t, hipEvent_t> win{nullptr, nullptr};
+    int win_n = 0;
+    bool win_dirty = false;
     double timed_ms = 0.0;
     int64_t timed_launches = 0;
 
@@ -111,10 +118,17 @@ struct tg_sim {
         if (hf) (void)hipFree(hf);
         for (auto *v : {&ev_pending, &ev_free})
             for (auto &e : *v) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+        if (win.first) { (void)hipEventDestroy(win.first); (void)hipEventDestroy(win.second); }
     }
 };
 
 namespace {
+// a launch other than the step kernel: an open timing window no longer
+// brackets step kernels only
+inline void win_touch(tg_sim *s) {
+    if (s->win.first) s->win_dirty = true;
+}
+
 int check_sim(tg_sim *s) { return s ? 0 : fail(TG_ERR_ARG, "null tg_sim"); }
 int check_ids(tg_sim *s, const int32_t *ids, int32_t n) {
     if (n < 0 || n > s->N) return fail(TG_ERR_ARG, "index count %d out of range [0, %d]", n, s->N);
@@ -358,6 +372,7 @@ int tg_set_actor_root_state_indexed(tg_sim *s, const float *root, const int32_t 
     if (int rc = check_ids(s, ids, n)) return rc;
     if (!root) return fail(TG_ERR_ARG, "null root state");
     if (root == s->root) return TG_OK;
+    win_touch(s);
     if (int rc = tg::launch_scatter_rows(s->root, root, ids, n, 13, s->stream)) return fail(rc, "scatter failed");
     return TG_OK;
 }
@@ -367,6 +382,7 @@ int tg_set_dof_state_indexed(tg_sim *s, const float *dof, const int32_t *ids, in
     if (int rc = check_ids(s, ids, n)) return rc;
     if (!dof) return fail(TG_ERR_ARG, "null dof state");
     if (dof == s->dof) return TG_OK;
+    win_touch(s);
     if (int rc = tg::launch_scatter_rows(s->dof, dof, ids, n, 2 * s->D, s->stream)) return fail(rc, "scatter failed");
     return TG_OK;
 }
@@ -379,7 +395,9 @@ int tg_set_dof_properties_indexed(tg_sim *s, int32_t field, const float *vals, c
     if (!vals) return fail(TG_ERR_ARG, "null property values");
     float *dst = s->props + (size_t)field * s->N * s->D;
     if (vals != dst)
+        win_touch(s);
         if (int rc = tg::launch_scatter_field(dst, vals, ids, n, s->D, s->stream)) return fail(rc, "scatter failed");
+    win_touch(s);
     if (int rc = tg::launch_mark_dirty(s->dirty, ids, n, s->stream)) return fail(rc, "mark dirty failed");
     return TG_OK;
 }
@@ -389,7 +407,9 @@ int tg_set_body_mass_scale_indexed(tg_sim *s, const float *scale, const int32_t 
     s->dirty_possible = true;
     if (int rc = check_ids(s, ids, n)) return rc;
     if (!scale) return fail(TG_ERR_ARG, "null mass scale");
+    win_touch(s);
     if (int rc = tg::launch_scatter_rows(s->mass_scale, scale, ids, n, s->L, s->stream)) return fail(rc, "scatter failed");
+    win_touch(s);
     if (int rc = tg::launch_mark_dirty(s->dirty, ids, n, s->stream)) return fail(rc, "mark dirty failed");
     return TG_OK;
 }
@@ -399,6 +419,7 @@ int tg_set_shape_friction_indexed(tg_sim *s, const float *mu, const int32_t *ids
     if (int rc = check_ids(s, ids, n)) return rc;
     if (!mu) return fail(TG_ERR_ARG, "null friction");
     if (s->S == 0) return TG_OK;
+    win_touch(s);
     if (int rc = tg::launch_scatter_rows(s->shape_mu, mu, ids, n, s->S, s->stream)) return fail(rc, "scatter failed");
     return TG_OK;
 }
@@ -483,20 +504,39 @@ static int simulate_args(tg_sim *s, const tg::StepArgs &a_in, const tg::WalkPost
         a.clist = s->clist + (size_t)prev * s->N;
         a.ccount = s->ccount + prev;
     }
+    bool rb_launch = false;
     if (s->rbf_pending) {   // the pending per-link forces: in the full compose launch, else on their own
         if (!a.skip_compose && !a.compose_list) {
             a.rbf_forces = s->rbf_f;
             a.rbf_torques = s->rbf_t;
             a.rbf_space = s->rbf_space;
             a.rbf_out = s->force;
-        } else if (int rc = tg::launch_rb_forces(s->hash, s->root, s->dof, s->comp, (int)s->N, s->mass_scale,
-                                                 s->rbf_f, s->rbf_t, s->rbf_space, s->force, s->props, s->stream)) {
-            return fail(rc, "rigid-body force launch failed");
+        } else {
+            rb_launch = true;
+            if (int rc = tg::launch_rb_forces(s->hash, s->root, s->dof, s->comp, (int)s->N, s->mass_scale, s->rbf_f,
+                                              s->rbf_t, s->rbf_space, s->force, s->props, s->stream))
+                return fail(rc, "rigid-body force launch failed");
         }
         s->rbf_pending = false;
     }
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     const bool timed = s->timing > 0 && s->timing_count % s->timing == 0;
+    // windowed timing: this call launches a compose / rigid-body force kernel
+    // too (other), or only the step kernel
+    const bool windowed = s->timing < 0, other = !a.skip_compose || rb_launch;
+    if (windowed && s->win.first && other) s->win_dirty = true;
+    if (windowed && !s->win.first && !other) {
+        if (!s->ev_free.empty()) {
+            s->win = s->ev_free.back();
+            s->ev_free.pop_back();
+        } else {
+            HIPCHK(hipEventCreate(&s->win.first));
+            HIPCHK(hipEventCreate(&s->win.second));
+        }
+        s->win_n = 0;
+        s->win_dirty = false;
+        HIPCHK(hipEventRecord(s->win.first, s->stream));
+    }
     if (timed) {
         if (!s->ev_free.empty()) {
             ev = s->ev_free.back();
@@ -513,11 +553,28 @@ static int simulate_args(tg_sim *s, const tg::StepArgs &a_in, const tg::WalkPost
     // launch that went through; otherwise it goes back to the free list
     if (rc != 0) {
         if (ev.first) s->ev_free.push_back(ev);
+        if (s->win.first) {   // the open window is dropped
+            s->ev_free.push_back(s->win);
+            s->win = {nullptr, nullptr};
+        }
         if (rc == 1) return 1;   // not launched (no such instantiation): caller falls back
         return fail(rc, "step launch failed: %s", hipGetErrorString(hipGetLastError()));
     }
     if (s->timing > 0) s->timing_count++;
-    if (ev.first) s->ev_pending.push_back(ev);
+    if (ev.first) {
+        s->ev_pending.push_back(ev);
+        s->ev_launches.push_back(1);
+    }
+    if (windowed && s->win.first && ++s->win_n == -s->timing) {   // the window closes
+        if (!s->win_dirty) {
+            HIPCHK(hipEventRecord(s->win.second, s->stream));
+            s->ev_pending.push_back(s->win);
+            s->ev_launches.push_back(s->win_n);
+        } else {
+            s->ev_free.push_back(s->win);
+        }
+        s->win = {nullptr, nullptr};
+    }
     s->forces_pending = false;   // apply_rigid_body_force_tensors acts for one simulate call
     if (!a.skip_compose) {   // every dirty env, or every listed one, is composed now
         if (!a.compose_list) s->dirty_possible = false;
@@ -566,6 +623,7 @@ int tg_apply_rigid_body_force_tensors(tg_sim *s, const float *forces, const floa
 int tg_rigid_body_states(tg_sim *s, float *out) {
     if (int rc = check_sim(s)) return rc;
     if (!out) return fail(TG_ERR_ARG, "tg_rigid_body_states: null output");
+    win_touch(s);
     if (int rc = tg::launch_body_states(s->hash, s->root, s->dof, (int)s->N, out, s->stream))
         return fail(rc, "rigid-body state launch failed");
     return TG_OK;
@@ -579,6 +637,7 @@ int tg_composite(tg_sim *s, float *out, int32_t recompose) {
         HIPCHK(hipMemsetAsync(s->dirty, 1, s->N, s->stream));
         tg::StepArgs a = step_args(s);
         a.cnext = s->ccount + s->list_cur;
+        win_touch(s);
         if (int rc = tg::launch_compose_only(s->hash, a, s->stream)) return fail(rc, "compose launch failed");
         s->list_pending = false;
         s->dirty_possible = false;
@@ -589,9 +648,12 @@ int tg_composite(tg_sim *s, float *out, int32_t recompose) {
 
 int tg_set_kernel_timing(tg_sim *s, int32_t period) {
     if (int rc = check_sim(s)) return rc;
-    if (period < 0) return fail(TG_ERR_ARG, "tg_set_kernel_timing: negative period");
     s->timing = period;
     s->timing_count = 0;
+    if (s->win.first) {   // an open window is dropped
+        s->ev_free.push_back(s->win);
+        s->win = {nullptr, nullptr};
+    }
     return TG_OK;
 }
 
@@ -599,14 +661,16 @@ int tg_read_kernel_timing(tg_sim *s, double *total_ms, int64_t *launches) {
     if (int rc = check_sim(s)) return rc;
     if (!total_ms || !launches) return fail(TG_ERR_ARG, "tg_read_kernel_timing: null argument");
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pend;
+    std::vector<int> cnt;
     pend.swap(s->ev_pending);   // every pair leaves the pending list, read or not
+    cnt.swap(s->ev_launches);
     for (auto &e : pend) s->ev_free.push_back(e);
-    for (auto &e : pend) {
-        HIPCHK(hipEventSynchronize(e.second));
+    for (size_t i = 0; i < pend.size(); ++i) {
+        HIPCHK(hipEventSynchronize(pend[i].second));
         float ms = 0.f;
-        HIPCHK(hipEventElapsedTime(&ms, e.first, e.second));
+        HIPCHK(hipEventElapsedTime(&ms, pend[i].first, pend[i].second));
         s->timed_ms += ms;
-        s->timed_launches += 1;
+        s->timed_launches += cnt[i];
     }
     *total_ms = s->timed_ms;
     *launches = s->timed_launches;
@@ -639,6 +703,7 @@ int tg_rng_fill(tg_sim *s, int32_t kind, uint64_t seed, uint64_t counter, float 
     if (int rc = check_sim(s)) return rc;
     if (n < 0 || (n > 0 && !out)) return fail(TG_ERR_ARG, "tg_rng_fill: bad output");
     if (kind < 0 || kind > 2) return fail(TG_ERR_ARG, "tg_rng_fill: unknown kind %d", kind);
+    win_touch(s);
     if (int rc = tg::launch_rng_fill(kind, seed, counter, out, n, s->stream)) return fail(rc, "rng launch failed");
     return TG_OK;
 }
@@ -649,6 +714,7 @@ int tg_gogoro_pre_physics(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_
     s->dirty_possible = true;
     if (!p || !b || !actions) return fail(TG_ERR_ARG, "tg_gogoro_pre_physics: null argument");
     if (p->num_envs != s->N || p->num_dof != s->D) return fail(TG_ERR_ARG, "gogoro params do not match the sim");
+    win_touch(s);
     if (int rc = tg::launch_gogoro_pre(*p, *b, actions, pre_draws, counter, s->stream)) return fail(rc, "launch failed");
     return TG_OK;
 }
@@ -698,6 +764,7 @@ int tg_gogoro_step(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_buffers
         }
         if (int rc = simulate_args(s, a)) return rc;
     }
+    win_touch(s);
     if (int rc = tg::launch_gogoro_post(*p, *b, nullptr, nullptr, nullptr, nullptr, counter_post, s->stream))
         return fail(rc, "launch failed");
     s->dirty_possible = true;   // the separate post kernel's resets mark envs dirty
@@ -712,6 +779,7 @@ int tg_gogoro_post_physics(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro
     if (p->num_envs != s->N || p->num_dof != s->D) return fail(TG_ERR_ARG, "gogoro params do not match the sim");
     if ((speed_draws == nullptr) != (yaw_draws == nullptr))
         return fail(TG_ERR_ARG, "speed_draws and yaw_draws must both be given or both be NULL");
+    win_touch(s);
     if (int rc = tg::launch_gogoro_post(*p, *b, reset_draws, obs_draws, speed_draws, yaw_draws, counter, s->stream))
         return fail(rc, "launch failed");
     return TG_OK;
@@ -724,6 +792,7 @@ int tg_gogoro_reset_idx(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_bu
     if (int rc = check_ids(s, ids, n)) return rc;
     if (!p || !b) return fail(TG_ERR_ARG, "tg_gogoro_reset_idx: null argument");
     if (p->num_envs != s->N || p->num_dof != s->D) return fail(TG_ERR_ARG, "gogoro params do not match the sim");
+    win_touch(s);
     if (int rc = tg::launch_gogoro_reset_idx(*p, *b, ids, n, reset_draws, counter, s->stream))
         return fail(rc, "launch failed");
     return TG_OK;
@@ -743,6 +812,7 @@ static int check_walk(tg_sim *s, const tg_walk_params *p, const tg_walk_buffers 
 int tg_walk_pre_physics(tg_sim *s, const tg_walk_params *p, const tg_walk_buffers *b, const float *actions) {
     if (int rc = check_walk(s, p, b)) return rc;
     if (!actions) return fail(TG_ERR_ARG, "walk: null actions");
+    win_touch(s);
     if (int rc = tg::launch_walk_pre(*p, *b, actions, s->stream)) return fail(rc, "launch failed");
     return TG_OK;
 }
@@ -793,6 +863,7 @@ int tg_walk_step(tg_sim *s, const tg_walk_params *p, const tg_walk_buffers *b, c
         }
         if (int rc = simulate_args(s, a)) return rc;
     }
+    win_touch(s);
     if (int rc = tg::launch_walk_post(*p, *b, reset_draws, push_draws, counter, s->stream))
         return fail(rc, "launch failed");
     return TG_OK;
@@ -801,6 +872,7 @@ int tg_walk_step(tg_sim *s, const tg_walk_params *p, const tg_walk_buffers *b, c
 int tg_walk_post_physics(tg_sim *s, const tg_walk_params *p, const tg_walk_buffers *b, const float *reset_draws,
                          const float *push_draws, uint64_t counter) {
     if (int rc = check_walk(s, p, b)) return rc;
+    win_touch(s);
     if (int rc = tg::launch_walk_post(*p, *b, reset_draws, push_draws, counter, s->stream))
         return fail(rc, "launch failed");
     return TG_OK;
@@ -810,6 +882,7 @@ int tg_walk_reset_idx(tg_sim *s, const tg_walk_params *p, const tg_walk_buffers 
                       const float *reset_draws, uint64_t counter) {
     if (int rc = check_walk(s, p, b)) return rc;
     if (int rc = check_ids(s, ids, n)) return rc;
+    win_touch(s);
     if (int rc = tg::launch_walk_reset_idx(*p, *b, ids, n, reset_draws, counter, s->stream))
         return fail(rc, "launch failed");
     return TG_OK;
@@ -837,6 +910,7 @@ int tg_paper_pre_physics(tg_sim *s, const tg_paper_params *p, const tg_paper_buf
     (void)counter;
     if (int rc = check_paper(s, p, b)) return rc;
     if (!actions) return fail(TG_ERR_ARG, "paper: null actions");   // (targets / history only: nothing to compose)
+    win_touch(s);
     if (int rc = tg::launch_paper_pre(*p, *b, actions, s->stream)) return fail(rc, "launch failed");
     return TG_OK;
 }
@@ -879,6 +953,7 @@ int tg_paper_step(tg_sim *s, const tg_paper_params *p, const tg_paper_buffers *b
     }
     bool inplace = false, rb_done = false;
     const bool rb_fuse = b->rb_forces && !s->paper_rb_launch;
+    win_touch(s);
     if (int rc = tg::launch_paper_post(*p, *b, nullptr, nullptr, nullptr, nullptr, nullptr, counter, s->stream,
                                        s->hash, s->no_inplace ? nullptr : s->comp, &inplace, fin,
                                        rb_fuse ? s->force : nullptr, &rb_done))
@@ -903,6 +978,7 @@ int tg_paper_post_physics(tg_sim *s, const tg_paper_params *p, const tg_paper_bu
     const bool dirty_before = s->dirty_possible;
     s->dirty_possible = true;
     bool inplace = false;
+    win_touch(s);
     if (int rc = tg::launch_paper_post(*p, *b, reset_draws, noise_draws, speed_draws, yaw_draws, push_draws, counter,
                                        s->stream, s->hash, s->no_inplace ? nullptr : s->comp, &inplace))
         return fail(rc, "launch failed");
@@ -915,6 +991,7 @@ int tg_paper_reset_idx(tg_sim *s, const tg_paper_params *p, const tg_paper_buffe
     if (int rc = check_paper(s, p, b)) return rc;
     s->dirty_possible = true;
     if (int rc = check_ids(s, ids, n)) return rc;
+    win_touch(s);
     if (int rc = tg::launch_paper_reset_idx(*p, *b, ids, n, reset_draws, counter, s->stream))
         return fail(rc, "launch failed");
     return TG_OK;

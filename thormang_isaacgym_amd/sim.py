@@ -245,7 +245,10 @@ class Sim:
 
     def set_kernel_timing(self, period: int):
         """Bracket every ``period``-th articulation step kernel launch with HIP
-        events on the sim stream (``True``/1: every launch, 0/``False``: off)."""
+        events on the sim stream (``True``/1: every launch, 0/``False``: off);
+        a negative period -W brackets windows of W consecutive step-kernel
+        launches with one event pair (a window another launch of the library
+        falls into is dropped)."""
         check(lib().tg_set_kernel_timing(self._h, int(period)), "set_kernel_timing")
 
     def read_kernel_timing(self):
