@@ -180,7 +180,9 @@ def test_gpu_paper_fused_step_equals_separate_calls(monkeypatch):
     reward term 7's per-env partials, and a post launch that sums the batch
     itself) against the three separate calls (TG_PAPER_UNFUSED=1: post kernel
     partials, finish launch): the same operations in the same order, so every
-    buffer agrees bit for bit."""
+    buffer agrees bit for bit -- including the head pushes, which tg_paper_step
+    reduces inside its post launch, after a root write between two steps
+    (the pre-reduced wrenches then give way to the next simulate's reduction)."""
     _cuda()
     import thormang_isaacgym_amd as tia
     out = []
@@ -188,8 +190,13 @@ def test_gpu_paper_fused_step_equals_separate_calls(monkeypatch):
         monkeypatch.setenv("TG_PAPER_UNFUSED", unfused)
         env = tia.make(seed=11, task="GogoroPaper", num_envs=256, sim_device="cuda:0", rl_device="cuda:0")
         g = torch.Generator(device="cuda:0").manual_seed(9)
-        for _ in range(150):
+        ids = torch.arange(0, 256, 3, device="cuda:0", dtype=torch.int32)
+        for i in range(150):
             obs, rew, reset, extras = env.step(torch.rand(256, 1, device="cuda:0", generator=g) * 2 - 1)
+            if i == 60:   # a root write after the step: the pushes of the next simulate see the new pose
+                r = env.root_tensor.clone()
+                r[:, 3:7] = torch.tensor([0.0, 0.0, 0.2955202, 0.9553365], device="cuda:0")
+                env.sim.set_actor_root_state_indexed(r, ids)
         torch.cuda.synchronize()
         out.append([t.detach().cpu().clone() for t in (obs["obs"], rew, reset, extras["time_outs"], env.root_tensor,
                                                         env.sim.dof_pos_target, env.sim.dof_vel_target,

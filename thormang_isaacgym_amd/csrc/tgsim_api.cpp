@@ -99,6 +99,11 @@ struct tg_sim {
     std::pair<hipEvent_t, hipEvent_t> win{nullptr, nullptr};
     int win_n = 0;
     bool win_dirty = false;
+    // tg_paper_step reduced its rb_forces (rbf_f) to the next simulate's group
+    // wrenches already, from the state it left; any later call that can change
+    // that state (every other launching entry point, tg_refresh, tg_bind_state)
+    // turns them back into a pending tensor, reduced at the next simulate
+    bool rbf_prereduced = false;
     double timed_ms = 0.0;
     int64_t timed_launches = 0;
 
@@ -127,6 +132,10 @@ namespace {
 // brackets step kernels only
 inline void win_touch(tg_sim *s) {
     if (s->win.first) s->win_dirty = true;
+    if (s->rbf_prereduced) {
+        s->rbf_pending = true;
+        s->rbf_prereduced = false;
+    }
 }
 
 int check_sim(tg_sim *s) { return s ? 0 : fail(TG_ERR_ARG, "null tg_sim"); }
@@ -315,12 +324,14 @@ int tg_state_ptrs(tg_sim *s, tg_state_view *v) {
 int tg_refresh(tg_sim *s) {
     if (int rc = check_sim(s)) return rc;
     s->dirty_possible = true;   // writes through the zero-copy views (env_dirty, dof_props) take effect
+    win_touch(s);
     return TG_OK;
 }
 
 int tg_bind_state(tg_sim *s, const tg_state_view *v) {
     if (int rc = check_sim(s)) return rc;
     s->dirty_possible = true;
+    win_touch(s);
     if (!v) return fail(TG_ERR_ARG, "null view");
     const size_t N = s->N, D = s->D;
     struct B {
@@ -350,6 +361,7 @@ int tg_bind_state(tg_sim *s, const tg_state_view *v) {
 static int copy_full(tg_sim *s, float *dst, const float *src, size_t count) {
     if (!src) return fail(TG_ERR_ARG, "null source tensor");
     if (src == dst) return TG_OK;
+    if (s->win.first) s->win_dirty = true;   // (a copy inside a timing window)
     HIPCHK(hipMemcpyAsync(dst, src, count * sizeof(float), hipMemcpyDeviceToDevice, s->stream));
     return TG_OK;
 }
@@ -437,6 +449,7 @@ int tg_apply_body_forces(tg_sim *s, const float *wrench) {
     if (int rc = copy_full(s, s->force, wrench, (size_t)s->N * s->G * 6)) return rc;
     s->forces_pending = true;
     s->rbf_pending = false;   // the group wrenches given here replace a pending per-link tensor
+    s->rbf_prereduced = false;
     return TG_OK;
 }
 
@@ -576,6 +589,7 @@ static int simulate_args(tg_sim *s, const tg::StepArgs &a_in, const tg::WalkPost
         s->win = {nullptr, nullptr};
     }
     s->forces_pending = false;   // apply_rigid_body_force_tensors acts for one simulate call
+    s->rbf_prereduced = false;
     if (!a.skip_compose) {   // every dirty env, or every listed one, is composed now
         if (!a.compose_list) s->dirty_possible = false;
         s->list_pending = false;
@@ -616,6 +630,7 @@ int tg_apply_rigid_body_force_tensors(tg_sim *s, const float *forces, const floa
     s->rbf_t = torques;
     s->rbf_space = space;
     s->rbf_pending = true;
+    s->rbf_prereduced = false;
     s->forces_pending = true;
     return TG_OK;
 }
@@ -824,9 +839,11 @@ int tg_walk_step(tg_sim *s, const tg_walk_params *p, const tg_walk_buffers *b, c
     if (n_simulate < 1) return fail(TG_ERR_ARG, "walk step: n_simulate %d < 1", n_simulate);
     if (p->num_dof > tg::TG_PM_MAX_DOF) return fail(TG_ERR_ARG, "walk step: num_dof %d > %d", p->num_dof, tg::TG_PM_MAX_DOF);
     if (b->body_force) {   // pre_physics_step: apply_rigid_body_force_tensors(body_force)
+        win_touch(s);      // (the copy is not the step kernel's time)
         if (int rc = copy_full(s, s->force, b->body_force, (size_t)s->N * s->G * 6)) return rc;
         s->forces_pending = true;
         s->rbf_pending = false;
+        s->rbf_prereduced = false;
     }
     if (n_simulate == 1 && !s->walk_unfused && !s->pre_in_compose) {
         // one launch per step: pre-physics (drive targets formed from the
@@ -963,6 +980,7 @@ int tg_paper_step(tg_sim *s, const tg_paper_params *p, const tg_paper_buffers *b
         s->rbf_t = nullptr;
         s->rbf_space = TG_ENV_SPACE;
         s->rbf_pending = !rb_done;
+        s->rbf_prereduced = rb_done;
         s->forces_pending = true;
     }
     // the post kernel's resets either update the seat composites in place or
