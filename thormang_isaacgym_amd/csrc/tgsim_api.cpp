@@ -839,7 +839,6 @@ int tg_walk_step(tg_sim *s, const tg_walk_params *p, const tg_walk_buffers *b, c
     if (n_simulate < 1) return fail(TG_ERR_ARG, "walk step: n_simulate %d < 1", n_simulate);
     if (p->num_dof > tg::TG_PM_MAX_DOF) return fail(TG_ERR_ARG, "walk step: num_dof %d > %d", p->num_dof, tg::TG_PM_MAX_DOF);
     if (b->body_force) {   // pre_physics_step: apply_rigid_body_force_tensors(body_force)
-        win_touch(s);      // (the copy is not the step kernel's time)
         if (int rc = copy_full(s, s->force, b->body_force, (size_t)s->N * s->G * 6)) return rc;
         s->forces_pending = true;
         s->rbf_pending = false;
