@@ -941,7 +941,8 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
 #pragma unroll
             for (int k = 0; k < 3; ++k) o[k] = pair_swap(v[k]);
         };
-#pragma unroll 1
+        // unrolled (round 2: ThormangWalk kernel 56.8 -> 56.5 us, A/B twice)
+#pragma unroll
         for (int t = M::NSTEP - 1; t >= 0; --t) {
             const I4 dc = dsc(t);
             const int g = dc.x;
