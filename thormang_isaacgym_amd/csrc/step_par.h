@@ -1040,7 +1040,8 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
             TG_SYNC();
         }
         } else {
-#pragma unroll 1
+        // unrolled (round 2: Gogoro 8.27e7 -> 8.36e7, GogoroPaper 8.55e7 -> 8.64e7, A/B twice)
+#pragma unroll
         for (int t = M::NSTEP - 1; t >= 0; --t) {
             const I4 dc = dsc(t);
             const int g = dc.x;
