@@ -118,12 +118,20 @@ int tg_gogoro_post_physics(tg_sim *sim, const tg_gogoro_params *p, const tg_gogo
                            const float *yaw_draws, uint64_t counter);
 
 /* One VecTask.step (vec_task.py:313-359): pre_physics_step + n_simulate x
- * simulate + post_physics_step with in-kernel Philox draws -- the same results
- * as tg_gogoro_pre_physics(counter_pre) + n_simulate x tg_simulate +
- * tg_gogoro_post_physics(counter_post) with NULL draw arrays, the pre-physics
- * work fused into the first simulate's compose launch. */
+ * simulate + post_physics_step -- the same operations as
+ * tg_gogoro_pre_physics(pre_draws, counter_pre) + n_simulate x tg_simulate +
+ * tg_gogoro_post_physics(reset/obs/speed/yaw draws, counter_post).  With
+ * n_simulate == 1 the whole step is ONE launch of the step kernel: the
+ * pre-physics runs at its start on each env's lead lane, the post-physics
+ * (resets with in-place seat composites, observations, reward, noise,
+ * command resample) as its epilogue on the final state.  With n_simulate > 1
+ * the pre-physics rides in the first simulate's compose launch.  The draw
+ * arrays (layouts above, NULL = in-kernel Philox) let the parity tests drive
+ * this timed path with the reference's recorded torch.rand/randn stream;
+ * speed_draws and yaw_draws go together. */
 int tg_gogoro_step(tg_sim *sim, const tg_gogoro_params *p, const tg_gogoro_buffers *b, const float *actions,
-                   int32_t n_simulate, uint64_t counter_pre, uint64_t counter_post);
+                   int32_t n_simulate, const float *pre_draws, const float *reset_draws, const float *obs_draws,
+                   const float *speed_draws, const float *yaw_draws, uint64_t counter_pre, uint64_t counter_post);
 
 /* Gogoro.reset_idx(env_ids) outside post_physics_step (gogoro_new.py:150,505-591;
  * VecTask.reset_done, vec_task.py:391-406): ids [n] int32 device, reset_draws

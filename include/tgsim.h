@@ -36,6 +36,8 @@
  *                            (tasks/gogoro_realistic_turning_sim_paper.py:457)
  *   tg_apply_body_forces     the same, pre-reduced: one wrench per group [N,G,6]
  *   tg_simulate              gym.simulate (vec_task.py:335): sim.substeps substeps
+ *   tg_get_sim_params / tg_set_sim_params
+ *                            gym.get_sim_params / set_sim_params (vec_task.py:650-660)
  *   tg_sync                  fetch_results(sim, True) (vec_task.py:339)
  *   tg_last_error            (replaces the reference's bool returns + assert,
  *                            gogoro_new.py:547,552, and quit() on creation
@@ -135,7 +137,11 @@ typedef struct tg_sim_params {
     float baumgarte;              /* penetration push-out factor per substep */
     float limit_stiffness;        /* implicit limit spring, fraction of joint inertia / h^2 */
     float limit_damping;          /* implicit limit damper, fraction of joint inertia / h   */
-    int32_t contact_iterations;   /* projected Gauss-Seidel sweeps per substep */
+    int32_t contact_iterations;   /* projected Gauss-Seidel sweeps per substep, with push-out bias
+                                     (physx.num_position_iterations) */
+    int32_t velocity_iterations;  /* bias-free sweeps after them (physx.num_velocity_iterations):
+                                     the positions integrate the velocity of the biased sweeps,
+                                     the stored velocity is the bias-free one */
     int32_t fix_base;             /* AssetOptions.fix_base_link            */
     float env_spacing;            /* create_env spacing (env origins grid) */
     int32_t envs_per_row;
@@ -205,6 +211,15 @@ int tg_apply_rigid_body_force_tensors(tg_sim *sim, const float *forces, const fl
 int tg_set_heightfield(tg_sim *sim, const float *heights, int32_t rows, int32_t cols, float horizontal_scale,
                        float vertical_scale, float origin_x, float origin_y, float friction);
 int tg_simulate(tg_sim *sim);
+/* gym.get_sim_params / gym.set_sim_params (vec_task.py:243,650-660; the
+ * reference reads the params back, edits them and writes them again for its
+ * gravity randomisation).  set takes effect at the next tg_simulate; the env
+ * grid (env_spacing, envs_per_row) is fixed at creation and ignored here.
+ * substeps may be 0 in set: simulate then integrates nothing and a step
+ * passes the state through unchanged -- the parity tests use it to replay
+ * the reference's recorded post-simulate states through the fused step. */
+int tg_get_sim_params(tg_sim *sim, tg_sim_params *out);
+int tg_set_sim_params(tg_sim *sim, const tg_sim_params *params);
 /* refresh_rigid_body_state_tensor on the tensor from acquire_rigid_body_state_tensor
  * (IsaacGym tensor API; SURVEY §8b lists it on the boundary, the reference
  * tasks do not read it): out [N, L, 13] device, caller-owned, links in model

@@ -781,37 +781,22 @@ static int collect_rows(const Env *e, Work *w, real h, Row *rows, Patch *patches
     return nr;
 }
 
-static void solve_contacts(const Env *e, Work *w, real h, real *qds, V6 v0s) {
-    const tg_model_desc *m = e->m;
-    int G = m->num_groups;
-    Row rows[3 * MAXC];
-    Patch patches[MAXC];
-    int npatch = 0;
-    int K = collect_rows(e, w, h, rows, patches, &npatch);
-    if (K == 0) return;
-    static __thread real W[3 * MAXC][3 * MAXC];
-    real vfree[3 * MAXC], lam[3 * MAXC];
-    V6 vg[MAXG];
-    group_vels(m, w, qds, v0s, vg);
-    for (int i = 0; i < K; ++i) vfree[i] = row_vel(w, &rows[i], vg);
-    for (int col = 0; col < K; ++col) {
-        V6 fi[MAXG];
-        memset(fi, 0, sizeof(V6) * G);
-        row_force(w, &rows[col], 1.0, fi);
-        real dqd[MAXD] = {0};
-        V6 dv0, dvg[MAXG];
-        impulse_response(e, w, fi, dqd, dv0);
-        group_vels(m, w, dqd, dv0, dvg);
-        for (int i = 0; i < K; ++i) W[i][col] = row_vel(w, &rows[i], dvg);
-    }
-    memset(lam, 0, sizeof(real) * K);
+/* Contact solve of one substep.  sp->contact_iterations projected
+ * Gauss-Seidel sweeps with the push-out bias (PhysX's position iterations),
+ * then sp->velocity_iterations bias-free sweeps continuing from those
+ * multipliers (PhysX's velocity iterations: a normal row's target becomes
+ * min(target, 0) -- the speculative approach bound stays, the push-out goes).
+ * qds / v0s leave with the velocity of the biased multipliers, which the
+ * positions integrate; qdv / v0v with the bias-free one, which is stored. */
+static void pgs_sweeps(int K, int npatch, const Patch *patches, const Row *rows, const real *target,
+                       real (*W)[3 * MAXC], const real *vfree, real *lam, int iters) {
 #define ROWV(i) ({ real v_ = vfree[i]; for (int j_ = 0; j_ < K; ++j_) v_ += W[i][j_] * lam[j_]; v_; })
-    for (int it = 0; it < e->sp->contact_iterations; ++it) {
+    for (int it = 0; it < iters; ++it) {
         for (int p = 0; p < npatch; ++p) {
-            Patch *P = &patches[p];
+            const Patch *P = &patches[p];
             real N = 0;
             for (int i = P->n0; i < P->n0 + P->nn; ++i) {
-                real l = lam[i] + (rows[i].target - ROWV(i)) / W[i][i];
+                real l = lam[i] + (target[i] - ROWV(i)) / W[i][i];
                 lam[i] = l > 0 ? l : 0;
                 N += lam[i];
             }
@@ -829,14 +814,61 @@ static void solve_contacts(const Env *e, Work *w, real h, real *qds, V6 v0s) {
         }
     }
 #undef ROWV
+}
+
+static void apply_impulses(const Env *e, Work *w, const Row *rows, int K, const real *lam, real *qd, V6 v0) {
+    const tg_model_desc *m = e->m;
+    int G = m->num_groups;
     V6 fi[MAXG];
     memset(fi, 0, sizeof(V6) * G);
     for (int i = 0; i < K; ++i) row_force(w, &rows[i], lam[i], fi);
     real dqd[MAXD] = {0};
     V6 dv0;
     impulse_response(e, w, fi, dqd, dv0);
-    for (int g = 1; g < G; ++g) qds[w->gdof[g]] += dqd[w->gdof[g]];
-    for (int k = 0; k < 6; ++k) v0s[k] += dv0[k];
+    for (int g = 1; g < G; ++g) qd[w->gdof[g]] += dqd[w->gdof[g]];
+    for (int k = 0; k < 6; ++k) v0[k] += dv0[k];
+}
+
+static void solve_contacts(const Env *e, Work *w, real h, real *qds, V6 v0s, real *qdv, V6 v0v) {
+    const tg_model_desc *m = e->m;
+    int G = m->num_groups, D = m->num_dofs;
+    memcpy(qdv, qds, sizeof(real) * D);
+    memcpy(v0v, v0s, sizeof(V6));
+    Row rows[3 * MAXC];
+    Patch patches[MAXC];
+    int npatch = 0;
+    int K = collect_rows(e, w, h, rows, patches, &npatch);
+    if (K == 0) return;
+    static __thread real W[3 * MAXC][3 * MAXC];
+    real vfree[3 * MAXC], lam[3 * MAXC], target[3 * MAXC];
+    V6 vg[MAXG];
+    group_vels(m, w, qds, v0s, vg);
+    for (int i = 0; i < K; ++i) vfree[i] = row_vel(w, &rows[i], vg);
+    for (int col = 0; col < K; ++col) {
+        V6 fi[MAXG];
+        memset(fi, 0, sizeof(V6) * G);
+        row_force(w, &rows[col], 1.0, fi);
+        real dqd[MAXD] = {0};
+        V6 dv0, dvg[MAXG];
+        impulse_response(e, w, fi, dqd, dv0);
+        group_vels(m, w, dqd, dv0, dvg);
+        for (int i = 0; i < K; ++i) W[i][col] = row_vel(w, &rows[i], dvg);
+    }
+    memset(lam, 0, sizeof(real) * K);
+    for (int i = 0; i < K; ++i) target[i] = rows[i].target;
+    pgs_sweeps(K, npatch, patches, rows, target, W, vfree, lam, e->sp->contact_iterations);
+    if (e->sp->velocity_iterations > 0) {
+        real lamv[3 * MAXC];
+        memcpy(lamv, lam, sizeof(real) * K);
+        for (int i = 0; i < K; ++i) target[i] = target[i] < 0 ? target[i] : 0;
+        pgs_sweeps(K, npatch, patches, rows, target, W, vfree, lamv, e->sp->velocity_iterations);
+        apply_impulses(e, w, rows, K, lamv, qdv, v0v);
+    }
+    apply_impulses(e, w, rows, K, lam, qds, v0s);
+    if (e->sp->velocity_iterations <= 0) {
+        memcpy(qdv, qds, sizeof(real) * D);
+        memcpy(v0v, v0s, sizeof(V6));
+    }
 }
 
 /* One env, one control step (all substeps).  root[13], dof[2D] updated in place. */
@@ -855,7 +887,7 @@ void oracle_physics_step_env(const tg_model_desc *m, const tg_sim_params *sp, fl
         qdd[d] = 0;
     }
     compose(m, lockq, mass_scale, &w);
-    real h = sp->dt / sp->substeps;
+    real h = sp->substeps > 0 ? sp->dt / sp->substeps : 0;
     /* floating base state */
     real pos[3] = {root[0], root[1], root[2]}, quat[4] = {root[3], root[4], root[5], root[6]};
     real qn = sqrt(quat[0] * quat[0] + quat[1] * quat[1] + quat[2] * quat[2] + quat[3] * quat[3]);
@@ -894,14 +926,18 @@ void oracle_physics_step_env(const tg_model_desc *m, const tg_sim_params *sp, fl
             cross3(wv, vv, wxv);
             for (int k = 0; k < 3; ++k) v0s[3 + k] += h * wxv[k];
         }
-        solve_contacts(&e, &w, h, qds, v0s);
-        /* velocity limits, integrate */
+        real qdv[MAXD];
+        V6 v0v;
+        solve_contacts(&e, &w, h, qds, v0s, qdv, v0v);
+        /* velocity limits, integrate: positions with the velocity of the
+         * biased sweeps, the stored velocity the bias-free one */
         for (int g = 1; g < G; ++g) {
             int d = w.gdof[g];
             real vl = props[TG_PROP_VELOCITY * prop_stride + d];
             if (vl > 0) qds[d] = qds[d] > vl ? vl : (qds[d] < -vl ? -vl : qds[d]);
-            qd[d] = qds[d];
-            q[d] += h * qd[d];
+            if (vl > 0) qdv[d] = qdv[d] > vl ? vl : (qdv[d] < -vl ? -vl : qdv[d]);
+            qd[d] = qdv[d];
+            q[d] += h * qds[d];
         }
         if (!sp->fix_base) {
             memcpy(v0, v0s, sizeof v0);
@@ -924,7 +960,9 @@ void oracle_physics_step_env(const tg_model_desc *m, const tg_sim_params *sp, fl
             qn = sqrt(quat[0] * quat[0] + quat[1] * quat[1] + quat[2] * quat[2] + quat[3] * quat[3]);
             for (int k = 0; k < 4; ++k) quat[k] /= qn;
             quat_to_m3(quat, R);
-            /* re-express the world-fixed velocity in the rotated body frame: v <- Rot(dq)^T v */
+            /* the stored (bias-free) velocity, re-expressed in the rotated body
+             * frame as a world-fixed vector: v <- Rot(dq)^T v */
+            memcpy(v0, v0v, sizeof v0);
             M3 Rd;
             quat_to_m3(dq, Rd);
             V3 wv = {v0[0], v0[1], v0[2]}, vv = {v0[3], v0[4], v0[5]};

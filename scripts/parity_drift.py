@@ -14,6 +14,10 @@ and are compared with it step by step:
              shifted by 1e-6 (random signs)
   f32        the same oracle compiled with real = float (liboracle_f32.so)
 
+``--variants label=lib.so,...`` adds one GPU column per developer build of
+libtgsim (each run in its own process with TG_LIB_PATH; e.g. a build with
+-DTG_PRECISE_SINCOS or -fno-fast-math), to locate a GPU-specific drift.
+
 Per step: max and median over envs of |obs - obs_ref| and the number of envs
 whose reset flags have differed so far.  The "horizon" of a run is the first
 step whose max error exceeds 1e-3 (north_star tolerance).  If the GPU run's
@@ -140,9 +144,27 @@ def main():
     ap.add_argument("--seed", type=int, default=21)
     ap.add_argument("--no-gpu", action="store_true")
     ap.add_argument("--out", default="gpurun_out/drift")
+    ap.add_argument("--kinds", default=None, help="comma list of perturbed,f32,gpu (default: all)")
+    ap.add_argument("--label", default=None, help="name the gpu column gpu_<label>")
+    ap.add_argument("--variants", default="", help="label=path.so,... extra GPU columns, one process each")
     a = ap.parse_args()
-    kinds = ["perturbed", "f32"] + ([] if a.no_gpu else ["gpu"])
+    kinds = a.kinds.split(",") if a.kinds else ["perturbed", "f32"] + ([] if a.no_gpu else ["gpu"])
     out = run(a.workload, a.steps, a.envs, a.seed, kinds)
+    if a.label and "gpu" in out["runs"]:
+        out["runs"]["gpu_" + a.label] = out["runs"].pop("gpu")
+    for v in filter(None, a.variants.split(",")):
+        import subprocess
+        import tempfile
+        label, lib = v.split("=", 1)
+        with tempfile.TemporaryDirectory() as td:
+            env = dict(os.environ, TG_LIB_PATH=os.path.abspath(lib))
+            r = subprocess.run([sys.executable, os.path.abspath(__file__), a.workload, "--steps", str(a.steps),
+                                "--envs", str(a.envs), "--seed", str(a.seed), "--kinds", "gpu", "--label", label,
+                                "--out", td], env=env)
+            if r.returncode != 0:
+                raise SystemExit(f"variant {label} failed ({r.returncode})")
+            with open(os.path.join(td, f"drift_{a.workload}.json")) as f:
+                out["runs"].update(json.load(f)["runs"])
     os.makedirs(a.out, exist_ok=True)
     with open(os.path.join(a.out, f"drift_{a.workload}.json"), "w") as f:
         json.dump(out, f)

@@ -72,7 +72,8 @@ def _rank_rlgames(rank, world, port, out):
     real = tia.make
     tia.make = fake_make
     try:
-        create = rlgames.get_rlgames_env_creator(seed=42, task_config={"env": {"numEnvs": 8}}, task_name="Gogoro",
+        # the seed as train.py:80 hands it over (cfg.seed += LOCAL_RANK)
+        create = rlgames.get_rlgames_env_creator(seed=42 + rank, task_config={"env": {"numEnvs": 8}}, task_name="Gogoro",
                                                  sim_device="cuda:0", rl_device="cuda:0", multi_gpu=True)
         env = create()
     finally:
@@ -98,7 +99,8 @@ def test_two_rank_env_creator_and_episode_gather():
     for r in range(world):
         env, seen, g, again = out[r]
         assert env == "env"
-        # rank -> device (LOCAL_RANK) and a distinct Philox key per rank (train.py:81: seed + rank)
+        # rank -> device (LOCAL_RANK); the seed passes through unchanged (train.py:80
+        # offset it by LOCAL_RANK already), so each rank keys its own Philox streams
         assert seen["sim_device"] == seen["rl_device"] == f"cuda:{r}"
         assert seen["seed"] == 42 + r and seen["num_envs"] == 8
         # 4 episodes per rank, lengths 1..4; returns (r+1)*len; summed over both ranks

@@ -86,3 +86,37 @@ def test_gpu_walk_32768_envs_runs():
     torch.cuda.synchronize()
     assert torch.isfinite(obs["obs"]).all() and torch.isfinite(rew).all()
     assert obs["obs"].shape == (32768, env.num_obs)
+
+
+def test_gpu_rb_forces_survive_a_declined_fused_walk_step():
+    """apply_rigid_body_force_tensors, then tg_walk_step on a
+    heightfield.  There is no fused walk instantiation on terrain, so the
+    launcher declines (rc 1) and the call falls back to compose + step +
+    post.  The pending per-link forces must still be reduced and act on that
+    step: the result equals the separate calls (tg_walk_pre_physics +
+    tg_simulate + tg_walk_post_physics) with the same forces, and differs from
+    a step without them."""
+    _cuda()
+    import thormang_isaacgym_amd as tia
+    from thormang_isaacgym_amd.tasks.base.vec_task import VecTask
+    n = 64
+    envs = [tia.make(seed=5, task="ThormangWalk", num_envs=n, sim_device="cuda:0", rl_device="cuda:0")
+            for _ in range(3)]
+    for env in envs:   # a heightfield below the plane: flat-ground physics, the HF kernel
+        env.sim.set_heightfield(np.zeros((8, 8), np.float32), 1.0, 1.0, -4.0, -4.0, friction=1.0)
+    L = envs[0].sim.L
+    f = torch.zeros(n, L, 3, device="cuda:0")
+    f[:, 0, 0] = 400.0   # a push on the pelvis (link 0)
+    g = torch.Generator(device="cuda:0").manual_seed(2)
+    for _ in range(3):
+        a = (torch.rand(n, envs[0].num_dof, device="cuda:0", generator=g) * 2 - 1) * 0.2
+        envs[0].sim.apply_rigid_body_force_tensors(f.view(-1, 3).contiguous())
+        envs[0].step(a)
+        envs[1].sim.apply_rigid_body_force_tensors(f.view(-1, 3).contiguous())
+        VecTask.step(envs[1], a)
+        envs[2].step(a)
+    torch.cuda.synchronize()
+    r0, r1, r2 = (e.root_tensor.clone() for e in envs)
+    assert torch.isfinite(r0).all()
+    assert float((r0 - r1).abs().max()) < 1e-5, float((r0 - r1).abs().max())
+    assert float((r0[:, 7] - r2[:, 7]).abs().min()) > 1e-2   # the push acted

@@ -80,6 +80,86 @@ def test_gpu_task_kernels_replay_reference_steps():
     assert src.i == len(f["draw_kind"])
 
 
+def test_gpu_fused_step_replays_reference_steps():
+    """The golden fixture through the TIMED path: ``Gogoro.step`` ->
+    tg_gogoro_step, one launch of the step kernel with the pre-physics at its
+    start and the GogoroPost epilogue (masked resets with in-place seat
+    composites, observations, reward, noise, command resample), the recorded
+    draws injected through its draw arrays.  The recorded post-simulate
+    physics state is written into the sim before each step and the sim runs
+    with 0 substeps (tg_set_sim_params), so the kernel passes it through to
+    its epilogue.  Differences from the separate-call replay above, both the
+    step kernel's semantics: the root state makes a frame round trip through
+    the kernel (2e-6), and a locked dof of a non-reset env is stored at the
+    centre of its lock window (the simulated state), not the fixture's
+    synthetic value."""
+    _cuda()
+    from thormang_isaacgym_amd.abi import TG_PROP_DAMPING, TG_PROP_LOWER, TG_PROP_STIFFNESS, TG_PROP_UPPER
+    from thormang_isaacgym_amd.tasks.gogoro import Gogoro
+    from thormang_isaacgym_amd.tasks.gogoro_draws import RecordedDraws
+    from tests.golden.make_golden import gogoro_cfg
+
+    f = np.load(os.path.join(GOLDEN, "gogoro_steps.npz"))
+    n = int(f["n_envs"])
+    src = RecordedDraws(f["draw_kind"], f["draw_size"], f["draw_vals"])
+
+    class Fused(Gogoro):
+        draw_source = src
+        env_spacing = 0.0
+
+    cfg = gogoro_cfg(n, int(f["max_steps"]), int(f["freq"]))
+    cfg["sim"]["use_gpu_pipeline"] = True
+    env = Fused(cfg, "cuda:0", "cuda:0", -1, True, False, False)
+    assert not env._replays_physics()
+    sp = env.sim.get_sim_params()
+    sp.substeps = 0
+    env.sim.set_sim_params(sp)
+    assert src.i == int(f["init_n_draws_init"])
+    dni = env.dof_name_to_id
+    st = dni["steering_joint"]
+    seat = [dni["base_x"], dni["base_y"], dni["base_z"]]
+    D = env.num_dof
+    locked = np.asarray(env.sim.desc.arrays["dof_locked"], bool)
+    assert locked.sum() == 34 and (~locked).sum() == 5
+    n_reset = 0
+    for t in range(f["actions"].shape[0]):
+        env.root_tensor.copy_(torch.from_numpy(f["sim_root"][t]))
+        env.state_dof.copy_(torch.from_numpy(f["sim_dof"][t]))
+        was_reset = env.reset_buf.cpu().numpy().copy()   # the envs this step's epilogue resets
+        obs, rew, reset, extras = env.step(torch.from_numpy(f["actions"][t]).cuda())
+        assert src.i == int(f["draw_end"][t])
+        np.testing.assert_allclose(env.sim.dof_pos_target[:, st].cpu().numpy(), f["pos_target"][t][:, st], atol=1e-6)
+        np.testing.assert_array_equal(env.sim.dof_vel_target.cpu().numpy(), f["vel_target"][t])
+        np.testing.assert_array_equal(reset.cpu().numpy(), f["reset"][t], err_msg=f"step {t}")
+        np.testing.assert_array_equal(env.progress_buf.cpu().numpy(), f["progress"][t])
+        np.testing.assert_array_equal(extras["time_outs"].cpu().numpy(), f["time_outs"][t])
+        np.testing.assert_allclose(obs["obs"].cpu().numpy(), f["obs"][t], atol=2e-5, err_msg=f"step {t}")
+        np.testing.assert_allclose(rew.cpu().numpy(), f["rew"][t], atol=2e-5)
+        for k, a in (("curent_command", env.curent_command), ("action_history", env.action_history),
+                     ("yaw_command", env.yaw_command), ("curent_speed", env.curent_speed),
+                     ("steer_offsets", env.steer_offsets), ("imu_offsets", env.imu_offsets),
+                     ("speed_offset", env.curent_speed_offset), ("buffer_obs", env.buffer_obs),
+                     ("config_vector", env.config_vector)):
+            np.testing.assert_allclose(a.cpu().numpy(), f[k][t], atol=2e-5, err_msg=f"{k} step {t}")
+        np.testing.assert_allclose(env.root_tensor.cpu().numpy(), f["root_after"][t], atol=2e-6)
+        dof = env.state_dof.cpu().numpy().reshape(n, D, 2)
+        ref = f["dof_after"][t].reshape(n, D, 2)
+        props = env.sim.dof_props.cpu().numpy()
+        r = was_reset != 0
+        n_reset += int(r.sum())
+        np.testing.assert_array_equal(dof[r], ref[r])                       # reset envs: the reset pose
+        np.testing.assert_array_equal(dof[~r][:, ~locked], ref[~r][:, ~locked])   # active dofs pass through
+        centre = 0.5 * (props[TG_PROP_LOWER] + props[TG_PROP_UPPER])
+        np.testing.assert_allclose(dof[~r][:, locked, 0], centre[~r][:, locked], atol=1e-7)
+        np.testing.assert_array_equal(dof[~r][:, locked, 1], 0.0)
+        np.testing.assert_allclose(props[TG_PROP_DAMPING, :, st], f["steer_damping"][t], rtol=1e-6)
+        np.testing.assert_array_equal(props[TG_PROP_STIFFNESS, :, st], f["steer_stiffness"][t])
+        np.testing.assert_allclose(props[TG_PROP_LOWER][:, seat], f["seat_lower"][t], atol=1e-7)
+        np.testing.assert_allclose(props[TG_PROP_UPPER][:, seat], f["seat_upper"][t], atol=1e-7)
+    assert src.i == len(f["draw_kind"])
+    assert n_reset > 0
+
+
 def test_gpu_env_matches_oracle_env():
     """Task kernels + HIP articulation step vs CPU oracle env, identical draws.
     Tolerance 1e-3 on obs/reward (north_star), exact on reset/timeout."""
@@ -166,26 +246,20 @@ def test_gpu_gogoro_inplace_seat_composites_equal_a_full_compose():
 
 
 def test_gpu_gogoro_fused_step_matches_separate_calls():
-    """tg_gogoro_step (pre-physics and post-physics in the step kernel) against
+    """tg_gogoro_step (pre-physics and post-physics in the step kernel, reset
+    envs' seat composites updated in place by the epilogue) against
     tg_gogoro_pre_physics + tg_simulate + tg_gogoro_post_physics (the
-    VecTask.step sequence) with in-kernel Philox draws, resets included.  The
-    two paths run different instantiations of the fast-math step kernel (with
-    and without the epilogue), whose physics rounds differently in the last
-    bit (root state 4e-9 apart after the first step), and random steering
-    amplifies that; so the comparison is the north_star tolerance 1e-3 over 40
-    free-running steps, while resets and progress must be identical."""
+    VecTask.step sequence: separate post kernel, reset envs re-composed) with
+    in-kernel Philox draws, resets included.  The two paths run different
+    instantiations of the fast-math step kernel and form the reset composites
+    two ways (2e-6 apart, test above), and random steering amplifies that; so
+    the comparison is the north_star tolerance 1e-3 over 40 free-running
+    steps, while resets and progress must be identical."""
     _cuda()
     import thormang_isaacgym_amd as tia
     from thormang_isaacgym_amd.tasks.base.vec_task import VecTask
-    # TG_SEAT_RECOMPOSE: the fused step re-composes its reset envs like the
-    # separate calls do, so the physics is the same on both sides (the
-    # in-place seat update has its own test above)
-    os.environ["TG_SEAT_RECOMPOSE"] = "1"
-    try:
-        envs = [tia.make(seed=21, task="Gogoro", num_envs=512, sim_device="cuda:0", rl_device="cuda:0")
-                for _ in range(2)]
-    finally:
-        del os.environ["TG_SEAT_RECOMPOSE"]
+    envs = [tia.make(seed=21, task="Gogoro", num_envs=512, sim_device="cuda:0", rl_device="cuda:0")
+            for _ in range(2)]
     f, u = envs
     g = torch.Generator(device="cuda:0").manual_seed(9)
     n_reset = 0

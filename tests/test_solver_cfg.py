@@ -29,21 +29,23 @@ def test_gogoro_cfg_warns_on_each_unhonoured_key():
     with pytest.warns(SolverCfgWarning) as rec:
         sim_params_from_cfg(_cfg_sim())
     msg = " ".join(str(w.message) for w in rec)
-    for k in ("solver_type", "num_velocity_iterations", "contact_offset", "bounce_threshold_velocity"):
+    for k in ("solver_type", "contact_offset", "bounce_threshold_velocity"):
         assert k in msg, k
     # resource knobs and honoured keys are not reported
-    for k in ("num_threads", "num_subscenes", "max_gpu_contact_pairs", "num_position_iterations", "rest_offset",
-              "max_depenetration_velocity"):
+    for k in ("num_threads", "num_subscenes", "max_gpu_contact_pairs", "num_position_iterations",
+              "num_velocity_iterations", "rest_offset", "max_depenetration_velocity"):
         assert f"{k}:" not in msg, k
 
 
 def test_honoured_keys_do_not_warn():
-    physx = {"solver_type": 0, "num_position_iterations": 6, "num_velocity_iterations": 0, "rest_offset": 0.0,
+    physx = {"solver_type": 0, "num_position_iterations": 6, "num_velocity_iterations": 3, "rest_offset": 0.0,
              "max_depenetration_velocity": 1.0, "num_threads": 4, "use_gpu": True}
     with warnings.catch_warnings():
         warnings.simplefilter("error", SolverCfgWarning)
         sp = sim_params_from_cfg({"dt": 0.01, "physx": physx})
-    assert sp.contact_iterations == 6
+    assert sp.contact_iterations == 6 and sp.velocity_iterations == 3
+    # IsaacGym's default of one velocity iteration when the key is absent
+    assert sim_params_from_cfg({"dt": 0.01, "physx": {}}, warn=False).velocity_iterations == 1
 
 
 def test_unknown_key_is_reported():
@@ -72,9 +74,47 @@ def _drop_tilted_box(physx, steps=40):
 BASE = {"num_position_iterations": 8, "rest_offset": 0.0, "max_depenetration_velocity": 1.0}
 
 
-@pytest.mark.parametrize("key,value", [("num_position_iterations", 1), ("rest_offset", 0.01),
-                                       ("max_depenetration_velocity", 0.05)])
+@pytest.mark.parametrize("key,value", [("num_position_iterations", 1), ("num_velocity_iterations", 0),
+                                       ("rest_offset", 0.01), ("max_depenetration_velocity", 0.05)])
 def test_honoured_key_changes_the_result(key, value):
     a = _drop_tilted_box(BASE)
     b = _drop_tilted_box(dict(BASE, **{key: value}))
     assert np.abs(a - b).max() > 1e-5, (key, a, b)
+
+
+def _push_out(viters, steps=1):
+    """A box resting 4 mm INSIDE the ground: the biased sweeps push it out."""
+    m = pm.box_body(mu=0.8)
+    physx = {"num_position_iterations": 8, "num_velocity_iterations": viters, "rest_offset": 0.0,
+             "max_depenetration_velocity": 10.0}
+    sp = sim_params_from_cfg({"dt": 0.01, "substeps": 1, "gravity": [0, 0, 0], "physx": physx},
+                             dict(angular_damping=0.0, linear_damping=0.0, ground_friction=0.8, baumgarte=0.5), 1,
+                             warn=False)
+    desc = ModelDesc(m)
+    props = default_dof_props(m, 1)
+    root = np.zeros((1, 13), np.float32)
+    root[0, 2] = 0.05 - 0.004   # box half height 0.05 (kat_models.box_body) - 4 mm
+    root[0, 6] = 1.0
+    z0 = float(root[0, 2])
+    dof = np.zeros((0, 2), np.float32)
+    z = np.zeros((1, 0), np.float32)
+    for _ in range(steps):
+        physics_step(desc, sp, root, dof, props, z, z)
+    return z0, root[0].copy()
+
+
+def test_velocity_iterations_drop_the_push_out_from_the_stored_velocity():
+    """num_velocity_iterations (PhysX semantics, Gogoro.yaml:21): the position
+    still moves by the biased sweeps' push-out velocity, but the velocity the
+    step stores is the bias-free one -- the penetration is recovered without
+    leaving the box flying up.  Without velocity sweeps the push-out velocity
+    is stored."""
+    z0, r0 = _push_out(0)
+    z1, r1 = _push_out(16)
+    assert r0[2] > z0 + 1e-4 and abs(r1[2] - r0[2]) < 1e-7   # same push-out of the position
+    assert r0[9] > 0.05                                        # biased: push-out velocity stored
+    assert abs(r1[9]) < 1e-6 and np.abs(r1[10:13]).max() < 1e-6   # bias-free: nothing stored
+    # Gauss-Seidel: fewer sweeps remove the stored push-out only in part (the
+    # corner rows are solved one after another), monotonically
+    v = [abs(_push_out(k)[1][9]) for k in (1, 4, 8)]
+    assert r0[9] > v[0] > v[1] > v[2] > abs(r1[9])

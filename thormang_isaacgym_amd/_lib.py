@@ -37,6 +37,8 @@ SIGNATURES = {
     "tg_apply_rigid_body_force_tensors": [_VP, _VP, _VP, C.c_int32],
     "tg_set_heightfield": [_VP, _VP, C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float],
     "tg_simulate": [_VP],
+    "tg_get_sim_params": [_VP, C.POINTER(abi.tg_sim_params)],
+    "tg_set_sim_params": [_VP, C.POINTER(abi.tg_sim_params)],
     "tg_rigid_body_states": [_VP, _VP],
     "tg_sync": [_VP],
     "tg_philox4x32_10": [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)],
@@ -48,7 +50,7 @@ SIGNATURES = {
     "tg_compiled_model_hashes": [C.POINTER(C.c_uint64), C.c_int32],
     "tg_model_jit": [C.c_uint64, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p],
     "tg_gogoro_step": [_VP, C.POINTER(abi.tg_gogoro_params), C.POINTER(abi.tg_gogoro_buffers), _VP, C.c_int32,
-                       C.c_uint64, C.c_uint64],
+                       _VP, _VP, _VP, _VP, _VP, C.c_uint64, C.c_uint64],
     "tg_gogoro_pre_physics": [_VP, C.POINTER(abi.tg_gogoro_params), C.POINTER(abi.tg_gogoro_buffers), _VP, _VP,
                               C.c_uint64],
     "tg_gogoro_post_physics": [_VP, C.POINTER(abi.tg_gogoro_params), C.POINTER(abi.tg_gogoro_buffers), _VP, _VP,

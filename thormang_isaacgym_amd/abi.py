@@ -43,7 +43,8 @@ class tg_sim_params(C.Structure):
         ("linear_damping", C.c_float), ("angular_damping", C.c_float),
         ("max_depenetration_velocity", C.c_float), ("rest_offset", C.c_float), ("contact_margin", C.c_float),
         ("ground_friction", C.c_float), ("baumgarte", C.c_float), ("limit_stiffness", C.c_float),
-        ("limit_damping", C.c_float), ("contact_iterations", C.c_int32), ("fix_base", C.c_int32),
+        ("limit_damping", C.c_float), ("contact_iterations", C.c_int32),
+        ("velocity_iterations", C.c_int32), ("fix_base", C.c_int32),
         ("env_spacing", C.c_float), ("envs_per_row", C.c_int32),
     ]
 
@@ -222,7 +223,8 @@ PHYSX_RESOURCE_KEYS = frozenset({
     "num_threads", "num_subscenes", "use_gpu", "default_buffer_size_multiplier", "max_gpu_contact_pairs",
     "contact_collection"})
 #: physx keys honoured by the solver (DESIGN.md §4 "Solver cfg")
-PHYSX_HONOURED_KEYS = frozenset({"num_position_iterations", "rest_offset", "max_depenetration_velocity"})
+PHYSX_HONOURED_KEYS = frozenset({"num_position_iterations", "num_velocity_iterations", "rest_offset",
+                                 "max_depenetration_velocity"})
 
 
 class SolverCfgWarning(UserWarning):
@@ -232,10 +234,11 @@ class SolverCfgWarning(UserWarning):
 def unhonoured_physx_keys(physx: dict, asset_opts: dict | None = None) -> Dict[str, str]:
     """The ``sim.physx`` keys (``vec_task.py:470-482`` sets them on PhysX's
     params) that would change a PhysX result but not this solver's, each with
-    the reason.  ``solver_type`` 1 (TGS) and ``num_velocity_iterations``: the
-    contact solve is one velocity-level projected Gauss-Seidel with
-    ``num_position_iterations`` sweeps and a Baumgarte push-out capped by
-    ``max_depenetration_velocity`` -- no bias-free velocity sweeps;
+    the reason.  ``solver_type`` 1 (TGS): the contact solve is velocity-level
+    projected Gauss-Seidel -- ``num_position_iterations`` sweeps with a
+    Baumgarte push-out capped by ``max_depenetration_velocity``, then
+    ``num_velocity_iterations`` bias-free sweeps (PhysX's split, honoured) --
+    without TGS's per-sub-iteration integration of the bias;
     ``contact_offset``: contacts are speculative within the asset option
     ``contact_margin`` instead; ``bounce_threshold_velocity``: no restitution
     model (every material has restitution 0, as the reference sets none, so a
@@ -248,10 +251,6 @@ def unhonoured_physx_keys(physx: dict, asset_opts: dict | None = None) -> Dict[s
         if k == "solver_type":
             if int(v) == 1:
                 out[k] = "TGS requested; the contact solve is velocity-level projected Gauss-Seidel"
-        elif k == "num_velocity_iterations":
-            if int(v) > 0:
-                out[k] = (f"{int(v)} bias-free velocity sweeps requested; only the "
-                          "num_position_iterations sweeps (with push-out bias) are run")
         elif k == "contact_offset":
             out[k] = (f"{v} ignored; contacts are speculative within contact_margin "
                       f"{float(ao.get('contact_margin', 0.05))}")
@@ -266,8 +265,10 @@ def sim_params_from_cfg(cfg_sim: dict, asset_opts: dict | None = None, num_envs:
                         env_spacing: float = 1.0, warn: bool = True) -> tg_sim_params:
     """Map the reference cfg 'sim' block (vec_task.py:442-490) onto tg_sim_params.
 
-    ``num_position_iterations`` is the number of PGS sweeps per substep (an
-    asset option ``contact_iterations`` overrides it); the physx keys the
+    ``num_position_iterations`` is the number of biased PGS sweeps per substep
+    (an asset option ``contact_iterations`` overrides it),
+    ``num_velocity_iterations`` the bias-free sweeps after them (asset option
+    ``velocity_iterations``); the physx keys the
     solver does not reproduce raise one ``SolverCfgWarning`` naming each
     (``unhonoured_physx_keys``)."""
     import warnings
@@ -292,6 +293,8 @@ def sim_params_from_cfg(cfg_sim: dict, asset_opts: dict | None = None, num_envs:
     sp.limit_stiffness = float(ao.get("limit_stiffness", 1.0))
     sp.limit_damping = float(ao.get("limit_damping", 1.0))
     sp.contact_iterations = int(ao.get("contact_iterations", max(1, int(physx.get("num_position_iterations", 4)))))
+    # IsaacGym's default num_velocity_iterations is 1; an asset option overrides it
+    sp.velocity_iterations = int(ao.get("velocity_iterations", max(0, int(physx.get("num_velocity_iterations", 1)))))
     sp.fix_base = int(bool(ao.get("fix_base_link", False)))
     sp.env_spacing = float(env_spacing)
     sp.envs_per_row = max(1, int(math.sqrt(num_envs)))

@@ -124,8 +124,14 @@ __device__ __forceinline__ void gogoro_pre_values(const GogoroPre &g, int e, flo
     float c = g.curent_command[e] + da;
     c = c < -ms ? -ms : (c > ms ? ms : c);
     cmd = c;
-    const U4 u = philox(U4{(uint32_t)e, g.c_lo, g.c_hi, 0x50524531u}, g.k0, g.k1);
-    const float noise = g.noise_mean + gauss(u.x, u.y) * g.noise_std;
+    float r;
+    if (g.pre_draws) {
+        r = g.pre_draws[e];
+    } else {
+        const U4 u = philox(U4{(uint32_t)e, g.c_lo, g.c_hi, 0x50524531u}, g.k0, g.k1);
+        r = gauss(u.x, u.y);
+    }
+    const float noise = g.noise_mean + r * g.noise_std;
     tsteer = c + g.steer_offsets[e] + noise;
     vrear = g.curent_speed[e];
 }
@@ -758,7 +764,7 @@ __device__ __forceinline__ void rb_force_env(const float *root, const float *dof
             }
             if (hg && M::jtype[g] == TG_JOINT_REVOLUTE) {   // Rpc Rz(q), as step pass 1a
                 float sq, cq;
-                __sincosf(qj, &sq, &cq);
+                tg_sincos(qj, &sq, &cq);
 #pragma unroll
                 for (int rr = 0; rr < 3; ++rr) {
                     const float c0 = Rpc.a[3 * rr], c1 = Rpc.a[3 * rr + 1];
@@ -863,7 +869,7 @@ __device__ __forceinline__ void rb_force_env(const float *root, const float *dof
                         }
                         if (M::jtype[g] == TG_JOINT_REVOLUTE) {   // Rpc Rz(q), as step pass 1a
                             float sq, cq;
-                            __sincosf(q[2 * M::gdof[g]], &sq, &cq);
+                            tg_sincos(q[2 * M::gdof[g]], &sq, &cq);
 #pragma unroll
                             for (int rr = 0; rr < 3; ++rr) {
                                 const float c0 = Rpc.a[3 * rr], c1 = Rpc.a[3 * rr + 1];
@@ -1464,7 +1470,21 @@ struct GogoroPost {
         for (int k = 0; k < TG_GOGORO_RESET_DRAWS; ++k) r[k] = slot(GOGORO_RSLOT[k]);
 #pragma unroll
         for (int k = 0; k < 5; ++k) nd[k] = slot(GOGORO_NSLOT[k]);
-        const float su = v8[0], yu = v8[1];
+        float su = v8[0], yu = v8[1];
+        // replayed draws (parity tests: the reference's recorded stream) in
+        // place of the Philox values, the same arithmetic after this point
+        if (pa.reset_draws && rflag) {
+#pragma unroll
+            for (int k = 0; k < TG_GOGORO_RESET_DRAWS; ++k) r[k] = pa.reset_draws[(size_t)e * TG_GOGORO_RESET_DRAWS + k];
+        }
+        if (pa.obs_draws) {
+#pragma unroll
+            for (int k = 0; k < 5; ++k) nd[k] = pa.obs_draws[(size_t)e * 5 + k];
+        }
+        if (pa.speed_draws) {
+            su = pa.speed_draws[e];
+            yu = pa.yaw_draws[e];
+        }
         int64_t prog = prog1;
         if (rflag) {
             // reset_env: dof rows (every lane), the rest on the lead lane

@@ -749,7 +749,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                 V3 tr = v3(ck[9], ck[10], ck[11]);
                 if (jt == TG_JOINT_REVOLUTE) {   // Rpc * Rz(q)
                     float sq, cq;
-                    __sincosf(qg, &sq, &cq);
+                    tg_sincos(qg, &sq, &cq);
 #pragma unroll
                     for (int r = 0; r < 3; ++r) {
                         const float c0 = Rpc.a[3 * r], c1 = Rpc.a[3 * r + 1];
@@ -1149,7 +1149,12 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         TG_PROF(3)
 
         // ---- contacts
+        SV v0v = v0s;   // the stored root velocity (bias-free with velocity iterations)
         if constexpr (M::NS > 0) {
+            // velocity iterations (sim.physx.num_velocity_iterations): the
+            // positions integrate the biased sweeps' velocity (F_QDS, v0s),
+            // the stored velocity is the bias-free one (F_QD, v0v)
+            const bool vit = a.viters > 0;
             // contact-group world poses and free velocities (one lane per contact group)
             for (int c = sub; c < M::NCG; c += LPE) {
                 // the group and its path (groups, joint types) selected from the
@@ -1411,8 +1416,9 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
 #pragma unroll
                     for (int jj = 0; jj < JL; ++jj) rv[jj] += wr[jj][i] * d;
                 };
+                auto sweeps = [&](int n_it) {
 #pragma unroll 1
-                for (int it = 0; it < a.iters; ++it) {
+                for (int it = 0; it < n_it; ++it) {
 #pragma unroll
                     for (int sh = 0; sh < M::NS; ++sh) {
                         const int rb = row_base<M>(sh), nr = M::shape_nrows[sh];
@@ -1442,6 +1448,20 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                         const float lim3 = mu * Nsum * reff;
                         set_lam(f + 2, fminf(fmaxf(lam[f + 2] - row_v(f + 2) / wd[f + 2], -lim3), lim3));
                     }
+                }
+                };
+                sweeps(a.iters);   // position iterations: push-out bias in the normal targets
+                if (vit) {
+                    // velocity iterations (PhysX): the biased multipliers park in the
+                    // dead Delassus slots (W is in registers now), the normal targets
+                    // lose the push-out (min(target, 0)), and the sweeps continue
+                    if (lead) {
+#pragma unroll
+                        for (int i = 0; i < K; ++i) s(PL::W + i) = lam[i];
+                    }
+#pragma unroll
+                    for (int i = 0; i < K; ++i) tg[i] = fminf(tg[i], 0.f);
+                    sweeps(a.viters);
                 }
                 if (lead) {
 #pragma unroll
@@ -1484,8 +1504,9 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                     for (int jj = 0; jj < JL; ++jj)
                         if (sub + LPE * jj == i) my[jj] = v;
                 };
+                auto sweeps = [&](int n_it) {
 #pragma unroll 1
-                for (int it = 0; it < a.iters; ++it) {
+                for (int it = 0; it < n_it; ++it) {
 #pragma unroll
                     for (int sh = 0; sh < M::NS; ++sh) {
                         const int rb = row_base<M>(sh), nr = M::shape_nrows[sh];
@@ -1519,6 +1540,17 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                         set_lam(f + 2, fminf(fmaxf(lam[f + 2], -lim3), lim3));
                     }
                 }
+                };
+                sweeps(a.iters);   // position iterations (biased), then the bias-free velocity iterations
+                if (vit) {
+                    if (lead) {
+#pragma unroll
+                        for (int i = 0; i < K; ++i) s(PL::W + i) = lam[i];   // the biased multipliers
+                    }
+#pragma unroll
+                    for (int i = 0; i < K; ++i) tg[i] = fminf(tg[i], 0.f);
+                    sweeps(a.viters);
+                }
                 if (lead) {
 #pragma unroll
                     for (int i = 0; i < K; ++i) s(PL::LAM + i) = lam[i];
@@ -1526,109 +1558,174 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
             }
             }
             TG_SYNC();
-            SV da0 = sv0();
+            SV da0 = sv0(), da0v = sv0();
             if constexpr (SUPER) {
                 TG_PROF(6)
                 // joint impulses u_g = sum_j lam_j du_j on the contact paths (0 elsewhere),
-                // one contact group at a time (paths may share ancestors)
-                for (int g = sub; g < M::NG; g += LPE) s(g * GF + F_UU) = 0.f;
+                // one contact group at a time (paths may share ancestors); with
+                // velocity iterations also u_v (F_C1, dead after pass 2b) from
+                // the bias-free multipliers, the biased ones parked at PL::W
+                const int LP = vit ? PL::W : PL::LAM;
+                for (int g = sub; g < M::NG; g += LPE) {
+                    s(g * GF + F_UU) = 0.f;
+                    if (vit) s(g * GF + F_C1) = 0.f;
+                }
                 TG_SYNC();
 #pragma unroll
                 for (int c = 0; c < M::NCG; ++c) {
                     for (int i = sub; i < M::cpath_len[c]; i += LPE) {
-                        float acc = 0.f;
+                        float acc = 0.f, accv = 0.f;
 #pragma unroll
                         for (int j = 0; j < K; ++j)
-                            if (M::shape_cg[row_shape<M>(j)] == c) acc += s(PL::LAM + j) * s(scr(j * SW + i));
-                        s(bounded(cpath[c * M::MAXD + i], -1, M::NG) * GF + F_UU) += acc;
+                            if (M::shape_cg[row_shape<M>(j)] == c) {
+                                const float du = s(scr(j * SW + i));
+                                acc += s(LP + j) * du;
+                                accv += s(PL::LAM + j) * du;
+                            }
+                        const int o = bounded(cpath[c * M::MAXD + i], -1, M::NG) * GF;
+                        s(o + F_UU) += acc;
+                        if (vit) s(o + F_C1) += accv;
                     }
                     TG_SYNC();
                 }
                 if (!fix_base) {
-                    float d6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                    float d6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, v6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                     for (int j = 0; j < K; ++j) {
-                        const float l = s(PL::LAM + j);
+                        const float l = s(LP + j), lv = s(PL::LAM + j);
 #pragma unroll
-                        for (int k = 0; k < 6; ++k) d6[k] += l * s(scr(j * SW + M::MAXD + k));
+                        for (int k = 0; k < 6; ++k) {
+                            const float aj = s(scr(j * SW + M::MAXD + k));
+                            d6[k] += l * aj;
+                            v6[k] += lv * aj;
+                        }
                     }
                     da0 = SV{v3(d6[0], d6[1], d6[2]), v3(d6[3], d6[4], d6[5])};
-                }
-            } else {
-                if (lead) {
-                    // impulses into the contact groups' F_PA slots (p = -f convention)
-                    for (int i = 0; i < K; ++i) {
-                        const int g = M::shape_group[row_shape<M>(i)];
-                        stsv(s, g * GF + F_PA, ldsv(s, g * GF + F_PA) + (-1.0f) * rforce(i, s(PL::LAM + i)));
-                    }
+                    da0v = SV{v3(v6[0], v6[1], v6[2]), v3(v6[3], v6[4], v6[5])};
                 }
                 TG_SYNC();
-                TG_PROF(6)
-                // impulse application: bottom-up gather, root solve, top-down
-#pragma unroll 1
-                for (int t = M::NSTEP - 1; t >= 0; --t) {
-                    const I4 dc = dsc(t);
+                if (lead) {
+                    stsv(s, F_PA, da0);
+                    stsv(s, F_V, da0v);   // (the root's F_V: dead after pass 1)
+                }
+                TG_SYNC();
+                // top-down, fully unrolled, own-group inputs one step ahead (as in
+                // pass 3); with velocity iterations the bias-free response rides
+                // along (F_V accelerations, F_QD the stored velocity)
+                struct OwnI { SV U, S; float uu, uv, dinv, qds; };
+                auto ld_own = [&](const I4 &dc) {
+                    const int g = max(dc.x, 0), o = g * GF;
+                    return OwnI{ldsv(s, o + F_U), ldS(s, g, d_jt(dc)), s(o + F_UU), s(o + F_C1), s(o + F_DINV),
+                                s(o + F_QDS)};
+                };
+                I4 dr[2];
+                OwnI ow[2];
+                dr[0] = dsc(0);
+                ow[0] = ld_own(dr[0]);
+#pragma unroll
+                for (int t = 0; t < M::NSTEP; ++t) {
+                    const I4 dc = dr[t % 2];
+                    const OwnI &w = ow[t % 2];
                     const int g = dc.x;
+                    const int op = max(dc.y, 0) * GF;
+                    const SV ap = ldsv(s, op + F_PA);
+                    const SV av = vit ? ldsv(s, op + F_V) : sv0();
+                    if (t + 1 < M::NSTEP) {
+                        dr[(t + 1) % 2] = dsc(t + 1);
+                        ow[(t + 1) % 2] = ld_own(dr[(t + 1) % 2]);
+                    }
                     if (g > 0) {
                         const int o = g * GF;
-                        SV p = ldsv(s, o + F_PA);
-                        for (int c = 0; c < d_nch(dc); ++c) p = p + ldsv(s, d_child(dc, c) * GF + F_PA);
-                        const float u = -dot(ldS(s, g, d_jt(dc)), p);
-                        s(o + F_UU) = u;
-                        stsv(s, o + F_PA, p + (u * s(o + F_DINV)) * ldsv(s, o + F_U));
+                        const float x = (w.uu - dot(w.U, ap)) * w.dinv;
+                        stsv(s, o + F_PA, ap + x * w.S);
+                        s(o + F_QDS) = w.qds + x;
+                        if (vit) {
+                            const float xv = (w.uv - dot(w.U, av)) * w.dinv;
+                            stsv(s, o + F_V, av + xv * w.S);
+                            s(o + F_QD) = w.qds + xv;
+                        }
                     }
                     TG_SYNC();
                 }
-                SV p0 = ldsv(s, F_PA);
-                for (int c = 0; c < M::nchild[0]; ++c) p0 = p0 + ldsv(s, M::child[0][c] * GF + F_PA);
-                if (!fix_base) da0 = ldl6_solve(rootf, -1.0f * p0);
-            }
-            TG_SYNC();
-            if (lead) stsv(s, F_PA, da0);
-            TG_SYNC();
-            {
-            // fully unrolled, own-group inputs one step ahead (as in pass 3)
-            struct OwnI { SV U, S; float uu, dinv, qds; };
-            auto ld_own = [&](const I4 &dc) {
-                const int g = max(dc.x, 0), o = g * GF;
-                return OwnI{ldsv(s, o + F_U), ldS(s, g, d_jt(dc)), s(o + F_UU), s(o + F_DINV), s(o + F_QDS)};
-            };
-            I4 dr[2];
-            OwnI ow[2];
-            dr[0] = dsc(0);
-            ow[0] = ld_own(dr[0]);
-#pragma unroll
-            for (int t = 0; t < M::NSTEP; ++t) {
-                const I4 dc = dr[t % 2];
-                const OwnI &w = ow[t % 2];
-                const int g = dc.x;
-                const SV ap = ldsv(s, max(dc.y, 0) * GF + F_PA);
-                if (t + 1 < M::NSTEP) {
-                    dr[(t + 1) % 2] = dsc(t + 1);
-                    ow[(t + 1) % 2] = ld_own(dr[(t + 1) % 2]);
+            } else {
+                // bottom-up gather, root solve, top-down -- once per multiplier
+                // set: with velocity iterations first the bias-free one (its
+                // joint velocities to F_QD, F_QDS untouched), then the biased one
+                for (int pass = vit ? 0 : 1; pass < 2; ++pass) {
+                    const int LS = (pass == 1 && vit) ? PL::W : PL::LAM;
+                    if (pass == 1 && vit) {   // the accumulators again
+                        for (int g = sub; g < M::NG; g += LPE) stsv(s, g * GF + F_PA, sv0());
+                        TG_SYNC();
+                    }
+                    if (lead) {
+                        // impulses into the contact groups' F_PA slots (p = -f convention)
+                        for (int i = 0; i < K; ++i) {
+                            const int g = M::shape_group[row_shape<M>(i)];
+                            stsv(s, g * GF + F_PA, ldsv(s, g * GF + F_PA) + (-1.0f) * rforce(i, s(LS + i)));
+                        }
+                    }
+                    TG_SYNC();
+                    TG_PROF(6)
+#pragma unroll 1
+                    for (int t = M::NSTEP - 1; t >= 0; --t) {
+                        const I4 dc = dsc(t);
+                        const int g = dc.x;
+                        if (g > 0) {
+                            const int o = g * GF;
+                            SV p = ldsv(s, o + F_PA);
+                            for (int c = 0; c < d_nch(dc); ++c) p = p + ldsv(s, d_child(dc, c) * GF + F_PA);
+                            const float u = -dot(ldS(s, g, d_jt(dc)), p);
+                            s(o + F_UU) = u;
+                            stsv(s, o + F_PA, p + (u * s(o + F_DINV)) * ldsv(s, o + F_U));
+                        }
+                        TG_SYNC();
+                    }
+                    SV p0 = ldsv(s, F_PA);
+                    for (int c = 0; c < M::nchild[0]; ++c) p0 = p0 + ldsv(s, M::child[0][c] * GF + F_PA);
+                    SV d0 = sv0();
+                    if (!fix_base) d0 = ldl6_solve(rootf, -1.0f * p0);
+                    TG_SYNC();
+                    if (lead) stsv(s, F_PA, d0);
+                    TG_SYNC();
+#pragma unroll 1
+                    for (int t = 0; t < M::NSTEP; ++t) {
+                        const I4 dc = dsc(t);
+                        const int g = dc.x;
+                        const SV ap = ldsv(s, max(dc.y, 0) * GF + F_PA);
+                        if (g > 0) {
+                            const int o = g * GF;
+                            const float x = (s(o + F_UU) - dot(ldsv(s, o + F_U), ap)) * s(o + F_DINV);
+                            stsv(s, o + F_PA, ap + x * ldS(s, g, d_jt(dc)));
+                            s(o + (pass == 0 ? F_QD : F_QDS)) = s(o + F_QDS) + x;
+                        }
+                        TG_SYNC();
+                    }
+                    if (pass == 0) da0v = d0;
+                    else da0 = d0;
                 }
-                if (g > 0) {
-                    const int o = g * GF;
-                    const float x = (w.uu - dot(w.U, ap)) * w.dinv;
-                    stsv(s, o + F_PA, ap + x * w.S);
-                    s(o + F_QDS) = w.qds + x;
-                }
-                TG_SYNC();
             }
+            if (!fix_base) {
+                v0v = v0s + (vit ? da0v : da0);
+                v0s = v0s + da0;
             }
-            if (!fix_base) v0s = v0s + da0;
             TG_PROF(7)
         }
-        // ---- velocity limits + integration
+        // ---- velocity limits + integration: the positions with the biased
+        // sweeps' velocity (F_QDS, v0s), the stored velocity the bias-free one
+        // (F_QD, v0v) when velocity iterations ran
+        const bool vst = M::NS > 0 && a.viters > 0;
 #pragma unroll
         for (int r = 0; r < (M::NG + LPE - 1) / LPE; ++r) {
             const int g = 1 + sub + r * LPE;
             if (g >= M::NG) break;
             const int o = g * GF;
             const float vl = vlim[r];
-            float x = s(o + F_QDS);
-            if (vl > 0.f) x = fminf(fmaxf(x, -vl), vl);
-            s(o + F_QD) = x;
+            float x = s(o + F_QDS), xv = vst ? s(o + F_QD) : x;
+            if (vl > 0.f) {
+                x = fminf(fmaxf(x, -vl), vl);
+                xv = fminf(fmaxf(xv, -vl), vl);
+            }
+            s(o + F_QD) = xv;
             s(o + F_Q) += h * x;
         }
         if (!fix_base) {
@@ -1643,6 +1740,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                 const float kk = sa / wn;
                 dx = v0.w.x * kk; dy = v0.w.y * kk; dz = v0.w.z * kk; dw = ca;
             }
+            v0 = v0v;
             const float nx = qw * dx + qx * dw + qy * dz - qz * dy;
             const float ny = qw * dy - qx * dz + qy * dw + qz * dx;
             const float nz = qw * dz + qx * dy - qy * dx + qz * dw;

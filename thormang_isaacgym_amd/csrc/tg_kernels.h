@@ -21,6 +21,7 @@ struct GogoroPre {
     const float *actions;     // [N] (null: none)
     float *action_history, *curent_command, *pos_target, *vel_target;
     const float *steer_offsets, *curent_speed;
+    const float *pre_draws;   // [N] replayed steering-noise N(0,1) draws, or null (Philox)
     float clip_actions, max_steering_change, max_steering, noise_mean, noise_std;
     int dof_steer, dof_rear;
     uint32_t k0, k1, c_lo, c_hi;
@@ -57,7 +58,7 @@ struct StepArgs {
     int substeps;
     float gx, gy, gz;
     float lin_damp, ang_damp, max_depen, rest, margin, ground_mu, baumgarte, lim_k, lim_c;
-    int iters, fix_base;
+    int iters, viters, fix_base;   // biased (position) and bias-free (velocity) PGS sweeps
     float *root;              // [N,13]
     float *dof;               // [N*D,2]
     const float *pos_tgt;     // [N,D]
@@ -122,6 +123,8 @@ struct GogoroPostArgs {
     uint32_t c_lo, c_hi;
     int *reset_list, *reset_count;   // [N] ids of the envs reset (and made dirty) / their count, or null
     int tl_inplace;                  // the epilogue updates a reset env's composite itself (M::NTL > 0)
+    // replayed draws (include/tg_gogoro.h layouts), each null for Philox
+    const float *reset_draws, *obs_draws, *speed_draws, *yaw_draws;
 };
 #ifndef __HIPCC_RTC__   // host launchers (not part of a hipRTC unit, jit.cpp)
 // compose + step kernel with the Gogoro post-physics fused in; returns 1 when

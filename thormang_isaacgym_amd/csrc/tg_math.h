@@ -42,10 +42,20 @@ __device__ __forceinline__ M3 mul(const M3 &x, const M3 &y) {
 __device__ __forceinline__ M3 transpose(const M3 &m) {
     return M3{{m.a[0], m.a[3], m.a[6], m.a[1], m.a[4], m.a[7], m.a[2], m.a[5], m.a[8]}};
 }
+// sine and cosine of a joint angle: the hardware approximation (v_sin /
+// v_cos on the angle in revolutions), or with TG_PRECISE_SINCOS (developer
+// build, the drift study scripts/parity_drift.py --variants) the libm one
+__device__ __forceinline__ void tg_sincos(float x, float *s, float *c) {
+#ifdef TG_PRECISE_SINCOS
+    sincosf(x, s, c);
+#else
+    __sincosf(x, s, c);
+#endif
+}
 // rotation about a unit axis (Rodrigues); axis components are usually compile-time constants
 __device__ __forceinline__ M3 rot_axis(float x, float y, float z, float q) {
     float s, c;
-    __sincosf(q, &s, &c);
+    tg_sincos(q, &s, &c);
     float t = 1.0f - c;
     return M3{{t * x * x + c, t * x * y - s * z, t * x * z + s * y, t * x * y + s * z, t * y * y + c, t * y * z - s * x,
                t * x * z - s * y, t * y * z + s * x, t * z * z + c}};

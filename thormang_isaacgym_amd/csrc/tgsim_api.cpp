@@ -149,7 +149,7 @@ tg::StepArgs step_args(tg_sim *s) {
     const tg_sim_params &p = s->params;
     a.N = s->N;
     a.D = s->D;
-    a.h = p.dt / (float)p.substeps;
+    a.h = p.substeps > 0 ? p.dt / (float)p.substeps : 0.f;   // (0 substeps: tg_set_sim_params replay mode)
     a.substeps = p.substeps;
     a.gx = s->gravity[0]; a.gy = s->gravity[1]; a.gz = s->gravity[2];
     a.lin_damp = p.linear_damping;
@@ -162,6 +162,7 @@ tg::StepArgs step_args(tg_sim *s) {
     a.lim_k = p.limit_stiffness;
     a.lim_c = p.limit_damping;
     a.iters = p.contact_iterations;
+    a.viters = p.velocity_iterations;
     a.fix_base = p.fix_base;
     a.root = s->root;
     a.dof = s->dof;
@@ -209,7 +210,8 @@ int tg_sim_create(const tg_model_desc *m, const tg_sim_params *params, int32_t n
     *out = nullptr;
     if (num_envs <= 0) return fail(TG_ERR_ARG, "num_envs must be positive (got %d)", num_envs);
     if (params->substeps <= 0 || !(params->dt > 0.f)) return fail(TG_ERR_ARG, "dt and substeps must be positive");
-    if (params->contact_iterations < 0) return fail(TG_ERR_ARG, "contact_iterations must be >= 0");
+    if (params->contact_iterations < 0 || params->velocity_iterations < 0)
+        return fail(TG_ERR_ARG, "contact / velocity iterations must be >= 0");
     int kc = tg::model_kc(m->model_hash);
     if (kc < 0)
         return fail(TG_ERR_MODEL,
@@ -406,10 +408,10 @@ int tg_set_dof_properties_indexed(tg_sim *s, int32_t field, const float *vals, c
     if (field < 0 || field >= TG_NUM_PROPS) return fail(TG_ERR_ARG, "unknown dof property field %d", field);
     if (!vals) return fail(TG_ERR_ARG, "null property values");
     float *dst = s->props + (size_t)field * s->N * s->D;
-    if (vals != dst)
-        win_touch(s);
-        if (int rc = tg::launch_scatter_field(dst, vals, ids, n, s->D, s->stream)) return fail(rc, "scatter failed");
     win_touch(s);
+    if (vals != dst) {   // (writes through the zero-copy props view need no copy)
+        if (int rc = tg::launch_scatter_field(dst, vals, ids, n, s->D, s->stream)) return fail(rc, "scatter failed");
+    }
     if (int rc = tg::launch_mark_dirty(s->dirty, ids, n, s->stream)) return fail(rc, "mark dirty failed");
     return TG_OK;
 }
@@ -517,9 +519,13 @@ static int simulate_args(tg_sim *s, const tg::StepArgs &a_in, const tg::WalkPost
         a.clist = s->clist + (size_t)prev * s->N;
         a.ccount = s->ccount + prev;
     }
-    bool rb_launch = false;
+    bool rb_launch = false, rb_in_compose = false;
     if (s->rbf_pending) {   // the pending per-link forces: in the full compose launch, else on their own
         if (!a.skip_compose && !a.compose_list) {
+            // reduced by the compose launch below: still pending until that
+            // launch went through (a fused launcher may decline the call,
+            // rc 1, and the caller's fallback simulate must reduce them then)
+            rb_in_compose = true;
             a.rbf_forces = s->rbf_f;
             a.rbf_torques = s->rbf_t;
             a.rbf_space = s->rbf_space;
@@ -529,8 +535,8 @@ static int simulate_args(tg_sim *s, const tg::StepArgs &a_in, const tg::WalkPost
             if (int rc = tg::launch_rb_forces(s->hash, s->root, s->dof, s->comp, (int)s->N, s->mass_scale, s->rbf_f,
                                               s->rbf_t, s->rbf_space, s->force, s->props, s->stream))
                 return fail(rc, "rigid-body force launch failed");
+            s->rbf_pending = false;   // s->force holds the reduced wrenches now
         }
-        s->rbf_pending = false;
     }
     std::pair<hipEvent_t, hipEvent_t> ev{nullptr, nullptr};
     const bool timed = s->timing > 0 && s->timing_count % s->timing == 0;
@@ -573,6 +579,7 @@ static int simulate_args(tg_sim *s, const tg::StepArgs &a_in, const tg::WalkPost
         if (rc == 1) return 1;   // not launched (no such instantiation): caller falls back
         return fail(rc, "step launch failed: %s", hipGetErrorString(hipGetLastError()));
     }
+    if (rb_in_compose) s->rbf_pending = false;
     if (s->timing > 0) s->timing_count++;
     if (ev.first) {
         s->ev_pending.push_back(ev);
@@ -602,6 +609,29 @@ static int simulate_args(tg_sim *s, const tg::StepArgs &a_in, const tg::WalkPost
             s->dirty_possible = true;
         }
     }
+    return TG_OK;
+}
+
+int tg_get_sim_params(tg_sim *s, tg_sim_params *out) {
+    if (int rc = check_sim(s)) return rc;
+    if (!out) return fail(TG_ERR_ARG, "tg_get_sim_params: null output");
+    *out = s->params;
+    memcpy(out->gravity, s->gravity, sizeof s->gravity);
+    return TG_OK;
+}
+
+int tg_set_sim_params(tg_sim *s, const tg_sim_params *p) {
+    if (int rc = check_sim(s)) return rc;
+    if (!p) return fail(TG_ERR_ARG, "tg_set_sim_params: null argument");
+    if (p->substeps < 0 || !(p->dt > 0.f)) return fail(TG_ERR_ARG, "dt must be positive and substeps >= 0");
+    if (p->contact_iterations < 0 || p->velocity_iterations < 0)
+        return fail(TG_ERR_ARG, "contact / velocity iterations must be >= 0");
+    const float spacing = s->params.env_spacing;
+    const int32_t per_row = s->params.envs_per_row;
+    s->params = *p;
+    s->params.env_spacing = spacing;   // the env grid is fixed at creation
+    s->params.envs_per_row = per_row;
+    memcpy(s->gravity, p->gravity, sizeof s->gravity);
     return TG_OK;
 }
 
@@ -735,11 +765,14 @@ int tg_gogoro_pre_physics(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_
 }
 
 int tg_gogoro_step(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_buffers *b, const float *actions,
-                   int32_t n_simulate, uint64_t counter_pre, uint64_t counter_post) {
+                   int32_t n_simulate, const float *pre_draws, const float *reset_draws, const float *obs_draws,
+                   const float *speed_draws, const float *yaw_draws, uint64_t counter_pre, uint64_t counter_post) {
     if (int rc = check_sim(s)) return rc;
     if (!p || !b || !actions) return fail(TG_ERR_ARG, "tg_gogoro_step: null argument");
     if (p->num_envs != s->N || p->num_dof != s->D) return fail(TG_ERR_ARG, "gogoro params do not match the sim");
     if (n_simulate < 1) return fail(TG_ERR_ARG, "tg_gogoro_step: n_simulate %d < 1", n_simulate);
+    if ((speed_draws == nullptr) != (yaw_draws == nullptr))
+        return fail(TG_ERR_ARG, "speed_draws and yaw_draws must both be given or both be NULL");
     for (int i = 0; i < n_simulate; ++i) {
         tg::StepArgs a = step_args(s);
         if (i == 0) {   // pre_physics_step fused into the first compose launch
@@ -751,6 +784,7 @@ int tg_gogoro_step(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_buffers
             g.vel_target = b->vel_target;
             g.steer_offsets = b->steer_offsets;
             g.curent_speed = b->curent_speed;
+            g.pre_draws = pre_draws;
             g.clip_actions = p->clip_actions;
             g.max_steering_change = p->max_steering_change;
             g.max_steering = p->max_steering;
@@ -769,7 +803,8 @@ int tg_gogoro_step(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_buffers
             const bool inplace = tg::model_tl(s->hash) > 0 && !s->no_inplace;
             const tg::GogoroPostArgs gp{*p, *b, (uint32_t)counter_post, (uint32_t)(counter_post >> 32),
                                         inplace ? nullptr : s->clist + (size_t)s->list_cur * s->N,
-                                        inplace ? nullptr : s->ccount + s->list_cur, inplace ? 1 : 0};
+                                        inplace ? nullptr : s->ccount + s->list_cur, inplace ? 1 : 0,
+                                        reset_draws, obs_draws, speed_draws, yaw_draws};
             // one launch: the pre-physics too runs in the step kernel
             a.gp_in_step = (n_simulate == 1 && !s->pre_in_compose) ? 1 : 0;
             const int rc = simulate_args(s, a, nullptr, &gp);
@@ -780,7 +815,8 @@ int tg_gogoro_step(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_buffers
         if (int rc = simulate_args(s, a)) return rc;
     }
     win_touch(s);
-    if (int rc = tg::launch_gogoro_post(*p, *b, nullptr, nullptr, nullptr, nullptr, counter_post, s->stream))
+    if (int rc = tg::launch_gogoro_post(*p, *b, reset_draws, obs_draws, speed_draws, yaw_draws, counter_post,
+                                        s->stream))
         return fail(rc, "launch failed");
     s->dirty_possible = true;   // the separate post kernel's resets mark envs dirty
     return TG_OK;
@@ -955,7 +991,9 @@ int tg_paper_step(tg_sim *s, const tg_paper_params *p, const tg_paper_buffers *b
             // in the step kernel itself when it is the only simulate and the
             // model's kernel has the pre-physics slots; else the compose prologue
             q.actions = actions;
-            a.pp_in_step = (n_simulate == 1 && (tg::model_fused(s->hash) & 6) && !s->pre_in_compose) ? 1 : 0;
+            // (FUSED bit 4: the bit the step kernel tests before it runs the
+            // paper pre-physics and forms the term-7 partials)
+            a.pp_in_step = (n_simulate == 1 && (tg::model_fused(s->hash) & 4) && !s->pre_in_compose) ? 1 : 0;
             // the step kernel also forms reward term 7's partials, so the post
             // launch finishes the batch itself (no finish launch)
             if (a.pp_in_step && !s->paper_finish_launch && p->num_envs % 8 == 0) {   // 8: PAPER_EPW

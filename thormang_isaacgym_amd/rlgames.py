@@ -37,15 +37,15 @@ def get_rlgames_env_creator(seed: int, task_config: dict, task_name: str, sim_de
     """train.py:99-122: a thunk creating the task env (torchrun rank -> device)."""
     def create_env(**kwargs):
         from . import make
-        dev_sim, dev_rl, env_seed = sim_device, rl_device, seed
+        dev_sim, dev_rl = sim_device, rl_device
         if multi_gpu:
-            # one process per GPU (torchrun): rank -> device, and a distinct
-            # stream per rank -- train.py:81 adds the global rank to the seed,
-            # and the seed keys the in-kernel Philox streams
+            # one process per GPU (torchrun): LOCAL_RANK -> device.  The seed is
+            # taken as given: the caller (train.py:80, cfg.seed += LOCAL_RANK)
+            # has already made it distinct per rank, and it keys the in-kernel
+            # Philox streams
             local = int(os.getenv("LOCAL_RANK", "0"))
             dev_sim = dev_rl = f"cuda:{local}"
-            env_seed = seed + int(os.getenv("RANK", "0"))
-        env = make(seed=env_seed, task=task_name, num_envs=task_config["env"]["numEnvs"], sim_device=dev_sim,
+        env = make(seed=seed, task=task_name, num_envs=task_config["env"]["numEnvs"], sim_device=dev_sim,
                    rl_device=dev_rl, graphics_device_id=graphics_device_id, headless=headless,
                    virtual_screen_capture=virtual_screen_capture, force_render=force_render, cfg=task_config)
         if post_create_hook is not None:

@@ -228,6 +228,19 @@ class Sim:
     def simulate(self):
         check(lib().tg_simulate(self._h), "simulate")
 
+    def get_sim_params(self) -> abi.tg_sim_params:
+        """gym.get_sim_params (vec_task.py:650): a copy of the live params."""
+        sp = abi.tg_sim_params()
+        check(lib().tg_get_sim_params(self._h, C.byref(sp)), "get_sim_params")
+        return sp
+
+    def set_sim_params(self, sp: abi.tg_sim_params):
+        """gym.set_sim_params (vec_task.py:660), effective from the next simulate
+        (substeps 0: simulate passes the state through, the recorded-physics replays)."""
+        check(lib().tg_set_sim_params(self._h, C.byref(sp)), "set_sim_params")
+        self.params = sp
+        self.gravity = [float(x) for x in sp.gravity]
+
     def acquire_rigid_body_state_tensor(self) -> torch.Tensor:
         """gym.acquire_rigid_body_state_tensor: [N*L, 13] world link states
         (origin pos, quat xyzw, com linvel, angvel), links in model order;

@@ -3,8 +3,10 @@
 Drop-in mirror of the reference's ``isaacgymenvs/tasks/gogoro_new.py``:
 same class name, constructor signature, cfg schema (cfg/task/Gogoro.yaml),
 attribute names, observation/action layout ([N,6] / [N,1]) and step
-semantics.  The per-step work runs in two fused HIP kernels plus the
-articulation step (libtgsim.so):
+semantics.  ``step`` is one library call, ``tg_gogoro_step``: one launch of
+the articulation step kernel with the pre-physics at its start and the
+post-physics as its epilogue (libtgsim.so).  The separate-call API the
+reference's method names map to stays available:
 
   pre_physics_step  (gogoro_new.py:347-369)  -> tg_gogoro_pre_physics
   gym.simulate      (vec_task.py:332-335)     -> tg_simulate
@@ -239,26 +241,42 @@ class Gogoro(VecTask):
         """Fused into post_physics_step (tg_gogoro_post_physics); kept for API parity."""
         raise NotImplementedError("compute_obs_rwd runs inside the fused post-physics kernel")
 
+    def _replays_physics(self) -> bool:
+        """A subclass that replaces ``simulate`` (a recorded-physics replay)
+        keeps the reference's call sequence pre -> simulate -> post."""
+        return type(self).simulate is not VecTask.simulate
+
     def step(self, actions):
         if self.dr_randomizations.get("actions", None) or self.dr_randomizations.get("observations", None):
             return super().step(actions)
-        if self.draw_source is None:
-            # pre_physics_step + control_freq_inv x simulate + post_physics_step in
-            # one library call (tg_gogoro_step: the pre-physics work rides in the
-            # first simulate's compose launch); same counters as the separate calls
-            a = actions.to(device=self.device, dtype=torch.float32).contiguous()
-            c_pre = self._counter()
-            c_post = self._counter()
-            check(lib().tg_gogoro_step(self.sim.handle, C.byref(self.params), C.byref(self._bufs), _p(a),
-                                       self.control_freq_inv, c_pre, c_post), "tg_gogoro_step")
-            self._keep = (a, None)
-            self.frame_count += self.control_freq_inv
-            self._post_host()
-        else:
+        if self._replays_physics():
             self.pre_physics_step(actions)
             for _ in range(self.control_freq_inv):
                 self.simulate()
             self.post_physics_step()
+        else:
+            # pre_physics_step + control_freq_inv x simulate + post_physics_step in
+            # one library call (tg_gogoro_step: with one simulate, one launch of
+            # the step kernel, the pre-physics at its start and the post-physics
+            # as its epilogue); the same counters as the separate calls, and with
+            # a draw_source the reference's draws in its call order (pre, then
+            # post: the resets are known before the step, reset_buf)
+            a = actions.to(device=self.device, dtype=torch.float32).contiguous()
+            draws = (None,) * 5
+            if self.draw_source is not None:
+                pre = self._dev(self.draw_source.normal(self.n_envs))
+                ids = self.reset_buf.nonzero(as_tuple=False).squeeze(-1).cpu().numpy()
+                post = post_draws(self.draw_source, ids, self.progress_buf.cpu().numpy(),
+                                  int(self.params.speed_freq_update), int(self.params.yaw_freq_update))
+                draws = (pre,) + tuple(self._dev(x) for x in post)
+            c_pre = self._counter()
+            c_post = self._counter()
+            check(lib().tg_gogoro_step(self.sim.handle, C.byref(self.params), C.byref(self._bufs), _p(a),
+                                       self.control_freq_inv, *[_p(d) for d in draws], c_pre, c_post),
+                  "tg_gogoro_step")
+            self._keep = (a, draws)
+            self.frame_count += self.control_freq_inv
+            self._post_host()
         self.extras["time_outs"] = self.timeout_buf
         self.obs_dict["obs"] = self.obs_buf
         if self.num_states > 0:
