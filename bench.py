@@ -23,8 +23,10 @@ algorithmic bytes per env-step
 HBM rate against the 8 TB/s MI355X peak.  ``traffic`` is the PMC-measured HBM
 bytes per launch of the same kernel from a committed rocprofv3 summary
 (scripts/gpu_profile.sh + scripts/pmc_summary.py) when one exists for this
-workload, else null.  cpu_baseline: the CPU oracle env (oracle/, fp64 physics +
-task restatement, OpenMP) on a bounded sample of the same workload, rank 0 only.
+workload, else null.  cpu_baseline: the CPU oracle env (oracle/: the same physics
++ task algorithm, OpenMP) on a bounded sample of the same workload, rank 0
+only: its fp32 build (the GPU's arithmetic type) as the value, the fp64 parity
+oracle beside it.
 """
 from __future__ import annotations
 
@@ -202,7 +204,12 @@ def committed_sq(task_name: str, num_envs: int):
     return None
 
 
-def cpu_baseline(task_name: str, num_envs: int, threads: int, terrain_env=None):
+def cpu_baseline(task_name: str, num_envs: int, threads: int, terrain_env=None, precision: str = "f32",
+                 seconds: float = 10.0):
+    """The oracle env (oracle/: the same physics and task algorithm) on the
+    host cores, bounded to ~``seconds``.  precision "f32" (real = float, the
+    GPU's arithmetic type: the fair comparator, reported as the baseline) or
+    "f64" (the parity oracle itself)."""
     from tests.gpu_harness import NumpyDraws, OracleGogoro, OracleWalk, parity_cfg, walk_cfg
     if terrain_env is not None:   # same heightfield and spawn heights as the GPU env
         from tests.oracle_lib import set_heightfield
@@ -211,24 +218,21 @@ def cpu_baseline(task_name: str, num_envs: int, threads: int, terrain_env=None):
         set_heightfield(t.heightsamples.cpu().numpy(), t.V_scale, t.H_scale, o, o, friction=0.98)
     if task_name == "Gogoro":
         spawn = None if terrain_env is None else terrain_env.root_reset_tensor[:, 2].cpu().numpy()
-        env = OracleGogoro(parity_cfg(num_envs), NumpyDraws(0), threads=threads, spawn_z=spawn)
+        env = OracleGogoro(parity_cfg(num_envs), NumpyDraws(0), threads=threads, spawn_z=spawn, precision=precision)
         shape = (num_envs,)
     else:
-        env = OracleWalk(walk_cfg(num_envs, task_name), NumpyDraws(0), threads=threads)
+        env = OracleWalk(walk_cfg(num_envs, task_name), NumpyDraws(0), threads=threads, precision=precision)
         shape = (num_envs, env.D)
     rs = np.random.default_rng(1234)
     steps = 0
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < 10.0 and steps < 400:
+    while time.perf_counter() - t0 < seconds and steps < 400:
         env.step(rs.uniform(-1, 1, shape).astype(np.float32))
         steps += 1
     dt = time.perf_counter() - t0
-    out = {"value": num_envs * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-           "sample": f"{task_name} {num_envs} envs x {steps} steps (oracle/ fp64 physics + C task restatement, "
-                     f"OpenMP {threads} threads) = {dt:.1f} s"}
-    if task_name == "Gogoro":
-        out["post_physics_only"] = post_physics_only(num_envs)
-    return out
+    return {"value": num_envs * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{task_name} {num_envs} envs x {steps} steps (oracle/ {precision} physics + C task "
+                      f"restatement, OpenMP {threads} threads) = {dt:.1f} s"}
 
 
 def post_physics_only(num_envs: int) -> dict:
@@ -276,9 +280,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    rccl_world = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group(backend="nccl", init_method="env://")
+        rccl_world = dist.get_world_size()   # what RCCL itself reports (the SCALE runs are checked on it)
+        if rccl_world != world:
+            raise RuntimeError(f"WORLD_SIZE {world} but the process group has {rccl_world} ranks")
     torch.cuda.set_device(local)
     dev = f"cuda:{local}"
 
@@ -355,6 +363,9 @@ def main():
                                f"dt {sim_cfg['dt']} s x "
                                f"{sim_cfg.get('substeps', 2)} substeps ({1.0 / sim_cfg['dt']:.1f} Hz control)",
                    "num_envs_per_gpu": N, "parallelism": f"env-dp{world}"},
+        "dist": {"backend": "nccl (RCCL)" if rccl_world else None, "world_size": rccl_world or 1,
+                 "collectives_in_timed_region": "barrier + max-over-ranks all_reduce of the elapsed time"
+                 if rccl_world else None},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "tg::step_par_kernel (one launch per simulate)", "kernel_ms": kern_ms,
@@ -375,8 +386,13 @@ def main():
     if not args.no_cpu_baseline and world == 1:
         try:
             info = host_cpu_info()
-            out["cpu_baseline"] = cpu_baseline(args.task, N, threads=baseline_threads(info),
-                                               terrain_env=env if args.terrain else None)
+            thr = baseline_threads(info)
+            tenv = env if args.terrain else None
+            out["cpu_baseline"] = cpu_baseline(args.task, N, threads=thr, terrain_env=tenv, precision="f32")
+            out["cpu_baseline"]["fp64_oracle"] = cpu_baseline(args.task, N, threads=thr, terrain_env=tenv,
+                                                              precision="f64", seconds=5.0)
+            if args.task == "Gogoro":
+                out["cpu_baseline"]["post_physics_only"] = post_physics_only(N)
             out["cpu_baseline"]["host"] = info
         except Exception as exc:  # baseline is reported, never the measured value
             out["cpu_baseline"] = {"value": None, "error": repr(exc)}

@@ -27,7 +27,12 @@ UNITS = {
     # physics: fast-math lets zero tree terms fold away in the specialised kernels
     # (SLP pairing into v_pk_* costs more register moves than it saves here:
     # Gogoro step 0.226 -> 0.128 ms without it, Thormang unchanged)
-    "articulation.hip": ["-O3", "-ffast-math", "-munsafe-fp-atomics", "-fno-slp-vectorize"],
+    # -ffp-contract=fast-honor-pragmas after -ffast-math: contraction stays on
+    # for the physics, but the fused task epilogues' `#pragma clang fp
+    # contract(off)` blocks (the reference's fp32 operation order) are honoured
+    # -- plain -ffast-math lets the backend fuse a*b+c there regardless
+    "articulation.hip": ["-O3", "-ffast-math", "-ffp-contract=fast-honor-pragmas", "-munsafe-fp-atomics",
+                         "-fno-slp-vectorize"],
     # task math must follow the reference's fp32 operation order
     "gogoro_task.hip": ["-O3", "-ffp-contract=off"],
     "walk_task.hip": ["-O3", "-ffp-contract=off"],

@@ -111,8 +111,8 @@ int compile(const std::string &src, const std::string &incdir, JitCode &out, std
     for (int k = 0; k < NK; ++k) hiprtcAddNameExpression(prog, KERNEL_EXPR[k]);
     const std::string inc = "-I" + incdir;
     // the flags of the compiled-in articulation unit (build_ext.py UNITS)
-    const char *opts[] = {"--offload-arch=gfx950", "-std=c++17", "-O3", "-ffast-math", "-munsafe-fp-atomics",
-                          "-fno-slp-vectorize", "-DTG_JIT=1", inc.c_str()};
+    const char *opts[] = {"--offload-arch=gfx950", "-std=c++17", "-O3", "-ffast-math",
+                          "-ffp-contract=fast-honor-pragmas", "-munsafe-fp-atomics", "-fno-slp-vectorize", "-DTG_JIT=1", inc.c_str()};
     const hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof opts / sizeof opts[0]), opts);
     if (rc != HIPRTC_SUCCESS) {
         size_t n = 0;

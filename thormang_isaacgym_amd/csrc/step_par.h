@@ -142,7 +142,8 @@ template <class M> struct ParLayout {
     static constexpr int T_CPATH = T_GI + M::NG * GIW;                 // [NCG][MAXD]
     // per (schedule step, lane) descriptor, one int4 (see step_desc)
     static constexpr int T_DESC = (T_CPATH + M::NCG * M::MAXD + 3) & ~3;
-    static constexpr int T_ZERO = T_DESC + 4 * M::NSTEP * M::LPE;     // 32 zero floats
+    static constexpr int T_PACK = T_DESC + 4 * M::NSTEP * M::LPE;     // PackTab words [NPW][LPE]
+    static constexpr int T_ZERO = T_PACK + (M::NSTEP + 1) / 2 * M::LPE;  // 32 zero floats (PackTab NPW)
     // GogoroPaper (FUSED bit 4): the envs' reward-term-7 partials
     static constexpr int T_T7 = T_ZERO + 32;
     static constexpr int T_TOTAL = T_T7 + ((M::FUSED & 4) ? M::EPB : 0);
@@ -218,6 +219,36 @@ template <class M> struct DescTab {
     }
     static constexpr Arr tab = make();
 };
+// The tree passes' (group, parent, joint type) of every schedule step of a
+// lane, packed 16 bits per step (g | jt == prismatic << 7 | parent << 8), two
+// steps per 32-bit word, held in registers for the whole launch: the forward
+// passes form their next step's LDS / HBM addresses with one bit-field
+// extract instead of a descriptor read from LDS, which sat behind the
+// previous step's stores in the in-order LDS queue (NG <= 128)
+template <class M> struct PackTab {
+    static constexpr bool ON = M::NG <= 128;
+    static constexpr int NPW = (M::NSTEP + 1) / 2;
+    struct Arr {
+        int v[NPW * M::LPE];
+    };
+    static constexpr Arr make() {
+        Arr a{};
+        for (int w = 0; w < NPW; ++w)
+            for (int lane = 0; lane < M::LPE; ++lane) {
+                int x = 0;
+                for (int k = 0; k < 2; ++k) {
+                    const int t = 2 * w + k;
+                    if (t >= M::NSTEP) break;
+                    const I4 d = step_desc<M>(t, lane);
+                    const int jp = (d.z >> 16) == TG_JOINT_PRISMATIC ? 1 : 0;
+                    x |= ((d.x & 127) | jp << 7 | (d.y & 255) << 8) << (16 * k);
+                }
+                a.v[w * M::LPE + lane] = x;
+            }
+        return a;
+    }
+    static constexpr Arr tab = make();
+};
 __device__ __forceinline__ int d_dof(const I4 &d) { return d.z & 0xFFFF; }
 __device__ __forceinline__ int d_jt(const I4 &d) { return d.z >> 16; }
 __device__ __forceinline__ int d_nch(const I4 &d) { return d.w & 15; }
@@ -233,6 +264,21 @@ __device__ __forceinline__ SV motion_S(int jt, V3 ax, V3 P) {
 }
 __device__ __forceinline__ SV ldS(const LE &s, int g, int jt) {
     return motion_S(jt, ldv3(s, g * GF + F_AX), ldv3(s, g * GF + F_P));
+}
+// models whose every joint group is revolute (Thormang, the scooters: their
+// prismatic joints are locked seat joints inside the root group): the joint
+// type drops out of every pass -- no per-lane select or branch on it
+template <class M> constexpr bool all_revolute() {
+    for (int g = 1; g < M::NG; ++g)
+        if (M::jtype[g] != TG_JOINT_REVOLUTE) return false;
+    return true;
+}
+template <class M> __device__ __forceinline__ SV motion_Sm(int jt, V3 ax, V3 P) {
+    if constexpr (all_revolute<M>()) return SV{ax, cross(P, ax)};
+    else return motion_S(jt, ax, P);
+}
+template <class M> __device__ __forceinline__ SV ldSm(const LE &s, int g, int jt) {
+    return motion_Sm<M>(jt, ldv3(s, g * GF + F_AX), ldv3(s, g * GF + F_P));
 }
 
 // The LPE lanes of an env are consecutive lanes of one wavefront, whose LDS
@@ -429,6 +475,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         int *p = tab + PL::T_DESC + 4 * i;
         p[0] = d.x; p[1] = d.y; p[2] = d.z; p[3] = d.w;
     }
+    for (int i = tid; i < PackTab<M>::NPW * LPE; i += EPB * LPE) tab[PL::T_PACK + i] = PackTab<M>::tab.v[i];
     for (int i = tid; i < 32; i += EPB * LPE) tab[PL::T_ZERO + i] = 0;
     for (int i = tid; i < M::NCG * M::MAXD; i += EPB * LPE) tab[PL::T_CPATH + i] = M::cpath[i / M::MAXD][i % M::MAXD];
 
@@ -529,6 +576,34 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         for (int k = 0; k < 13; ++k) rt0[k] = root[k];
     }
     __syncthreads();   // group tables (shared by both wavefronts)
+    constexpr int NPW = PackTab<M>::NPW;
+    int pkw[NPW];
+#pragma unroll
+    for (int w = 0; w < NPW; ++w) pkw[w] = tab[PL::T_PACK + w * LPE + sub];
+    // step t's (group, parent, joint type) from the packed words (descriptor
+    // fields x, y and z's joint type), or the LDS descriptor for NG > 128
+#ifndef TG_PACK_MASK
+#define TG_PACK_MASK 15   // passes using the packed words: 1 pass 1a, 2 pass 2b, 4 pass 3, 8 impulse top-down
+#endif
+    auto pdsc_on = [&](int t, auto PASS) {
+        if constexpr (PackTab<M>::ON && (TG_PACK_MASK & decltype(PASS)::value)) {
+            // (laundered through an empty volatile asm, which stays between the
+            // wave barriers around it: the loads this step's fields address are
+            // then issued where the pass issues them, a step or two ahead, not
+            // hoisted to the start of the pass with all their registers live)
+            int wv = pkw[t / 2];
+            __asm__ volatile("" : "+v"(wv));
+            const int v = (wv >> (16 * (t % 2))) & 0xFFFF;
+            return I4{bounded(v & 127, 0, M::NG), bounded(v >> 8, 0, M::NG),
+                      ((v >> 7) & 1 ? TG_JOINT_PRISMATIC : TG_JOINT_REVOLUTE) << 16, 0};
+        } else {
+            return dsc(t);
+        }
+    };
+    auto pdsc = [&](int t) { return pdsc_on(t, IntC<1>{}); };
+    auto pdsc2 = [&](int t) { return pdsc_on(t, IntC<2>{}); };
+    auto pdsc3 = [&](int t) { return pdsc_on(t, IntC<4>{}); };
+    auto pdsc4 = [&](int t) { return pdsc_on(t, IntC<8>{}); };
     if constexpr ((M::FUSED & 4) != 0) {
         if (a.pp_in_step && a.pp.t7 && tid == 0) paper_t7_block(a.pp, reinterpret_cast<const float *>(tab + PL::T_T7), chunk);
     }
@@ -747,7 +822,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
 #pragma unroll
                 for (int k = 0; k < 9; ++k) Rpc.a[k] = ck[k];
                 V3 tr = v3(ck[9], ck[10], ck[11]);
-                if (jt == TG_JOINT_REVOLUTE) {   // Rpc * Rz(q)
+                if (all_revolute<M>() || jt == TG_JOINT_REVOLUTE) {   // Rpc * Rz(q)
                     float sq, cq;
                     tg_sincos(qg, &sq, &cq);
 #pragma unroll
@@ -763,7 +838,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                 const V3 Pg = Pp + mul(Rp, tr);
                 stR(s, g, Rg);
                 stv3(s, o + F_P, Pg);
-                const SV Sg = motion_S(jt, v3(Rg.a[2], Rg.a[5], Rg.a[8]), Pg);
+                const SV Sg = motion_Sm<M>(jt, v3(Rg.a[2], Rg.a[5], Rg.a[8]), Pg);
                 const SV vg = vp + qdg * Sg;
                 stsv(s, o + F_V, vg);
             }
@@ -774,16 +849,16 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         // t + 1 and t + 2 in flight)
         float kr[3][12];
         I4 dr[3];
-        dr[0] = dsc(0);
+        dr[0] = pdsc(0);
         load_kin(dr[0].x, kr[0]);
         if constexpr (M::NSTEP > 1) {
-            dr[1] = dsc(1);
+            dr[1] = pdsc(1);
             load_kin(dr[1].x, kr[1]);
         }
 #pragma unroll
         for (int t = 0; t < M::NSTEP; ++t) {
             if (t + 2 < M::NSTEP) {
-                dr[(t + 2) % 3] = dsc(t + 2);
+                dr[(t + 2) % 3] = pdsc(t + 2);
                 load_kin(dr[(t + 2) % 3].x, kr[(t + 2) % 3]);
             }
             body1(dr[t % 3], kr[t % 3]);
@@ -850,7 +925,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
             // with D0 = S.I^A.S + armature: D = (1 + be) D0 + Dimp, tau + al D0
             // cb replaces v (dead after pass 1b) in F_V; on a SEPC rerun pass 1
             // was not rerun and F_V already holds cb
-            const SV cbv = crm(ldsv(s, o + F_V), qd * ldS(s, g, bounded(gi[g * GIW + GI_JT], 0, 4)));
+            const SV cbv = crm(ldsv(s, o + F_V), qd * ldSm<M>(s, g, bounded(gi[g * GIW + GI_JT], 0, 4)));
             if (valid) {
                 if (cp == 0) {
                     s(o + F_CL) = cl0;
@@ -916,7 +991,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                 // with D0 = S.I^A.S + armature: D = (1 + be) D0 + Dimp, tau + al D0
                 // cb replaces v (dead after pass 1b) in F_V; on a SEPC rerun pass 1
                 // was not rerun and F_V already holds cb
-                if (!SEPC || cp == 0) stsv(s, o + F_V, crm(ldsv(s, o + F_V), qd * ldS(s, g, bounded(gi[g * GIW + GI_JT], 0, 4))));
+                if (!SEPC || cp == 0) stsv(s, o + F_V, crm(ldsv(s, o + F_V), qd * ldSm<M>(s, g, bounded(gi[g * GIW + GI_JT], 0, 4))));
                 s(o + F_DINV) = (1.f + be) * cd[0] + Dimp;
                 s(o + F_UU) = tau + al * cd[0];
                 s(o + F_QDS) = al;
@@ -944,8 +1019,9 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         // unrolled (round 2: ThormangWalk kernel 56.8 -> 56.5 us, A/B twice)
 #pragma unroll
         for (int t = M::NSTEP - 1; t >= 0; --t) {
-            const I4 dc = dsc(t);
-            const int g = dc.x;
+            const I4 dc = dsc(t);   // (children for the gather)
+            const I4 pc = pdsc2(t);  // own group from registers: its loads need not wait for dc
+            const int g = pc.x;
             if (g > 0) {
                 const int o = g * GF;
                 float X[6], Bm[9], ph[3], cb1[3], cb2[3];
@@ -959,7 +1035,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                     cb1[k] = s(o + F_V + 3 * hh + k);
                     cb2[k] = s(o + F_V + 3 - 3 * hh + k);
                 }
-                const SV Sg = ldS(s, g, d_jt(dc));
+                const SV Sg = ldSm<M>(s, g, d_jt(pc));
                 const float c0 = s(o + F_DINV), tau = s(o + F_UU), al = s(o + F_QDS), c1 = s(o + F_C1);
                 // children: every load issued before the first add (absent children read the zero block)
                 auto gather2 = [&](auto NCc) {
@@ -1043,13 +1119,14 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         // unrolled (round 2: Gogoro 8.27e7 -> 8.36e7, GogoroPaper 8.55e7 -> 8.64e7, A/B twice)
 #pragma unroll
         for (int t = M::NSTEP - 1; t >= 0; --t) {
-            const I4 dc = dsc(t);
-            const int g = dc.x;
+            const I4 dc = dsc(t);   // (children for the gather)
+            const I4 pc = pdsc2(t);
+            const int g = pc.x;
             if (g > 0) {
                 const int o = g * GF;
                 SI IA = ldsi(s, o + F_IA);
                 SV pA = ldsv(s, o + F_PA);
-                const SV Sg = ldS(s, g, d_jt(dc));
+                const SV Sg = ldSm<M>(s, g, d_jt(pc));
                 const SV cb = ldsv(s, o + F_V);
                 const float c0 = s(o + F_DINV), tau = s(o + F_UU), al = s(o + F_QDS), c1 = s(o + F_C1);
                 const int smax = d_smax(dc);
@@ -1109,13 +1186,13 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         struct Own { SV cb, U, S; float qd, uu, dinv, te, K, eff; };
         auto ld_own = [&](const I4 &dc) {
             const int g = max(dc.x, 0), o = g * GF;
-            return Own{ldsv(s, o + F_V), ldsv(s, o + F_U), ldS(s, g, d_jt(dc)),
+            return Own{ldsv(s, o + F_V), ldsv(s, o + F_U), ldSm<M>(s, g, d_jt(dc)),
                        s(o + F_QD), s(o + F_UU), s(o + F_DINV),
                        s(o + F_CL), s(o + F_CL + 1), s(o + F_CL + 2)};
         };
         I4 dr[2];
         Own ow[2];
-        dr[0] = dsc(0);
+        dr[0] = pdsc3(0);
         ow[0] = ld_own(dr[0]);
 #pragma unroll
         for (int t = 0; t < M::NSTEP; ++t) {
@@ -1124,7 +1201,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
             const int g = dc.x;
             const SV apar = ldsv(s, ac_s(max(dc.y, 0)));
             if (t + 1 < M::NSTEP) {
-                dr[(t + 1) % 2] = dsc(t + 1);
+                dr[(t + 1) % 2] = pdsc3(t + 1);
                 ow[(t + 1) % 2] = ld_own(dr[(t + 1) % 2]);
             }
             if (g > 0) {
@@ -1186,7 +1263,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
 #pragma unroll
                 for (int i = 0; i < M::MAXD; ++i) {
                     qv[i] = i < lk ? s(pk[i] * GF + F_QDS) : 0.f;
-                    sv[i] = ldS(s, pk[i], pj[i]);
+                    sv[i] = ldSm<M>(s, pk[i], pj[i]);
                 }
 #pragma unroll
                 for (int i = 0; i < M::MAXD; ++i) v = v + qv[i] * sv[i];
@@ -1344,7 +1421,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                     du[i] = 0.f;
                     if (i < lk) {
                         const int g = pk[i];
-                        const float u = -dot(ldS(s, g, pj[i]), p);
+                        const float u = -dot(ldSm<M>(s, g, pj[i]), p);
                         du[i] = u;
                         p = p + (u * s(g * GF + F_DINV)) * ldsv(s, g * GF + F_U);
                     }
@@ -1368,7 +1445,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                             const int hg = M::cpath[c][i];
                             const float dui = (i < lk && pk[i] == hg) ? du[i] : 0.0f;
                             const float x = (dui - dot(ldsv(s, hg * GF + F_U), av)) * s(hg * GF + F_DINV);
-                            av = av + x * ldS(s, hg, M::jtype[hg]);
+                            av = av + x * ldSm<M>(s, hg, M::jtype[hg]);
                         }
                     }
                     dvc[c] = av;
@@ -1416,9 +1493,23 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
 #pragma unroll
                     for (int jj = 0; jj < JL; ++jj) rv[jj] += wr[jj][i] * d;
                 };
+#ifdef TG_PGS_REFRESH   // developer build (drift study): row velocities re-formed at every sweep
+                float vfr[JL];
+#pragma unroll
+                for (int jj = 0; jj < JL; ++jj) vfr[jj] = rv[jj];
+#endif
                 auto sweeps = [&](int n_it) {
 #pragma unroll 1
                 for (int it = 0; it < n_it; ++it) {
+#ifdef TG_PGS_REFRESH
+#pragma unroll
+                    for (int jj = 0; jj < JL; ++jj) {
+                        float r = vfr[jj];
+#pragma unroll
+                        for (int c = 0; c < K; ++c) r += wr[jj][c] * lam[c];
+                        rv[jj] = r;
+                    }
+#endif
 #pragma unroll
                     for (int sh = 0; sh < M::NS; ++sh) {
                         const int rb = row_base<M>(sh), nr = M::shape_nrows[sh];
@@ -1615,12 +1706,12 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                 struct OwnI { SV U, S; float uu, uv, dinv, qds; };
                 auto ld_own = [&](const I4 &dc) {
                     const int g = max(dc.x, 0), o = g * GF;
-                    return OwnI{ldsv(s, o + F_U), ldS(s, g, d_jt(dc)), s(o + F_UU), s(o + F_C1), s(o + F_DINV),
+                    return OwnI{ldsv(s, o + F_U), ldSm<M>(s, g, d_jt(dc)), s(o + F_UU), s(o + F_C1), s(o + F_DINV),
                                 s(o + F_QDS)};
                 };
                 I4 dr[2];
                 OwnI ow[2];
-                dr[0] = dsc(0);
+                dr[0] = pdsc4(0);
                 ow[0] = ld_own(dr[0]);
 #pragma unroll
                 for (int t = 0; t < M::NSTEP; ++t) {
@@ -1631,7 +1722,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                     const SV ap = ldsv(s, op + F_PA);
                     const SV av = vit ? ldsv(s, op + F_V) : sv0();
                     if (t + 1 < M::NSTEP) {
-                        dr[(t + 1) % 2] = dsc(t + 1);
+                        dr[(t + 1) % 2] = pdsc4(t + 1);
                         ow[(t + 1) % 2] = ld_own(dr[(t + 1) % 2]);
                     }
                     if (g > 0) {
@@ -1674,7 +1765,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                             const int o = g * GF;
                             SV p = ldsv(s, o + F_PA);
                             for (int c = 0; c < d_nch(dc); ++c) p = p + ldsv(s, d_child(dc, c) * GF + F_PA);
-                            const float u = -dot(ldS(s, g, d_jt(dc)), p);
+                            const float u = -dot(ldSm<M>(s, g, d_jt(dc)), p);
                             s(o + F_UU) = u;
                             stsv(s, o + F_PA, p + (u * s(o + F_DINV)) * ldsv(s, o + F_U));
                         }
@@ -1695,7 +1786,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                         if (g > 0) {
                             const int o = g * GF;
                             const float x = (s(o + F_UU) - dot(ldsv(s, o + F_U), ap)) * s(o + F_DINV);
-                            stsv(s, o + F_PA, ap + x * ldS(s, g, d_jt(dc)));
+                            stsv(s, o + F_PA, ap + x * ldSm<M>(s, g, d_jt(dc)));
                             s(o + (pass == 0 ? F_QD : F_QDS)) = s(o + F_QDS) + x;
                         }
                         TG_SYNC();
@@ -1736,7 +1827,16 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
             float dx = 0.f, dy = 0.f, dz = 0.f, dw = 1.f;
             if (an > 1e-12f) {
                 float sa, ca;
+                // the libm half-angle sine / cosine, not the hardware v_sin / v_cos
+                // (__sincosf): at these small angles the approximation's absolute
+                // error is a large relative error in the orientation increment,
+                // the largest GPU-specific term of the Gogoro drift study
+                // (profiles/r3/drift_gogoro.txt); once per substep
+#ifdef TG_FAST_QUAT   // developer build: the hardware approximation (drift study control)
                 __sincosf(0.5f * an, &sa, &ca);
+#else
+                sincosf(0.5f * an, &sa, &ca);
+#endif
                 const float kk = sa / wn;
                 dx = v0.w.x * kk; dy = v0.w.y * kk; dz = v0.w.z * kk; dw = ca;
             }
