@@ -16,7 +16,10 @@
  *                            (tasks/gogoro_new.py:125-130)
  *   tg_refresh               refresh_actor_root_state_tensor /
  *                            refresh_dof_state_tensor (gogoro_new.py:141-142,426-427)
- *                            -- a stream-ordered no-op: the views are the live state
+ *                            -- the views are the live state, nothing is copied; it
+ *                            is REQUIRED after writes through the dof_props /
+ *                            env_dirty views (it re-arms the compose launch the
+ *                            library otherwise skips while no env can be dirty)
  *   tg_set_dof_position_targets / tg_set_dof_velocity_targets
  *                            set_dof_position_target_tensor /
  *                            set_dof_velocity_target_tensor (gogoro_new.py:364,369)

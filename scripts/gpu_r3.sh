@@ -27,6 +27,13 @@ for t in ${TASKS:-ThormangWalk Gogoro}; do
     cut -d, -f1-4 $OUT/trace_$t/run_kernel_stats.csv | head -4
   fi
 done
+# in-kernel section profile (s_memtime stamps) of a developer build
+if [ -n "${SECT:-}" ]; then
+  for t in ${TASKS:-ThormangWalk Gogoro}; do
+    TG_LIB_PATH=thormang_isaacgym_amd/libtgsim_prof.so timeout -k 10 300 python scripts/section_prof.py $t > $OUT/section_$t.txt 2>&1
+    rc=$?; ok $rc; grep -v Warning $OUT/section_$t.txt | grep -v "^ *sp = " | head -16
+  done
+fi
 # A/B: the bench lines again with developer builds (AB="label=path.so ...")
 for ab in ${AB:-}; do
   for t in ${TASKS:-ThormangWalk Gogoro}; do

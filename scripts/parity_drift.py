@@ -2,7 +2,8 @@
 
     python scripts/parity_drift.py WORKLOAD [--steps 1000] [--envs N] [--no-gpu] [--out DIR]
 
-WORKLOAD: gogoro (free base, balance policy), gogoro_fixbase (DEBUGFIXBASE),
+WORKLOAD: gogoro (free base, balance policy), gogoro_random (free base, the
+bench's U(-1,1) actions), gogoro_fixbase (DEBUGFIXBASE),
 walk (random actions), walk_stand (zero actions), walk_fixbase.
 
 One reference run -- the fp64 oracle env (oracle/physics_ref.c + the task
@@ -55,6 +56,9 @@ def build(workload, n, seed, kinds):
     if gogoro:
         mk = lambda prec: OracleGogoro(parity_cfg(n, max_steps=1000), NumpyDraws(seed), precision=prec, fix_base=fix)
         act = balance_policy
+        if workload == "gogoro_random":
+            rsa = np.random.default_rng(seed + 100)
+            act = lambda o: rsa.uniform(-1, 1, (n, 1)).astype(np.float32)
     else:
         mk = lambda prec: OracleWalk(_walk_cfg(n, fix), NumpyDraws(seed), precision=prec)
         rs = np.random.default_rng(seed + 100)
@@ -138,7 +142,8 @@ def table(out):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("workload", choices=["gogoro", "gogoro_fixbase", "walk", "walk_stand", "walk_fixbase"])
+    ap.add_argument("workload", choices=["gogoro", "gogoro_random", "gogoro_fixbase", "walk", "walk_stand",
+                                        "walk_fixbase"])
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--envs", type=int, default=64)
     ap.add_argument("--seed", type=int, default=21)

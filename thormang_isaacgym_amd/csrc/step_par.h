@@ -62,6 +62,13 @@ static __device__ unsigned long long tg_prof_acc[24];   // [16..]: sub-sections 
 template <int N> struct IntC {
     static constexpr int value = N;
 };
+// f(IntC<I>), ..., f(IntC<N-1>): a loop whose index is a compile-time constant
+template <int I, int N, class F> __device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (I < N) {
+        f(IntC<I>{});
+        static_for<I + 1, N>(f);
+    }
+}
 
 // one env's LDS state
 struct LE {
@@ -201,6 +208,14 @@ template <class M> constexpr I4 step_desc(int t, int lane) {
     int w = M::nchild[g] | smax << 4;
     for (int c = 0; c < M::nchild[g]; ++c) w |= M::child[g][c] << (8 + 8 * c);
     return I4{g, M::parent[g], M::gdof[g] | M::jtype[g] << 16, w};
+}
+// the largest child count among schedule step t's groups (the gather width
+// of pass 2b at that step, a compile-time constant)
+template <class M> constexpr int step_smax(int t) {
+    int m = 0;
+    for (int l = 0; l < M::SL; ++l)
+        if (M::sched[t][l] > 0 && M::nchild[M::sched[t][l]] > m) m = M::nchild[M::sched[t][l]];
+    return m;
 }
 template <class M> constexpr int max_nonroot_children() {
     int m = 0;
@@ -1016,10 +1031,14 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
 #pragma unroll
             for (int k = 0; k < 3; ++k) o[k] = pair_swap(v[k]);
         };
-        // unrolled (round 2: ThormangWalk kernel 56.8 -> 56.5 us, A/B twice)
-#pragma unroll
-        for (int t = M::NSTEP - 1; t >= 0; --t) {
-            const I4 dc = dsc(t);   // (children for the gather)
+        // unrolled (round 2: ThormangWalk kernel 56.8 -> 56.5 us, A/B twice),
+        // the step index a compile-time constant (its gather width too)
+        // (the children's descriptor read one step ahead, ahead of the step's own loads)
+        I4 dnext = dsc(M::NSTEP - 1);
+        static_for<0, M::NSTEP>([&](auto TT) {
+            constexpr int t = M::NSTEP - 1 - decltype(TT)::value;
+            const I4 dc = dnext;   // (children for the gather)
+            if constexpr (t > 0) dnext = dsc(t - 1);
             const I4 pc = pdsc2(t);  // own group from registers: its loads need not wait for dc
             const int g = pc.x;
             if (g > 0) {
@@ -1063,10 +1082,8 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                         for (int k = 0; k < 3; ++k) ph[k] += cp[c][k];
                     }
                 };
-                const int smax = d_smax(dc);
-                if (smax == 1) gather2(IntC<1>{});
-                else if (smax == 2) gather2(IntC<2>{});
-                else if (smax >= 3) gather2(IntC<3>{});
+                constexpr int smax = step_smax<M>(t);
+                if constexpr (smax >= 1) gather2(IntC<(smax < 3 ? smax : 3)>{});
                 // the half's orientation of B
                 float Y[9];
                 Y[0] = Bm[0]; Y[4] = Bm[4]; Y[8] = Bm[8];
@@ -1114,12 +1131,15 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                 stv3(s, pa_c(g) + 3 * hh, pav);
             }
             TG_SYNC();
-        }
+        });
         } else {
         // unrolled (round 2: Gogoro 8.27e7 -> 8.36e7, GogoroPaper 8.55e7 -> 8.64e7, A/B twice)
-#pragma unroll
-        for (int t = M::NSTEP - 1; t >= 0; --t) {
-            const I4 dc = dsc(t);   // (children for the gather)
+        // (the children's descriptor read one step ahead, ahead of the step's own loads)
+        I4 dnext = dsc(M::NSTEP - 1);
+        static_for<0, M::NSTEP>([&](auto TT) {
+            constexpr int t = M::NSTEP - 1 - decltype(TT)::value;
+            const I4 dc = dnext;   // (children for the gather)
+            if constexpr (t > 0) dnext = dsc(t - 1);
             const I4 pc = pdsc2(t);
             const int g = pc.x;
             if (g > 0) {
@@ -1129,10 +1149,8 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                 const SV Sg = ldSm<M>(s, g, d_jt(pc));
                 const SV cb = ldsv(s, o + F_V);
                 const float c0 = s(o + F_DINV), tau = s(o + F_UU), al = s(o + F_QDS), c1 = s(o + F_C1);
-                const int smax = d_smax(dc);
-                if (smax == 1) gather(IntC<1>{}, dc, IA, pA);
-                else if (smax == 2) gather(IntC<2>{}, dc, IA, pA);
-                else if (smax >= 3) gather(IntC<3>{}, dc, IA, pA);
+                constexpr int smax = step_smax<M>(t);
+                if constexpr (smax >= 1) gather(IntC<(smax < 3 ? smax : 3)>{}, dc, IA, pA);
                 const SV U = mul(IA, Sg);
                 const float D0 = dot(Sg, U);   // without the armature (folded into c0, tau)
                 const float Dinv = 1.0f / (c1 * D0 + c0);
@@ -1147,7 +1165,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                 stsv(s, pa_c(g), pa);
             }
             TG_SYNC();
-        }
+        });
         }
         TG_PROF(18)
         // root: every lane factors the root articulated inertia itself

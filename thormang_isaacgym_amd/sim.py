@@ -5,7 +5,9 @@ simulate), with torch tensors as zero-copy state views.
 Reference calls mirrored (isaacgymenvs/tasks/...):
   acquire_actor_root_state_tensor / acquire_dof_state_tensor + wrap_tensor
       -> Sim.root_state [N,13], Sim.dof_state [N*D,2]      (gogoro_new.py:125-130)
-  refresh_*_tensor -> Sim.refresh() (no-op, state is live)  (gogoro_new.py:141-142)
+  refresh_*_tensor -> Sim.refresh() (state is live: nothing copied; REQUIRED after writes
+      through the dof_props / env_dirty views, which take effect at the next simulate only
+      after it -- the library skips the compose launch while no env can be dirty)  (gogoro_new.py:141-142)
   set_dof_position/velocity_target_tensor -> Sim.set_dof_*_targets (gogoro_new.py:364,369)
   set_actor_root_state_tensor_indexed / set_dof_state_tensor_indexed  (gogoro_new.py:547,552)
   set_actor_dof_properties (per env)   -> Sim.set_dof_properties_indexed (gogoro_new.py:294,601)
@@ -140,6 +142,9 @@ class Sim:
 
     # ---------------------------------------------------------------- tensor API
     def refresh(self):
+        """refresh_*_tensor: the views are live, nothing is copied.  Call it after
+        writing through ``dof_props`` / ``env_dirty`` (tg_refresh re-arms the
+        compose launch those writes need)."""
         check(lib().tg_refresh(self._h), "refresh")
 
     def set_dof_position_targets(self, t: torch.Tensor):
