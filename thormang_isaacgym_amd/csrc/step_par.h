@@ -160,7 +160,26 @@ template <class M> struct ParLayout {
     // forces survive and the drive-clamp rerun starts at pass 2
     static constexpr int CB = (FLG + 1 + 3) & ~3;
     static constexpr bool SEPC = ((size_t)M::EPB * (CB + 32 * M::NG) + T_TOTAL) * 4 <= 160 * 1024;
-    static constexpr int TOTAL = SEPC ? CB + 32 * M::NG : FLG + 1;
+    static constexpr int TOTAL0 = SEPC ? CB + 32 * M::NG : FLG + 1;
+    // Woodbury drive-clamp update (small trees, one lane per non-root group,
+    // impulse application by superposition): instead of re-running passes 2-3
+    // with the saturated drives explicit, the first solve is corrected by the
+    // unit-torque responses of up to WCM clamped drives.  Per env: G (the
+    // responses' joint accelerations per group), R (root accelerations), A
+    // (contact-group accelerations), J (row velocities, = J G), Minv
+    static constexpr bool SUPER = K > 0 && K * (M::MAXD + 6) <= M::NG * 21;
+#ifdef TG_NO_WOOD   // developer build: the drive-clamp rerun instead (A/B)
+    static constexpr bool WOOD = false;
+#else
+    static constexpr bool WOOD = M::NG <= 8 && M::NG - 1 <= M::LPE && (SUPER || K == 0);
+#endif
+    static constexpr int WCM = 2;
+    static constexpr int WB_G = (TOTAL0 + 3) & ~3;          // [WCM][8]
+    static constexpr int WB_R = WB_G + WCM * 8;             // [WCM][6]
+    static constexpr int WB_A = WB_R + WCM * 6;             // [WCM][NCG][6]
+    static constexpr int WB_J = WB_A + WCM * 6 * M::NCG;    // [WCM][K]
+    static constexpr int WB_M = WB_J + WCM * (K > 0 ? K : 1);   // [WCM][WCM]
+    static constexpr int TOTAL = WOOD ? WB_M + WCM * WCM : TOTAL0;
 #ifndef TG_ES_PAD
 #define TG_ES_PAD 0   // developer experiment: extra floats per env (LDS bank pattern)
 #endif
@@ -776,6 +795,134 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
     TG_SYNC();
     TG_PROF(0)
 
+    // ---- Woodbury drive-clamp state of the current substep (PL::WOOD):
+    // the env's clamped groups as a lane mask, their count
+    unsigned wmask = 0u;
+    int wn = 0;
+    // the a-th clamped group of the env (ascending group order)
+    auto wgroup = [&](int aidx) {
+        unsigned m = wmask;
+        for (int k = 0; k < aidx; ++k) m &= m - 1u;
+        return 1 + (int)__builtin_ctz(m);
+    };
+    // LDL6 / a0 of the substep are passed in (the lambda is defined once)
+    auto wood_update_impl = [&](const LDL6 &rf, SV &acc0) -> bool {
+        if constexpr (PL::WOOD) {
+            constexpr int WCM = PL::WCM;
+            const int gl = 1 + sub;
+            const bool clm = gl < M::NG && s(gl * GF + F_C1) != 0.f;
+            const uint64_t bal = __ballot(clm);
+            const int lw = (int)(threadIdx.x % 64);
+            wmask = (unsigned)(bal >> (lw - sub)) & ((1u << LPE) - 1u);
+            wn = __builtin_popcount(wmask);
+            if (wn > WCM) { wn = 0; wmask = 0u; return false; }   // more than WCM saturate: the rerun
+            // (1) lane aidx < wn: the response of the whole tree to a unit torque
+            // at clamped group ga (the articulated inertias of the first solve):
+            // up-walk along ga's ancestors, root solve, top-down over every group
+            if (sub < wn) {
+                const int ga = wgroup(sub);
+                SV dp = sv0();
+                float dus[M::NG];
+                dus[0] = 0.f;
+#pragma unroll
+                for (int g = M::NG - 1; g >= 1; --g) {
+                    // g on ga's path: g == ga or an ancestor of ga (compile-time table)
+                    bool onp = false;
+#pragma unroll
+                    for (int k = 1; k < M::NG; ++k) onp = (ga == k) ? (M::anc[k][g] != 0) : onp;
+                    const SV Ug = ldsv(s, g * GF + F_U);
+                    const float di = s(g * GF + F_DINV);
+                    const SV Sg = ldSm<M>(s, g, M::jtype[g]);
+                    float du = g == ga ? 1.f : -dot(Sg, dp);
+                    du = onp ? du : 0.f;
+                    dus[g] = du;
+                    dp = dp + (du * di) * Ug;
+                }
+                const SV ar = fix_base ? sv0() : ldl6_solve(rf, -1.0f * dp);
+                SV acc[M::NG];
+                acc[0] = ar;
+#pragma unroll
+                for (int g = 1; g < M::NG; ++g) {
+                    const SV ap = acc[M::parent[g]];
+                    const SV Ug = ldsv(s, g * GF + F_U);
+                    const float di = s(g * GF + F_DINV);
+                    const float qg = (dus[g] - dot(Ug, ap)) * di;
+                    acc[g] = ap + qg * ldSm<M>(s, g, M::jtype[g]);
+                    s(PL::WB_G + 8 * sub + g) = qg;
+                }
+                stsv(s, PL::WB_R + 6 * sub, ar);
+#pragma unroll
+                for (int c = 0; c < M::NCG; ++c) stsv(s, PL::WB_A + 6 * (M::NCG * sub + c), acc[M::cgroup[c]]);
+            }
+            TG_SYNC();
+            // (2) every lane: the clamped system M = K^-1 - E^T G (wn x wn), the
+            // correction w = delta + M^-1 (qdd_C + N delta), delta = +-effort - te
+            float Kc[WCM], dl[WCM], qc[WCM], Nm[WCM][WCM];
+            int gc[WCM];
+#pragma unroll
+            for (int i = 0; i < WCM; ++i) {
+                gc[i] = i < wn ? wgroup(i) : 1;
+                const int o = gc[i] * GF;
+                const float te = s(o + F_CL), K = s(o + F_CL + 1), eff = s(o + F_CL + 2), sg = s(o + F_C1);
+                Kc[i] = K;
+                dl[i] = i < wn ? sg * eff - te : 0.f;
+                qc[i] = s(o + F_UU);
+            }
+#pragma unroll
+            for (int i = 0; i < WCM; ++i)
+#pragma unroll
+                for (int j = 0; j < WCM; ++j) Nm[i][j] = s(PL::WB_G + 8 * j + gc[i]);   // response of i's dof to torque j
+            float Mm[WCM][WCM], Mi[WCM][WCM];
+#pragma unroll
+            for (int i = 0; i < WCM; ++i)
+#pragma unroll
+                for (int j = 0; j < WCM; ++j) Mm[i][j] = (i == j ? 1.0f / Kc[i] : 0.f) - Nm[i][j];
+            static_assert(WCM == 2, "closed-form inverse below");
+            if (wn == 1) {
+                Mi[0][0] = 1.0f / Mm[0][0]; Mi[0][1] = Mi[1][0] = Mi[1][1] = 0.f;
+            } else {
+                const float det = Mm[0][0] * Mm[1][1] - Mm[0][1] * Mm[1][0], id = 1.0f / det;
+                Mi[0][0] = Mm[1][1] * id; Mi[1][1] = Mm[0][0] * id;
+                Mi[0][1] = -Mm[0][1] * id; Mi[1][0] = -Mm[1][0] * id;
+            }
+            float wv[WCM];
+#pragma unroll
+            for (int i = 0; i < WCM; ++i) {
+                float r = qc[i];
+#pragma unroll
+                for (int j = 0; j < WCM; ++j) r += Nm[i][j] * dl[j];
+                wv[i] = r;
+            }
+#pragma unroll
+            for (int i = 0; i < WCM; ++i) {
+                float z = 0.f;
+#pragma unroll
+                for (int j = 0; j < WCM; ++j) z += Mi[i][j] * wv[j];
+                wv[i] = i < wn ? dl[i] + z : 0.f;
+            }
+            // (3) the corrected accelerations: qdd += G w (the lane's group), a0 += R w
+            if (gl < M::NG) {
+                float dq = 0.f;
+#pragma unroll
+                for (int i = 0; i < WCM; ++i) dq += s(PL::WB_G + 8 * i + gl) * wv[i];
+                s(gl * GF + F_UU) += dq;
+                s(gl * GF + F_QDS) += h * dq;
+            }
+#pragma unroll
+            for (int i = 0; i < WCM; ++i) acc0 = acc0 + wv[i] * ldsv(s, PL::WB_R + 6 * i);
+            if (sub == 0) {
+#pragma unroll
+                for (int i = 0; i < WCM; ++i)
+#pragma unroll
+                    for (int j = 0; j < WCM; ++j) s(PL::WB_M + WCM * i + j) = Mi[i][j];
+            }
+            TG_SYNC();
+            return true;
+        } else {
+            (void)rf; (void)acc0;
+            return false;
+        }
+    };
     for (int sub_i = 0; sub_i < a.substeps; ++sub_i) {
         // Passes 1-3 run with every position/velocity drive implicit and
         // unclamped; if some drive's implicit end-of-substep torque te - K*qdd
@@ -787,6 +934,9 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         // LDS store (the compiler keeps LDS loads and stores in program order).
         LDL6 rootf{};
         SV a0 = sv0();
+        wmask = 0u;
+        wn = 0;
+        auto wood_update = [&]() { return wood_update_impl(rootf, a0); };
         // velocity limits of the lane's groups (used by the integration at the
         // end of the substep), issued now so their latency is hidden
         float vlim[(M::NG + LPE - 1) / LPE];
@@ -1230,11 +1380,18 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                 s(o + F_QDS) = w.qd + h * qdd;
                 if (cp == 0) {
                     s(o + F_UU) = qdd;
-                    if (w.K >= 0.f && fabsf(w.te - w.K * qdd) > w.eff) s(PL::FLG) = 1.f;
+                    const float ti = w.te - w.K * qdd;
+                    const bool sat = w.K >= 0.f && fabsf(ti) > w.eff;
+                    if (sat) s(PL::FLG) = 1.f;
+                    // (Woodbury: the drive's clamp side, F_C1 being dead after pass 2b)
+                    if constexpr (PL::WOOD) s(o + F_C1) = sat ? (ti > 0.f ? 1.f : -1.f) : 0.f;
                 }
             }
             TG_SYNC();
         }
+        }
+        if constexpr (PL::WOOD) {
+            if (cp == 0 && s(PL::FLG) != 0.f && wood_update()) break;   // else the rerun below
         }
         if (cp == 0 && s(PL::FLG) == 0.f) break;
         }   // clamp pass
@@ -1472,6 +1629,37 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                 for (int i = 0; i < K; ++i) s(PL::W + i * K + j) = rvel(i, dvc[M::shape_cg[row_shape<M>(i)]]);
             }
             TG_SYNC();
+            if constexpr (PL::WOOD) {
+                if (wn > 0) {
+                    // clamped drives (Woodbury): W' = W + (J G) M^-1 (J G)^T, J G =
+                    // each row's velocity response to the drives' unit torques
+                    for (int j = sub; j < K; j += LPE) {
+#pragma unroll
+                        for (int i = 0; i < PL::WCM; ++i)
+                            s(PL::WB_J + K * i + j) =
+                                i < wn ? rvel(j, ldsv(s, PL::WB_A + 6 * (M::NCG * i + row_cg<M>(j)))) : 0.f;
+                    }
+                    TG_SYNC();
+                    for (int j = sub; j < K; j += LPE) {
+                        float t[PL::WCM];
+#pragma unroll
+                        for (int i = 0; i < PL::WCM; ++i) {
+                            float x = 0.f;
+#pragma unroll
+                            for (int k = 0; k < PL::WCM; ++k) x += s(PL::WB_M + PL::WCM * i + k) * s(PL::WB_J + K * k + j);
+                            t[i] = x;
+                        }
+#pragma unroll
+                        for (int r = 0; r < K; ++r) {
+                            float x = s(PL::W + r * K + j);
+#pragma unroll
+                            for (int i = 0; i < PL::WCM; ++i) x += s(PL::WB_J + K * i + r) * t[i];
+                            s(PL::W + r * K + j) = x;
+                        }
+                    }
+                    TG_SYNC();
+                }
+            }
             TG_PROF(5)
             if constexpr (!SUPER) {   // impulse accumulators (F_PA slots) cleared by all lanes
                 for (int g = sub; g < M::NG; g += LPE) stsv(s, g * GF + F_PA, sv0());
@@ -1499,7 +1687,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                 for (int i = 0; i < K; ++i) {
                     tg[i] = s(PL::ROW + i * 8 + 6);
                     onr[i] = s(PL::ROW + i * 8 + 7);
-                    wd[i] = s(PL::W + i * K + i);
+                    wd[i] = 1.0f / s(PL::W + i * K + i);   // (the inverse diagonal, formed once)
                     lam[i] = 0.f;
                 }
                 auto row_v = [&](int i) {   // vfree_i + (W lambda)_i, from its owner lane
@@ -1537,7 +1725,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                             if (k >= nr) break;
                             const int i = rb + k;
                             const float vi = row_v(i);
-                            const float l = lam[i] + (tg[i] - vi) / wd[i];
+                            const float l = lam[i] + (tg[i] - vi) * wd[i];
                             const float li = onr[i] * fmaxf(l, 0.f);
                             set_lam(i, li);
                             Nsum += li;
@@ -1546,16 +1734,16 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                         const float mu = s(PL::SHP + 2 * sh), reff = s(PL::SHP + 2 * sh + 1);
                         // tangent 1, then tangent 2 with the cone projection of the
                         // pair, then the torsional row clamped
-                        set_lam(f, lam[f] - row_v(f) / wd[f]);
+                        set_lam(f, lam[f] - row_v(f) * wd[f]);
                         {
-                            const float l0 = lam[f], l1 = lam[f + 1] - row_v(f + 1) / wd[f + 1];
+                            const float l0 = lam[f], l1 = lam[f + 1] - row_v(f + 1) * wd[f + 1];
                             const float lt = sqrtf(l0 * l0 + l1 * l1), lim = mu * Nsum;
                             const float sc = lt > lim ? (lt > 0.f ? lim / lt : 0.f) : 1.f;
                             set_lam(f, l0 * sc);
                             set_lam(f + 1, l1 * sc);
                         }
                         const float lim3 = mu * Nsum * reff;
-                        set_lam(f + 2, fminf(fmaxf(lam[f + 2] - row_v(f + 2) / wd[f + 2], -lim3), lim3));
+                        set_lam(f + 2, fminf(fmaxf(lam[f + 2] - row_v(f + 2) * wd[f + 2], -lim3), lim3));
                     }
                 }
                 };
@@ -1596,7 +1784,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                     vf[i] = s(PL::VFREE + i);
                     tg[i] = s(PL::ROW + i * 8 + 6);
                     onr[i] = s(PL::ROW + i * 8 + 7);
-                    wd[i] = s(PL::W + i * K + i);
+                    wd[i] = 1.0f / s(PL::W + i * K + i);   // (the inverse diagonal, formed once)
                     lam[i] = 0.f;
                 }
 #pragma unroll
@@ -1625,7 +1813,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                             if (k >= nr) break;
                             const int i = rb + k;
                             const float vi = row_v(i);
-                            const float l = lam[i] + (tg[i] - vi) / wd[i];
+                            const float l = lam[i] + (tg[i] - vi) * wd[i];
                             const float li = onr[i] * fmaxf(l, 0.f);
                             set_lam(i, li);
                             Nsum += li;
@@ -1636,7 +1824,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                         for (int t = 0; t < 3; ++t) {
                             const int i = f + t;
                             const float vi = row_v(i);
-                            set_lam(i, lam[i] - vi / wd[i]);
+                            set_lam(i, lam[i] - vi * wd[i]);
                             if (t == 1) {
                                 const float l0 = lam[f], l1 = lam[f + 1];
                                 const float lt = sqrtf(l0 * l0 + l1 * l1), lim = mu * Nsum;
@@ -1698,6 +1886,9 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                     TG_SYNC();
                 }
                 if (!fix_base) {
+                    // (every lane forms the root response from all columns:
+                    // broadcast LDS reads; an LPE-lane DPP sum of per-column
+                    // terms measured slower, ThormangWalk 55.5 -> 56.9 us)
                     float d6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, v6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                     for (int j = 0; j < K; ++j) {
@@ -1811,6 +2002,57 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                     }
                     if (pass == 0) da0v = d0;
                     else da0 = d0;
+                }
+            }
+            if constexpr (PL::WOOD) {
+                if (wn > 0) {
+                    // clamped drives (Woodbury): the impulse response A'^-1 J^T lam =
+                    // A^-1 J^T lam (above) + G M^-1 (J G)^T lam, for both multiplier sets
+                    const int LPW = vit ? PL::W : PL::LAM;
+                    float jl[PL::WCM], jlv[PL::WCM];
+#pragma unroll
+                    for (int i = 0; i < PL::WCM; ++i) {
+                        float x = 0.f, xv = 0.f;
+#pragma unroll
+                        for (int r = 0; r < K; ++r) {
+                            const float jg = s(PL::WB_J + K * i + r);
+                            x += jg * s(LPW + r);
+                            xv += jg * s(PL::LAM + r);
+                        }
+                        jl[i] = x;
+                        jlv[i] = xv;
+                    }
+                    float y[PL::WCM], yv[PL::WCM];
+#pragma unroll
+                    for (int i = 0; i < PL::WCM; ++i) {
+                        float x = 0.f, xv = 0.f;
+#pragma unroll
+                        for (int k = 0; k < PL::WCM; ++k) {
+                            const float mi = s(PL::WB_M + PL::WCM * i + k);
+                            x += mi * jl[k];
+                            xv += mi * jlv[k];
+                        }
+                        y[i] = x;
+                        yv[i] = xv;
+                    }
+                    const int gl = 1 + sub;
+                    if (gl < M::NG) {
+                        float dq = 0.f, dqv = 0.f;
+#pragma unroll
+                        for (int i = 0; i < PL::WCM; ++i) {
+                            const float gi = s(PL::WB_G + 8 * i + gl);
+                            dq += gi * y[i];
+                            dqv += gi * yv[i];
+                        }
+                        s(gl * GF + F_QDS) += dq;
+                        if (vit) s(gl * GF + F_QD) += dqv;
+                    }
+#pragma unroll
+                    for (int i = 0; i < PL::WCM; ++i) {
+                        const SV ri = ldsv(s, PL::WB_R + 6 * i);
+                        da0 = da0 + y[i] * ri;
+                        da0v = da0v + yv[i] * ri;
+                    }
                 }
             }
             if (!fix_base) {
