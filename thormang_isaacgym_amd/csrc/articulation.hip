@@ -37,12 +37,17 @@ namespace tg {
 // or every dirty env (compose_kernel)
 template <class M> void launch_compose(const StepArgs &a, hipStream_t stream) {
     if (a.skip_compose) return;
-    if (a.compose_list)
+    if (a.compose_list) {
         hipLaunchKernelGGL(compose_list_kernel<M>, dim3((a.N + COMPOSE_WPB - 1) / COMPOSE_WPB), dim3(64), 0, stream,
                            a);
-    else
+    } else {
         hipLaunchKernelGGL(compose_kernel<M>, dim3((a.N + COMPOSE_WPB - 1) / COMPOSE_WPB), dim3(64 * COMPOSE_WPB), 0,
                            stream, a);
+        if (a.cuni) {   // shared-cache flag for the step kernels that follow
+            (void)hipMemsetD32Async(a.cuni, 1, 1, stream);
+            hipLaunchKernelGGL(uniform_check_kernel<M>, dim3(a.N), dim3(64), 0, stream, a);
+        }
+    }
 }
 
 // HF: terrain heightfield present (tg_set_heightfield); the flat-ground

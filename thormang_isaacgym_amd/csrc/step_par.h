@@ -522,7 +522,9 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
 #ifdef TG_EXP_HOT   // developer experiment: every env reads env (e % 64)'s inputs (cache-resident)
     const int ein = e % 64;
 #else
-    const int ein = e;
+    // every env reads env 0's composite block and property rows while they are
+    // all equal (a.cuni, uniform_check_kernel): one shared, cache-resident copy
+    const int ein = (a.cuni && *a.cuni) ? 0 : e;
 #endif
     // per-env inputs through 32-bit element offsets from the uniform base
     // pointers (scalar base + vector offset addressing, no 64-bit address math)

@@ -76,6 +76,10 @@ struct tg_sim {
     float *env_origin = nullptr;
     uint8_t *dirty = nullptr;
     int *err = nullptr;   // sticky state-error flag set by kernels (tg_sync reports it)
+    // shared-cache flag (StepArgs::cuni) for compiled-in models whose task
+    // kernels never edit composites / properties in place (not FUSED 2|4)
+    int *cuni = nullptr;
+    bool uni_ok = false;
     // terrain heightfield (tg_set_heightfield)
     float *hf = nullptr;
     int hf_rows = 0, hf_cols = 0;
@@ -176,6 +180,7 @@ tg::StepArgs step_args(tg_sim *s) {
     a.comp = s->comp;
     a.dirty = s->dirty;
     a.err = s->err;
+    a.cuni = s->uni_ok ? s->cuni : nullptr;
     a.hf = s->hf_rows > 0 ? s->hf : nullptr;
     a.hf_rows = s->hf_rows;
     a.hf_cols = s->hf_cols;
@@ -231,6 +236,9 @@ int tg_sim_create(const tg_model_desc *m, const tg_sim_params *params, int32_t n
     if (const char *u = getenv("TG_SEAT_RECOMPOSE")) s->no_inplace = u[0] == '1';
     if (const char *u = getenv("TG_PAPER_FINISH")) s->paper_finish_launch = u[0] == '1';
     if (const char *u = getenv("TG_PAPER_RB_LAUNCH")) s->paper_rb_launch = u[0] == '1';
+    // (TG_NO_SHARED_CACHE=1: every env reads its own block, the A/B control)
+    const char *nsc = getenv("TG_NO_SHARED_CACHE");
+    s->uni_ok = !(nsc && nsc[0] == '1') && (tg::model_fused(m->model_hash) & 6) == 0 && !tg::jit_has(m->model_hash);
     s->device = device;
     s->N = num_envs;
     s->D = m->num_dofs;
@@ -256,6 +264,7 @@ int tg_sim_create(const tg_model_desc *m, const tg_sim_params *params, int32_t n
     rc |= s->alloc(&s->env_origin, N * 3);
     rc |= s->alloc(&s->dirty, N);
     rc |= s->alloc(&s->err, 1);
+    rc |= s->alloc(&s->cuni, 1);   // 0: not uniform until a compose checked it
     rc |= s->alloc(&s->clist, 2 * N);
     rc |= s->alloc(&s->ccount, 2);
     if (rc) return TG_ERR_HIP;   // g_err holds the failing allocation; owner frees the rest
