@@ -56,6 +56,11 @@ template <class M, bool HF, class P = NoPost>
 int launch_par(const StepArgs &a, hipStream_t stream, const typename P::Args &pa = {}) {
     constexpr size_t bytes = ParLayout<M>::template bytes<M::EPB>();
     static_assert(bytes <= 160 * 1024, "LDS budget");
+#ifdef TG_EPB_DEV   // developer experiment: fewer envs per workgroup, the full LDS allocated (waves per CU)
+    constexpr int EPBX = M::PAIR ? TG_EPB_DEV : M::EPB;
+#else
+    constexpr int EPBX = M::EPB;
+#endif
     // the dynamic-LDS attribute is per device: one bit per device of this
     // instantiation, set the first time the kernel launches there (sims on
     // several devices in one process, from any thread)
@@ -64,12 +69,12 @@ int launch_par(const StepArgs &a, hipStream_t stream, const typename P::Args &pa
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return TG_ERR_HIP;
     const uint64_t bit = 1ull << dev;
     if (!(attr_set.load(std::memory_order_acquire) & bit)) {
-        if (hipFuncSetAttribute((const void *)step_par_kernel<M, M::EPB, HF, P>,
+        if (hipFuncSetAttribute((const void *)step_par_kernel<M, EPBX, HF, P>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess)
             return TG_ERR_HIP;
         attr_set.fetch_or(bit, std::memory_order_acq_rel);
     }
-    hipLaunchKernelGGL((step_par_kernel<M, M::EPB, HF, P>), dim3((a.N + M::EPB - 1) / M::EPB), dim3(M::EPB * M::LPE),
+    hipLaunchKernelGGL((step_par_kernel<M, EPBX, HF, P>), dim3((a.N + EPBX - 1) / EPBX), dim3(EPBX * M::LPE),
                        bytes, stream, a, pa);
     return 0;
 }
