@@ -66,17 +66,6 @@ const char *const HEADERS[] = {"articulation_kernels.h", "step_par.h", "tg_math.
                                "../../include/tgsim.h", "../../include/tg_gogoro.h",
                                "../../include/tg_gogoro_paper.h", "../../include/tg_walk.h"};
 
-// the compiled-in units' pass configuration (tg_kernels.h TG_SEG), so a
-// run-time model runs the same kernel code as a compiled one
-#define TG_JIT_STR2(x) #x
-#define TG_JIT_STR(x) TG_JIT_STR2(x)
-#define JIT_SEG_OPT "-DTG_SEG=" TG_JIT_STR(TG_SEG)
-#ifdef TG_SEG_NOMERGE
-#define JIT_SEG_OPT2 "-DTG_SEG_NOMERGE"
-#else
-#define JIT_SEG_OPT2 "-DTG_SEG_MERGE"
-#endif
-
 uint64_t fnv1a(uint64_t h, const std::string &s) {
     for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
     return h;
@@ -123,8 +112,7 @@ int compile(const std::string &src, const std::string &incdir, JitCode &out, std
     const std::string inc = "-I" + incdir;
     // the flags of the compiled-in articulation unit (build_ext.py UNITS)
     const char *opts[] = {"--offload-arch=gfx950", "-std=c++17", "-O3", "-ffast-math",
-                          "-ffp-contract=fast-honor-pragmas", "-munsafe-fp-atomics", "-fno-slp-vectorize", "-DTG_JIT=1",
-                          JIT_SEG_OPT, JIT_SEG_OPT2, inc.c_str()};
+                          "-ffp-contract=fast-honor-pragmas", "-munsafe-fp-atomics", "-fno-slp-vectorize", "-DTG_JIT=1", inc.c_str()};
     const hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof opts / sizeof opts[0]), opts);
     if (rc != HIPRTC_SUCCESS) {
         size_t n = 0;
@@ -228,7 +216,6 @@ int jit_compile(uint64_t hash, const char *struct_name, const char *model_source
     const std::string inc = include_dir && *include_dir ? include_dir : default_include_dir();
     uint64_t digest = fnv1a(14695981039346656037ull, struct_name);
     digest = fnv1a(digest, model_source);
-    digest = fnv1a(digest, JIT_SEG_OPT JIT_SEG_OPT2);
     for (const char *h : HEADERS) {
         std::string t;
         if (!read_file(inc + "/" + h, t)) {

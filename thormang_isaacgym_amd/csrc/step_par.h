@@ -133,196 +133,6 @@ __device__ __forceinline__ void stR(const LE &s, int g, const M3 &R) { stm3(s, g
 // per-group model table in LDS (ints; axis as float bits), built once per block
 enum : int { GI_PARENT = 0, GI_DOF = 1, GI_JT = 2, GI_NCH = 3, GI_CH = 4 };
 
-// ---- Two tree levels per schedule step ("segments", round 3) ----
-// A schedule step costs its arithmetic plus a fixed LDS round trip (the
-// parent's values stored by the previous step, read back by this one).  A
-// segment puts a group and one child on one lane: the child is computed from
-// the group's registers, so a chain of n groups takes ceil(n / 2) steps.
-//   forward passes (1a, 3, the impulse top-down pass): slot = (g1, c) -- g1
-//     from its parent's LDS values, then c (a child of g1) from g1's
-//     registers; the two lanes of a pair (M::PAIR) share g1 and may take two
-//     different children.  Thormang: 9 steps -> 5.
-//   backward pass (2b): slot = (g2, g1) -- g2 (its children gathered from
-//     LDS), then its parent g1 when g2 is g1's last child to finish (the other
-//     children done at earlier steps): g2's contribution to g1 never goes
-//     through LDS.  Thormang: 9 steps -> 6.
-// Built at compile time from the model's tree (greedy list schedule, longest
-// remaining path first), so run-time (JIT) models get them too.
-template <class M> struct SegSched {
-    static constexpr int MS = M::NG > 1 ? M::NG : 1;   // steps (upper bound)
-    struct Arr {
-        int nf, nb;
-        int fg[MS][M::SL], fc[MS][M::SL][2];   // forward: g1, the two halves' child (0: none)
-        int bg2[MS][M::SL], bg1[MS][M::SL];    // backward: g2, g1 (0: none)
-    };
-    static constexpr Arr make() {
-        Arr a{};
-        int height[MS] = {}, depth[MS] = {};
-        for (int g = M::NG - 1; g > 0; --g) {
-            const int p = M::parent[g];
-            if (height[g] + 1 > height[p]) height[p] = height[g] + 1;
-        }
-        for (int g = 1; g < M::NG; ++g) depth[g] = depth[M::parent[g]] + 1;
-        // forward
-        int st[MS] = {};
-        for (int g = 0; g < M::NG; ++g) st[g] = -2;   // -2: not scheduled
-        st[0] = -1;
-        int left = M::NG - 1, t = 0;
-        while (left > 0 && t < MS) {
-            int ns = 0;
-            while (ns < M::SL) {
-                int b = -1;
-                for (int g = 1; g < M::NG; ++g) {
-                    const int p = M::parent[g];
-                    if (st[g] != -2 || st[p] == -2 || st[p] >= t) continue;
-                    if (b < 0 || height[g] > height[b]) b = g;
-                }
-                if (b < 0) break;
-                st[b] = t;
-                --left;
-                int c0 = 0, c1 = 0;
-                for (int k = 0; k < M::nchild[b]; ++k) {
-                    const int c = M::child[b][k];
-                    if (c0 == 0 || height[c] > height[c0]) { c1 = c0; c0 = c; }
-                    else if (c1 == 0 || height[c] > height[c1]) c1 = c;
-                }
-                if (!M::PAIR) c1 = 0;
-                if (c0) { st[c0] = t; --left; }
-                if (c1) { st[c1] = t; --left; }
-                a.fg[t][ns] = b;
-                a.fc[t][ns][0] = c0;
-                a.fc[t][ns][1] = c1 ? c1 : c0;
-                ++ns;
-            }
-            ++t;
-        }
-        a.nf = t > 0 ? t : 1;
-        // backward
-        for (int g = 0; g < M::NG; ++g) st[g] = -2;
-        left = M::NG - 1;
-        t = 0;
-        while (left > 0 && t < MS) {
-            int ns = 0;
-            while (ns < M::SL) {
-                int b = -1;
-                for (int g = 1; g < M::NG; ++g) {
-                    if (st[g] != -2) continue;
-                    bool ok = true;
-                    for (int k = 0; k < M::nchild[g]; ++k) {
-                        const int c = M::child[g][k];
-                        if (st[c] == -2 || st[c] >= t) ok = false;
-                    }
-                    if (!ok) continue;
-                    if (b < 0 || depth[g] > depth[b]) b = g;
-                }
-                if (b < 0) break;
-                st[b] = t;
-                --left;
-                const int p = M::parent[b];
-#ifdef TG_SEG_NOMERGE   // developer switch: the backward schedule without two-level slots
-                bool merge = false;
-#else
-                bool merge = p > 0 && st[p] == -2;
-#endif
-                for (int k = 0; merge && k < M::nchild[p]; ++k) {
-                    const int c = M::child[p][k];
-                    if (c != b && (st[c] == -2 || st[c] >= t)) merge = false;
-                }
-                if (merge) { st[p] = t; --left; }
-                a.bg2[t][ns] = b;
-                a.bg1[t][ns] = merge ? p : 0;
-                ++ns;
-            }
-            ++t;
-        }
-        a.nb = t > 0 ? t : 1;
-        return a;
-    }
-    static constexpr Arr tab = make();
-    static constexpr int NF = tab.nf, NB = tab.nb;
-    static constexpr int slot_of(int lane) { return lane % M::SL; }
-    static constexpr int half_of(int lane) { return M::PAIR ? lane / M::SL : 0; }
-    // forward word of (step, lane): g1 | c << 8 | parent(g1) << 16 | prismatic(g1) << 24 | prismatic(c) << 25
-    static constexpr int fword(int t, int lane) {
-        const int g1 = (M::PAIR || lane < M::SL) ? tab.fg[t][slot_of(lane)] : 0;
-        if (g1 <= 0) return 0;
-        const int c = tab.fc[t][slot_of(lane)][half_of(lane)];
-        return g1 | c << 8 | M::parent[g1] << 16 | (M::jtype[g1] == TG_JOINT_PRISMATIC ? 1 : 0) << 24 |
-               (c > 0 && M::jtype[c] == TG_JOINT_PRISMATIC ? 1 : 0) << 25;
-    }
-    // the step's largest child counts (compile-time gather widths of pass 2b):
-    // of g2, and of g1 other than g2; whether any slot carries a g1
-    static constexpr int bn2(int t) {
-        int m = 0;
-        for (int l = 0; l < M::SL; ++l)
-            if (tab.bg2[t][l] > 0 && M::nchild[tab.bg2[t][l]] > m) m = M::nchild[tab.bg2[t][l]];
-        return m;
-    }
-    static constexpr int bn1(int t) {
-        int m = 0;
-        for (int l = 0; l < M::SL; ++l)
-            if (tab.bg1[t][l] > 0 && M::nchild[tab.bg1[t][l]] - 1 > m) m = M::nchild[tab.bg1[t][l]] - 1;
-        return m;
-    }
-    static constexpr bool bseg(int t) {
-        for (int l = 0; l < M::SL; ++l)
-            if (tab.bg1[t][l] > 0) return true;
-        return false;
-    }
-    static constexpr bool fseg(int t) {
-        for (int l = 0; l < M::SL; ++l)
-            if (tab.fg[t][l] > 0 && tab.fc[t][l][0] > 0) return true;
-        return false;
-    }
-};
-// the backward descriptor of (step, lane), one int4:
-//   x = g2 | g1 << 8 | prismatic(g2) << 16 | prismatic(g1) << 17
-//   y = g2's children: count | c0 << 8 | c1 << 16 | c2 << 24
-//   z = g1's children other than g2, same packing
-template <class M> struct BSegTab {
-    static_assert(M::NG <= 255, "8-bit group ids");
-    using S = SegSched<M>;
-    struct Arr {
-        int d[S::NB * M::LPE * 4];
-    };
-    static constexpr Arr make() {
-        Arr a{};
-        for (int t = 0; t < S::NB; ++t)
-            for (int lane = 0; lane < M::LPE; ++lane) {
-                int *p = a.d + 4 * (t * M::LPE + lane);
-                const int sl = S::slot_of(lane);
-                const int g2 = (M::PAIR || lane < M::SL) ? S::tab.bg2[t][sl] : 0;
-                if (g2 <= 0) continue;
-                const int g1 = S::tab.bg1[t][sl];
-                p[0] = g2 | g1 << 8 | (M::jtype[g2] == TG_JOINT_PRISMATIC ? 1 : 0) << 16 |
-                       (g1 > 0 && M::jtype[g1] == TG_JOINT_PRISMATIC ? 1 : 0) << 17;
-                p[1] = M::nchild[g2];
-                for (int k = 0; k < M::nchild[g2]; ++k) p[1] |= M::child[g2][k] << (8 + 8 * k);
-                if (g1 > 0) {
-                    int n = 0;
-                    for (int k = 0; k < M::nchild[g1]; ++k)
-                        if (M::child[g1][k] != g2) p[2] |= M::child[g1][k] << (8 + 8 * n++);
-                    p[2] |= n;
-                }
-            }
-        return a;
-    }
-    static constexpr Arr tab = make();
-};
-template <class M> struct FSegTab {
-    using S = SegSched<M>;
-    struct Arr {
-        int v[S::NF * M::LPE];
-    };
-    static constexpr Arr make() {
-        Arr a{};
-        for (int t = 0; t < S::NF; ++t)
-            for (int lane = 0; lane < M::LPE; ++lane) a.v[t * M::LPE + lane] = S::fword(t, lane);
-        return a;
-    }
-    static constexpr Arr tab = make();
-};
-
 template <class M> struct ParLayout {
     static constexpr int K = M::NROWS;
     static constexpr int GIW = GI_CH + M::MAXC;
@@ -352,10 +162,7 @@ template <class M> struct ParLayout {
     static constexpr int T_ZERO = T_PACK + (M::NSTEP + 1) / 2 * M::LPE;  // 32 zero floats (PackTab NPW)
     // GogoroPaper (FUSED bit 4): the envs' reward-term-7 partials
     static constexpr int T_T7 = T_ZERO + 32;
-    // segment schedules (SegSched): forward words [NF][LPE], backward int4 [NB][LPE]
-    static constexpr int T_FSEG = T_T7 + ((M::FUSED & 4) ? M::EPB : 0);
-    static constexpr int T_BSEG = (T_FSEG + SegSched<M>::NF * M::LPE + 3) & ~3;
-    static constexpr int T_TOTAL = T_BSEG + 4 * SegSched<M>::NB * M::LPE;
+    static constexpr int T_TOTAL = T_T7 + ((M::FUSED & 4) ? M::EPB : 0);
     // SEPC (when the LDS has room): pass 2 writes each group's contribution to
     // its parent (I^a 21 at +0, p^a 6 at +24) and pass 3 its acceleration (+0)
     // into a separate 32-float block, so pass 1's rigid inertias and bias
@@ -720,8 +527,6 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
     }
     for (int i = tid; i < PackTab<M>::NPW * LPE; i += EPB * LPE) tab[PL::T_PACK + i] = PackTab<M>::tab.v[i];
     for (int i = tid; i < 32; i += EPB * LPE) tab[PL::T_ZERO + i] = 0;
-    for (int i = tid; i < SegSched<M>::NF * LPE; i += EPB * LPE) tab[PL::T_FSEG + i] = FSegTab<M>::tab.v[i];
-    for (int i = tid; i < 4 * SegSched<M>::NB * LPE; i += EPB * LPE) tab[PL::T_BSEG + i] = BSegTab<M>::tab.d[i];
     for (int i = tid; i < M::NCG * M::MAXD; i += EPB * LPE) tab[PL::T_CPATH + i] = M::cpath[i / M::MAXD][i % M::MAXD];
 
     const LE s{lds_raw + le * PL::ES};
@@ -827,23 +632,6 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
     int pkw[NPW];
 #pragma unroll
     for (int w = 0; w < NPW; ++w) pkw[w] = tab[PL::T_PACK + w * LPE + sub];
-    // the segment schedule's forward words (registers, laundered like the
-    // packed words) and backward descriptors (LDS, one int4 a step)
-    using SS = SegSched<M>;
-    int fsw[SS::NF];
-#pragma unroll
-    for (int t = 0; t < SS::NF; ++t) fsw[t] = tab[PL::T_FSEG + t * LPE + sub];
-    auto fwd = [&](int t) {
-        int w = fsw[t];
-        __asm__ volatile("" : "+v"(w));
-        return w;
-    };
-    auto bdsc = [&](int t) { return reinterpret_cast<const I4 *>(tab + PL::T_BSEG)[t * LPE + sub]; };
-    auto f_g1 = [](int w) { return bounded(w & 255, 0, M::NG); };
-    auto f_c = [](int w) { return bounded((w >> 8) & 255, 0, M::NG); };
-    auto f_par = [](int w) { return bounded((w >> 16) & 255, 0, M::NG); };
-    auto f_jt1 = [](int w) { return (w >> 24) & 1 ? TG_JOINT_PRISMATIC : TG_JOINT_REVOLUTE; };
-    auto f_jt2 = [](int w) { return (w >> 25) & 1 ? TG_JOINT_PRISMATIC : TG_JOINT_REVOLUTE; };
     // step t's (group, parent, joint type) from the packed words (descriptor
     // fields x, y and z's joint type), or the LDS descriptor for NG > 128
 #ifndef TG_PACK_MASK
@@ -1205,93 +993,37 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         }
         if (lead) stsv(s, F_V, v0);
         TG_SYNC();
-        // a child's root-frame pose and velocity from its parent's (Rp, Pp,
-        // vp), its joint placement ck (12) and its joint position / velocity
-        auto child_pose = [&](const M3 &Rp, V3 Pp, const SV &vp, const float *ck, float qg, float qdg, int jt,
-                              M3 &Rg, V3 &Pg, SV &vg) {
-            M3 Rpc;   // child -> parent rotation at q, then the root-frame pose
-#pragma unroll
-            for (int k = 0; k < 9; ++k) Rpc.a[k] = ck[k];
-            V3 tr = v3(ck[9], ck[10], ck[11]);
-            if (all_revolute<M>() || jt == TG_JOINT_REVOLUTE) {   // Rpc * Rz(q)
-                float sq, cq;
-                tg_sincos(qg, &sq, &cq);
-#pragma unroll
-                for (int r = 0; r < 3; ++r) {
-                    const float c0 = Rpc.a[3 * r], c1 = Rpc.a[3 * r + 1];
-                    Rpc.a[3 * r] = c0 * cq + c1 * sq;
-                    Rpc.a[3 * r + 1] = c1 * cq - c0 * sq;
-                }
-            } else {
-                tr = tr + qg * v3(Rpc.a[2], Rpc.a[5], Rpc.a[8]);
-            }
-            Rg = mul(Rp, Rpc);
-            Pg = Pp + mul(Rp, tr);
-            const SV Sg = motion_Sm<M>(jt, v3(Rg.a[2], Rg.a[5], Rg.a[8]), Pg);
-            vg = vp + qdg * Sg;
-        };
-        auto st_pose = [&](int g, const M3 &Rg, V3 Pg, const SV &vg) {
-            stR(s, g, Rg);
-            stv3(s, g * GF + F_P, Pg);
-            stsv(s, g * GF + F_V, vg);
-        };
-        if constexpr ((TG_SEG & 1) != 0) {
-            // segments (SegSched): g1 from its parent's LDS values, then the
-            // lane's child c from g1's registers; both groups' joint
-            // placements one step ahead
-            auto body1s = [&](int w, const float *ck) {
-                const int g1 = f_g1(w);
-                if (g1 > 0) {
-                    const int c = f_c(w), par = f_par(w);
-                    const M3 Rp = ldR(s, par);
-                    const V3 Pp = ldv3(s, par * GF + F_P);
-                    const SV vp = ldsv(s, par * GF + F_V);
-                    const float q1 = s(g1 * GF + F_Q), qd1 = s(g1 * GF + F_QD);
-                    const float q2 = s(c * GF + F_Q), qd2 = s(c * GF + F_QD);   // (c = 0: unused)
-                    M3 R1;
-                    V3 P1;
-                    SV v1;
-                    child_pose(Rp, Pp, vp, ck, q1, qd1, f_jt1(w), R1, P1, v1);
-                    st_pose(g1, R1, P1, v1);
-                    if (c > 0) {
-                        M3 R2;
-                        V3 P2;
-                        SV v2;
-                        child_pose(R1, P1, v1, ck + 12, q2, qd2, f_jt2(w), R2, P2, v2);
-                        st_pose(c, R2, P2, v2);
-                    }
-                }
-                TG_SYNC();
-            };
-            float kr[2][24];
-            {
-                const int w0 = fwd(0);
-                load_kin(f_g1(w0), kr[0]);
-                load_kin(f_c(w0), kr[0] + 12);
-            }
-#pragma unroll
-            for (int t = 0; t < SS::NF; ++t) {
-                if (t + 1 < SS::NF) {
-                    const int wn = fwd(t + 1);
-                    load_kin(f_g1(wn), kr[(t + 1) % 2]);
-                    load_kin(f_c(wn), kr[(t + 1) % 2] + 12);
-                }
-                body1s(fwd(t), kr[t % 2]);
-            }
-        } else {
         auto body1 = [&](const I4 &dc, const float *ck) {
             const int g = dc.x;
             if (g > 0) {
-                const int par = dc.y;
+                const int o = g * GF, par = dc.y, jt = d_jt(dc);
                 const M3 Rp = ldR(s, par);
                 const V3 Pp = ldv3(s, par * GF + F_P);
                 const SV vp = ldsv(s, par * GF + F_V);
-                const float qg = s(g * GF + F_Q), qdg = s(g * GF + F_QD);
-                M3 Rg;
-                V3 Pg;
-                SV vg;
-                child_pose(Rp, Pp, vp, ck, qg, qdg, d_jt(dc), Rg, Pg, vg);
-                st_pose(g, Rg, Pg, vg);
+                const float qg = s(o + F_Q), qdg = s(o + F_QD);
+                M3 Rpc;   // child -> parent rotation at q, then the root-frame pose
+#pragma unroll
+                for (int k = 0; k < 9; ++k) Rpc.a[k] = ck[k];
+                V3 tr = v3(ck[9], ck[10], ck[11]);
+                if (all_revolute<M>() || jt == TG_JOINT_REVOLUTE) {   // Rpc * Rz(q)
+                    float sq, cq;
+                    tg_sincos(qg, &sq, &cq);
+#pragma unroll
+                    for (int r = 0; r < 3; ++r) {
+                        const float c0 = Rpc.a[3 * r], c1 = Rpc.a[3 * r + 1];
+                        Rpc.a[3 * r] = c0 * cq + c1 * sq;
+                        Rpc.a[3 * r + 1] = c1 * cq - c0 * sq;
+                    }
+                } else {
+                    tr = tr + qg * v3(Rpc.a[2], Rpc.a[5], Rpc.a[8]);
+                }
+                const M3 Rg = mul(Rp, Rpc);
+                const V3 Pg = Pp + mul(Rp, tr);
+                stR(s, g, Rg);
+                stv3(s, o + F_P, Pg);
+                const SV Sg = motion_Sm<M>(jt, v3(Rg.a[2], Rg.a[5], Rg.a[8]), Pg);
+                const SV vg = vp + qdg * Sg;
+                stsv(s, o + F_V, vg);
             }
             TG_SYNC();
         };
@@ -1313,7 +1045,6 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                 load_kin(dr[(t + 2) % 3].x, kr[(t + 2) % 3]);
             }
             body1(dr[t % 3], kr[t % 3]);
-        }
         }
 #ifdef TG_DUMMY_STEPS
         // developer ablation: TG_DUMMY_STEPS dependent LDS round trips with no
@@ -1503,251 +1234,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         TG_SYNC();
         TG_PROF(17)
         // ---- pass 2b: schedule backward, children contributions gathered
-        if constexpr ((TG_SEG & 2) != 0) {
-        // segments (SegSched backward): g2 (children gathered from LDS), then,
-        // where the slot carries it, g2's parent g1 with g2's contribution
-        // added from registers and g1's other children (done at earlier steps)
-        // from LDS.  Every load of the step is issued before its first store.
-        auto bjt = [](int x, int sh) { return (x >> sh) & 1 ? TG_JOINT_PRISMATIC : TG_JOINT_REVOLUTE; };
-        auto bch = [](int pk, int c) { return bounded((pk >> (8 + 8 * c)) & 255, 0, M::NG); };
-        I4 dn = bdsc(0);
         if constexpr (M::PAIR) {
-        // lane pairs split each group's update as in the unsegmented pass below
-        const int hh = sub >= M::SL ? 1 : 0;
-        const bool hb = hh != 0;
-        struct HB { float X[6], Bm[9], ph[3], cb1[3], cb2[3], c0, tau, al, c1; SV S; };
-        struct HO { float X[6], Y[9], pav[3]; V3 U; float Dinv, u; };
-        auto hb_load = [&](int g, int jt, HB &b) {
-            const int o = g * GF;
-#pragma unroll
-            for (int k = 0; k < 6; ++k) b.X[k] = s(o + F_IA + 15 * hh + k);
-#pragma unroll
-            for (int k = 0; k < 9; ++k) b.Bm[k] = s(o + F_IA + 6 + k);
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                b.ph[k] = s(o + F_PA + 3 * hh + k);
-                b.cb1[k] = s(o + F_V + 3 * hh + k);
-                b.cb2[k] = s(o + F_V + 3 - 3 * hh + k);
-            }
-            b.S = ldSm<M>(s, g, jt);
-            b.c0 = s(o + F_DINV);
-            b.tau = s(o + F_UU);
-            b.al = s(o + F_QDS);
-            b.c1 = s(o + F_C1);
-        };
-        // children contributions (count | ids, SegSched packing): every load
-        // issued before the first add; absent children read the zero block
-        auto hb_gather = [&](auto NCc, int pk, HB &b) {
-            constexpr int n = decltype(NCc)::value;
-            if constexpr (n > 0) {
-                float cx[n][6], cbm[n][9], cp[n][3];
-#pragma unroll
-                for (int c = 0; c < n; ++c) {
-                    const bool has = c < (pk & 255);
-                    const int ch = bch(pk, c);
-                    const float *pi = has ? s.b + ia_c(ch) : zeros, *pp = has ? s.b + pa_c(ch) : zeros;
-#pragma unroll
-                    for (int k = 0; k < 6; ++k) cx[c][k] = pi[15 * hh + k];
-#pragma unroll
-                    for (int k = 0; k < 9; ++k) cbm[c][k] = pi[6 + k];
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) cp[c][k] = pp[3 * hh + k];
-                }
-#pragma unroll
-                for (int c = 0; c < n; ++c) {
-#pragma unroll
-                    for (int k = 0; k < 6; ++k) b.X[k] += cx[c][k];
-#pragma unroll
-                    for (int k = 0; k < 9; ++k) b.Bm[k] += cbm[c][k];
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) b.ph[k] += cp[c][k];
-                }
-            }
-        };
-        // the half's share of the group's update (add: a segment child's
-        // contribution, already in the half's orientation)
-        auto hb_core = [&](HB &b, const HO *add) {
-            HO r;
-            float Y[9];
-            Y[0] = b.Bm[0]; Y[4] = b.Bm[4]; Y[8] = b.Bm[8];
-            Y[1] = hb ? b.Bm[3] : b.Bm[1]; Y[3] = hb ? b.Bm[1] : b.Bm[3];
-            Y[2] = hb ? b.Bm[6] : b.Bm[2]; Y[6] = hb ? b.Bm[2] : b.Bm[6];
-            Y[5] = hb ? b.Bm[7] : b.Bm[5]; Y[7] = hb ? b.Bm[5] : b.Bm[7];
-            if (add) {
-#pragma unroll
-                for (int k = 0; k < 6; ++k) b.X[k] += add->X[k];
-#pragma unroll
-                for (int k = 0; k < 9; ++k) Y[k] += add->Y[k];
-#pragma unroll
-                for (int k = 0; k < 3; ++k) b.ph[k] += add->pav[k];
-            }
-            const V3 S1 = hb ? b.S.v : b.S.w, S2 = hb ? b.S.w : b.S.v;
-            const V3 Uv = symmul(b.X, S1) + bmul(Y, S2);
-            const float Uh[3] = {Uv.x, Uv.y, Uv.z};
-            const float d0 = dot(S1, Uv);
-            const float D0 = d0 + pair_swap(d0);   // S.U, without the armature (folded into c0, tau)
-            const float sp = dot(S1, v3(b.ph[0], b.ph[1], b.ph[2]));
-            const float SpA = sp + pair_swap(sp);
-            const float Dinv = 1.0f / (b.c1 * D0 + b.c0);
-            const float u = b.tau + b.al * D0 - SpA;
-            float Uo[3], DUh[3], DUo[3], Pf[3], Qf[3];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) Uo[k] = pair_swap(Uh[k]);
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                DUh[k] = Dinv * Uh[k];
-                DUo[k] = Dinv * Uo[k];
-                Pf[k] = hb ? Uh[k] : DUh[k];   // B entries from the same two factors on both halves
-                Qf[k] = hb ? DUo[k] : Uo[k];
-            }
-            const int ii[6] = {0, 1, 2, 0, 0, 1}, jj[6] = {0, 1, 2, 1, 2, 2};
-#pragma unroll
-            for (int k = 0; k < 6; ++k) r.X[k] = b.X[k] - DUh[ii[k]] * Uh[jj[k]];
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-#pragma unroll
-                for (int j = 0; j < 3; ++j) r.Y[3 * i + j] = Y[3 * i + j] - Pf[i] * Qf[j];
-            const float ud = u * Dinv;
-            const V3 pav = v3(b.ph[0], b.ph[1], b.ph[2]) + symmul(r.X, v3(b.cb1[0], b.cb1[1], b.cb1[2])) +
-                           bmul(r.Y, v3(b.cb2[0], b.cb2[1], b.cb2[2])) + ud * Uv;
-            r.pav[0] = pav.x; r.pav[1] = pav.y; r.pav[2] = pav.z;
-            r.U = Uv;
-            r.Dinv = Dinv;
-            r.u = u;
-            return r;
-        };
-        auto hb_store = [&](int g, const HO &r, bool contrib) {
-            const int o = g * GF;
-            stv3(s, o + F_U + 3 * hh, r.U);
-            s(o + F_DINV) = r.Dinv;
-            s(o + F_UU) = r.u;
-            if (contrib) {   // contribution to the parent (same frame: no transform)
-#pragma unroll
-                for (int k = 0; k < 6; ++k) s(ia_c(g) + 15 * hh + k) = r.X[k];
-                if (!hb) {
-#pragma unroll
-                    for (int k = 0; k < 9; ++k) s(ia_c(g) + 6 + k) = r.Y[k];
-                }
-                stv3(s, pa_c(g) + 3 * hh, v3(r.pav[0], r.pav[1], r.pav[2]));
-            }
-        };
-        static_for<0, SS::NB>([&](auto TT) {
-            constexpr int t = decltype(TT)::value;
-            const I4 d = dn;
-            if constexpr (t + 1 < SS::NB) dn = bdsc(t + 1);
-            const int g2 = bounded(d.x & 255, 0, M::NG), g1 = bounded((d.x >> 8) & 255, 0, M::NG);
-            if (g2 > 0) {
-                HB b2, b1;
-                hb_load(g2, bjt(d.x, 16), b2);
-                hb_gather(IntC<(SS::bn2(t) < 3 ? SS::bn2(t) : 3)>{}, d.y, b2);
-                if constexpr (SS::bseg(t)) {
-                    hb_load(g1 > 0 ? g1 : g2, bjt(d.x, 17), b1);   // (no g1: a harmless reload)
-                    hb_gather(IntC<(SS::bn1(t) < 3 ? SS::bn1(t) : 3)>{}, d.z, b1);
-                }
-                const HO r2 = hb_core(b2, nullptr);
-                if constexpr (SS::bseg(t)) {
-                    if (g1 > 0) {
-                        const HO r1 = hb_core(b1, &r2);
-                        hb_store(g2, r2, false);
-                        hb_store(g1, r1, true);
-                    } else {
-                        hb_store(g2, r2, true);
-                    }
-                } else {
-                    hb_store(g2, r2, true);
-                }
-            }
-            TG_SYNC();
-        });
-        } else {
-        struct NB2 { SI IA; SV pA, S, cb; float c0, tau, al, c1; };
-        auto nb_load = [&](int g, int jt, NB2 &b) {
-            const int o = g * GF;
-            b.IA = ldsi(s, o + F_IA);
-            b.pA = ldsv(s, o + F_PA);
-            b.S = ldSm<M>(s, g, jt);
-            b.cb = ldsv(s, o + F_V);
-            b.c0 = s(o + F_DINV);
-            b.tau = s(o + F_UU);
-            b.al = s(o + F_QDS);
-            b.c1 = s(o + F_C1);
-        };
-        auto nb_gather = [&](auto NCc, int pk, NB2 &b) {
-            constexpr int n = decltype(NCc)::value;
-            if constexpr (n > 0) {
-                SI ci[n];
-                SV cv[n];
-#pragma unroll
-                for (int c = 0; c < n; ++c) {
-                    const bool has = c < (pk & 255);
-                    const int ch = bch(pk, c);
-                    const float *pi = has ? s.b + ia_c(ch) : zeros, *pp = has ? s.b + pa_c(ch) : zeros;
-                    ci[c] = ldsi(LE{(float *)__builtin_assume_aligned(pi, PL::ES % 4 == 0 ? 16 : 8)}, 0);
-                    cv[c] = ldsv(LE{(float *)__builtin_assume_aligned(pp, PL::ES % 4 == 0 ? 16 : 8)}, 0);
-                }
-#pragma unroll
-                for (int c = 0; c < n; ++c) {
-                    si_add(b.IA, ci[c]);
-                    b.pA = b.pA + cv[c];
-                }
-            }
-        };
-        struct NO { SI Ia; SV pa, U; float Dinv, u; };
-        auto nb_core = [&](NB2 &b, const NO *add) {
-            if (add) {
-                si_add(b.IA, add->Ia);
-                b.pA = b.pA + add->pa;
-            }
-            NO r;
-            r.U = mul(b.IA, b.S);
-            const float D0 = dot(b.S, r.U);   // without the armature (folded into c0, tau)
-            r.Dinv = 1.0f / (b.c1 * D0 + b.c0);
-            r.u = b.tau + b.al * D0 - dot(b.S, b.pA);
-            r.Ia = b.IA;
-            si_sub_outer(r.Ia, r.U, r.Dinv);
-            r.pa = b.pA + mul(r.Ia, b.cb) + (r.u * r.Dinv) * r.U;
-            return r;
-        };
-        auto nb_store = [&](int g, const NO &r, bool contrib) {
-            const int o = g * GF;
-            stsv(s, o + F_U, r.U);
-            s(o + F_DINV) = r.Dinv;
-            s(o + F_UU) = r.u;
-            if (contrib) {
-                stsi(s, ia_c(g), r.Ia);   // contribution to the parent (same frame: no transform)
-                stsv(s, pa_c(g), r.pa);
-            }
-        };
-        static_for<0, SS::NB>([&](auto TT) {
-            constexpr int t = decltype(TT)::value;
-            const I4 d = dn;
-            if constexpr (t + 1 < SS::NB) dn = bdsc(t + 1);
-            const int g2 = bounded(d.x & 255, 0, M::NG), g1 = bounded((d.x >> 8) & 255, 0, M::NG);
-            if (g2 > 0) {
-                NB2 b2, b1;
-                nb_load(g2, bjt(d.x, 16), b2);
-                nb_gather(IntC<(SS::bn2(t) < 3 ? SS::bn2(t) : 3)>{}, d.y, b2);
-                if constexpr (SS::bseg(t)) {
-                    nb_load(g1 > 0 ? g1 : g2, bjt(d.x, 17), b1);
-                    nb_gather(IntC<(SS::bn1(t) < 3 ? SS::bn1(t) : 3)>{}, d.z, b1);
-                }
-                const NO r2 = nb_core(b2, nullptr);
-                if constexpr (SS::bseg(t)) {
-                    if (g1 > 0) {
-                        const NO r1 = nb_core(b1, &r2);
-                        nb_store(g2, r2, false);
-                        nb_store(g1, r1, true);
-                    } else {
-                        nb_store(g2, r2, true);
-                    }
-                } else {
-                    nb_store(g2, r2, true);
-                }
-            }
-            TG_SYNC();
-        });
-        }
-        } else if constexpr (M::PAIR) {
         // Lane pairs split the group's update as the same instructions on
         // different data: with I = [A B; B^T C] acting on (w, v), lane half 0
         // computes the angular rows (X = A, Y = B, S1 = S.w, S2 = S.v), half 1
@@ -1932,56 +1419,12 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         // untouched by the earlier steps) are loaded one step ahead, so only
         // the parent's acceleration is waited on along the chain
         struct Own { SV cb, U, S; float qd, uu, dinv, te, K, eff; };
-        auto ld_own_g = [&](int g, int jt) {
-            const int o = g * GF;
-            return Own{ldsv(s, o + F_V), ldsv(s, o + F_U), ldSm<M>(s, g, jt),
+        auto ld_own = [&](const I4 &dc) {
+            const int g = max(dc.x, 0), o = g * GF;
+            return Own{ldsv(s, o + F_V), ldsv(s, o + F_U), ldSm<M>(s, g, d_jt(dc)),
                        s(o + F_QD), s(o + F_UU), s(o + F_DINV),
                        s(o + F_CL), s(o + F_CL + 1), s(o + F_CL + 2)};
         };
-        auto ld_own = [&](const I4 &dc) { return ld_own_g(max(dc.x, 0), d_jt(dc)); };
-        // group g's acceleration from its parent's, stored; returned for a segment's child
-        auto acc3 = [&](int g, const Own &w, const SV &apar) {
-            const int o = g * GF;
-            const SV ap = apar + w.cb;   // cb: pass 2a
-            const float qdd = (w.uu - dot(w.U, ap)) * w.dinv;
-            const SV ag = ap + qdd * w.S;
-            stsv(s, ac_s(g), ag);
-            s(o + F_QDS) = w.qd + h * qdd;
-            if (cp == 0) {
-                s(o + F_UU) = qdd;
-                const float ti = w.te - w.K * qdd;
-                const bool sat = w.K >= 0.f && fabsf(ti) > w.eff;
-                if (sat) s(PL::FLG) = 1.f;
-                // (Woodbury: the drive's clamp side, F_C1 being dead after pass 2b)
-                if constexpr (PL::WOOD) s(o + F_C1) = sat ? (ti > 0.f ? 1.f : -1.f) : 0.f;
-            }
-            return ag;
-        };
-        if constexpr ((TG_SEG & 4) != 0) {
-            // segments: g1's inputs one step ahead, the child's issued at the
-            // step start (behind the parent's acceleration, ahead of g1's stores)
-            Own ow[2];
-            ow[0] = ld_own_g(f_g1(fwd(0)), f_jt1(fwd(0)));
-            static_for<0, SS::NF>([&](auto TT) {
-                constexpr int t = decltype(TT)::value;
-                const int w = fwd(t);
-                const int g1 = f_g1(w), c = f_c(w);
-                const SV apar = ldsv(s, ac_s(f_par(w)));
-                Own wc{};
-                if constexpr (SS::fseg(t)) wc = ld_own_g(c, f_jt2(w));
-                if constexpr (t + 1 < SS::NF) {
-                    const int wn = fwd(t + 1);
-                    ow[(t + 1) % 2] = ld_own_g(f_g1(wn), f_jt1(wn));
-                }
-                if (g1 > 0) {
-                    const SV a1 = acc3(g1, ow[t % 2], apar);
-                    if constexpr (SS::fseg(t)) {
-                        if (c > 0) acc3(c, wc, a1);
-                    }
-                }
-                TG_SYNC();
-            });
-        } else {
         I4 dr[2];
         Own ow[2];
         dr[0] = pdsc3(0);
@@ -1989,15 +1432,29 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
 #pragma unroll
         for (int t = 0; t < M::NSTEP; ++t) {
             const I4 dc = dr[t % 2];
+            const Own &w = ow[t % 2];
             const int g = dc.x;
             const SV apar = ldsv(s, ac_s(max(dc.y, 0)));
             if (t + 1 < M::NSTEP) {
                 dr[(t + 1) % 2] = pdsc3(t + 1);
                 ow[(t + 1) % 2] = ld_own(dr[(t + 1) % 2]);
             }
-            if (g > 0) acc3(g, ow[t % 2], apar);
+            if (g > 0) {
+                const int o = g * GF;
+                const SV ap = apar + w.cb;   // cb: pass 2a
+                const float qdd = (w.uu - dot(w.U, ap)) * w.dinv;
+                stsv(s, ac_s(g), ap + qdd * w.S);
+                s(o + F_QDS) = w.qd + h * qdd;
+                if (cp == 0) {
+                    s(o + F_UU) = qdd;
+                    const float ti = w.te - w.K * qdd;
+                    const bool sat = w.K >= 0.f && fabsf(ti) > w.eff;
+                    if (sat) s(PL::FLG) = 1.f;
+                    // (Woodbury: the drive's clamp side, F_C1 being dead after pass 2b)
+                    if constexpr (PL::WOOD) s(o + F_C1) = sat ? (ti > 0.f ? 1.f : -1.f) : 0.f;
+                }
+            }
             TG_SYNC();
-        }
         }
         }
         if constexpr (PL::WOOD) {
@@ -2523,55 +1980,11 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                 // pass 3); with velocity iterations the bias-free response rides
                 // along (F_V accelerations, F_QD the stored velocity)
                 struct OwnI { SV U, S; float uu, uv, dinv, qds; };
-                auto ld_own_g = [&](int g, int jt) {
-                    const int o = g * GF;
-                    return OwnI{ldsv(s, o + F_U), ldSm<M>(s, g, jt), s(o + F_UU), s(o + F_C1), s(o + F_DINV),
+                auto ld_own = [&](const I4 &dc) {
+                    const int g = max(dc.x, 0), o = g * GF;
+                    return OwnI{ldsv(s, o + F_U), ldSm<M>(s, g, d_jt(dc)), s(o + F_UU), s(o + F_C1), s(o + F_DINV),
                                 s(o + F_QDS)};
                 };
-                auto ld_own = [&](const I4 &dc) { return ld_own_g(max(dc.x, 0), d_jt(dc)); };
-                struct AccI { SV a, av; };
-                auto impulse_down = [&](int g, const OwnI &w, const AccI &ap) {
-                    const int o = g * GF;
-                    AccI r;
-                    const float x = (w.uu - dot(w.U, ap.a)) * w.dinv;
-                    r.a = ap.a + x * w.S;
-                    stsv(s, o + F_PA, r.a);
-                    s(o + F_QDS) = w.qds + x;
-                    if (vit) {
-                        const float xv = (w.uv - dot(w.U, ap.av)) * w.dinv;
-                        r.av = ap.av + xv * w.S;
-                        stsv(s, o + F_V, r.av);
-                        s(o + F_QD) = w.qds + xv;
-                    } else {
-                        r.av = sv0();
-                    }
-                    return r;
-                };
-                if constexpr ((TG_SEG & 8) != 0) {
-                    // segments: as pass 3 (g1's inputs a step ahead, the child's at the step start)
-                    OwnI ow[2];
-                    ow[0] = ld_own_g(f_g1(fwd(0)), f_jt1(fwd(0)));
-                    static_for<0, SS::NF>([&](auto TT) {
-                        constexpr int t = decltype(TT)::value;
-                        const int w = fwd(t);
-                        const int g1 = f_g1(w), c = f_c(w);
-                        const int op = f_par(w) * GF;
-                        const AccI ap{ldsv(s, op + F_PA), vit ? ldsv(s, op + F_V) : sv0()};
-                        OwnI wc{};
-                        if constexpr (SS::fseg(t)) wc = ld_own_g(c, f_jt2(w));
-                        if constexpr (t + 1 < SS::NF) {
-                            const int wn = fwd(t + 1);
-                            ow[(t + 1) % 2] = ld_own_g(f_g1(wn), f_jt1(wn));
-                        }
-                        if (g1 > 0) {
-                            const AccI a1 = impulse_down(g1, ow[t % 2], ap);
-                            if constexpr (SS::fseg(t)) {
-                                if (c > 0) impulse_down(c, wc, a1);
-                            }
-                        }
-                        TG_SYNC();
-                    });
-                } else {
                 I4 dr[2];
                 OwnI ow[2];
                 dr[0] = pdsc4(0);
@@ -2579,16 +1992,27 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
 #pragma unroll
                 for (int t = 0; t < M::NSTEP; ++t) {
                     const I4 dc = dr[t % 2];
+                    const OwnI &w = ow[t % 2];
                     const int g = dc.x;
                     const int op = max(dc.y, 0) * GF;
-                    const AccI ap{ldsv(s, op + F_PA), vit ? ldsv(s, op + F_V) : sv0()};
+                    const SV ap = ldsv(s, op + F_PA);
+                    const SV av = vit ? ldsv(s, op + F_V) : sv0();
                     if (t + 1 < M::NSTEP) {
                         dr[(t + 1) % 2] = pdsc4(t + 1);
                         ow[(t + 1) % 2] = ld_own(dr[(t + 1) % 2]);
                     }
-                    if (g > 0) impulse_down(g, ow[t % 2], ap);
+                    if (g > 0) {
+                        const int o = g * GF;
+                        const float x = (w.uu - dot(w.U, ap)) * w.dinv;
+                        stsv(s, o + F_PA, ap + x * w.S);
+                        s(o + F_QDS) = w.qds + x;
+                        if (vit) {
+                            const float xv = (w.uv - dot(w.U, av)) * w.dinv;
+                            stsv(s, o + F_V, av + xv * w.S);
+                            s(o + F_QD) = w.qds + xv;
+                        }
+                    }
                     TG_SYNC();
-                }
                 }
             } else {
                 // bottom-up gather, root solve, top-down -- once per multiplier

@@ -12,13 +12,6 @@
 #include "../../include/tg_walk.h"
 #include "../../include/tgsim.h"
 
-// step-kernel passes on the two-levels-per-step schedule (step_par.h
-// SegSched): 1 pass 1a, 2 pass 2b, 4 pass 3, 8 the impulse top-down pass.
-// jit.cpp compiles run-time models with the same value.
-#ifndef TG_SEG
-#define TG_SEG 0
-#endif
-
 namespace tg {
 
 constexpr int TG_PM_MAX_DOF = 64;   // prologue lanes: one wavefront per env, lane = dof
