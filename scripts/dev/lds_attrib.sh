@@ -9,7 +9,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 OUT=${OUT_DIR:-gpurun_out/ldsattr}
 mkdir -p $OUT
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-CTR="SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU"
+CTR=${CTR:-"SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU"}
 for task in ${TASKS:-ThormangWalk Gogoro}; do
   for k in ${STOPS:-0 16 1 17 18 2 3 4 5 6 7 8 full}; do
     lib=thormang_isaacgym_amd/libtgsim_stop$k.so

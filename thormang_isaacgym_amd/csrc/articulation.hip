@@ -54,7 +54,7 @@ template <class M> void launch_compose(const StepArgs &a, hipStream_t stream) {
 // instantiation keeps the contact normal a compile-time e_z.
 template <class M, bool HF, class P = NoPost>
 int launch_par(const StepArgs &a, hipStream_t stream, const typename P::Args &pa = {}) {
-    constexpr size_t bytes = ParLayout<M>::template bytes<M::EPB>();
+    constexpr size_t bytes = ParLayout<M>::template bytes<alias_slots<M>(M::EPB)>();
     static_assert(bytes <= 160 * 1024, "LDS budget");
 #ifdef TG_EPB_DEV   // developer experiment: fewer envs per workgroup, the full LDS allocated (waves per CU)
     constexpr int EPBX = M::PAIR ? TG_EPB_DEV : M::EPB;

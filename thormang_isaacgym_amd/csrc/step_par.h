@@ -468,8 +468,19 @@ template <class M> __device__ __forceinline__ int dof_group(int d) {
     else return DofGroup<M>::tab.g[d];
 }
 
+// TG_ALIAS_DEV (developer timing experiment, wrong results): the lane-pair
+// trees' envs share TG_ALIAS_DEV LDS slots and the kernel is compiled for two
+// waves per SIMD, so two workgroups fit a CU -- what a per-env LDS footprint
+// half the size would buy
+#ifdef TG_ALIAS_DEV
+template <class M> constexpr int alias_slots(int epb) { return M::PAIR ? TG_ALIAS_DEV : epb; }
+#define TG_STEP_BOUNDS(M, EPB) __launch_bounds__(EPB * M::LPE, M::PAIR ? 2 : 1)
+#else
+template <class M> constexpr int alias_slots(int epb) { return epb; }
+#define TG_STEP_BOUNDS(M, EPB) __launch_bounds__(EPB * M::LPE)
+#endif
 template <class M, int EPB, bool HF, class P = NoPost>
-__global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, typename P::Args pa) {
+__global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::Args pa) {
     constexpr int LPE = M::LPE;
     static_assert(64 % LPE == 0, "an env's lanes must share a wavefront");
     using CL = CompLayout<M>;
@@ -489,7 +500,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
     auto pa_c = [](int g) { return SEPC ? PL::CB + 32 * g + 24 : g * GF + F_PA; };   // pass-2 contribution p^a
     auto ac_s = [](int g) { return SEPC ? PL::CB + 32 * g : g * GF + F_PA; };        // pass-3 acceleration
     extern __shared__ __attribute__((aligned(16))) float lds_raw[];
-    int *tab = reinterpret_cast<int *>(lds_raw + EPB * PL::ES);
+    int *tab = reinterpret_cast<int *>(lds_raw + alias_slots<M>(EPB) * PL::ES);
     const int *gi = tab + PL::T_GI;
     const I4 *desc = reinterpret_cast<const I4 *>(tab + PL::T_DESC);   // [NSTEP][LPE]
     const float *zeros = reinterpret_cast<const float *>(tab + PL::T_ZERO);
@@ -529,7 +540,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
     for (int i = tid; i < 32; i += EPB * LPE) tab[PL::T_ZERO + i] = 0;
     for (int i = tid; i < M::NCG * M::MAXD; i += EPB * LPE) tab[PL::T_CPATH + i] = M::cpath[i / M::MAXD][i % M::MAXD];
 
-    const LE s{lds_raw + le * PL::ES};
+    const LE s{lds_raw + (le % alias_slots<M>(EPB)) * PL::ES};
     const size_t N = a.N;
     const int D = a.D;
     const float h = a.h;
@@ -615,14 +626,21 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
     // overlaps the table fill's (larger trees: measured no gain, more live
     // registers across the barrier)
     constexpr int NGR = (M::NG - 1 + LPE - 1) / LPE;
-    constexpr bool EARLY = NGR == 1;
-    float q0 = 0.f, qd0 = 0.f, rt0[13];
+#ifndef TG_EARLY_STATE
+#define TG_EARLY_STATE 0   // developer switch: 1 = every tree with an affine group -> dof map
+#endif
+    constexpr bool EARLY = NGR == 1 || (TG_EARLY_STATE && group_dof_offset<M>() != -1000);
+    float q0[NGR > 0 ? NGR : 1], qd0[NGR > 0 ? NGR : 1], rt0[13];
     if constexpr (EARLY) {
-        const int g = 1 + sub;
-        if (g < M::NG) {
-            const int d = group_dof<M>(g);
-            q0 = dofs[2 * d];
-            qd0 = dofs[2 * d + 1];
+#pragma unroll
+        for (int r = 0; r < NGR; ++r) {
+            const int g = 1 + sub + r * LPE;
+            q0[r] = qd0[r] = 0.f;
+            if (g < M::NG) {
+                const int d = group_dof<M>(g);
+                q0[r] = dofs[2 * d];
+                qd0[r] = dofs[2 * d + 1];
+            }
         }
 #pragma unroll
         for (int k = 0; k < 13; ++k) rt0[k] = root[k];
@@ -673,9 +691,13 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         }
     }
     if constexpr (EARLY) {
-        if (1 + sub < M::NG) {
-            s((1 + sub) * GF + F_Q) = q0;
-            s((1 + sub) * GF + F_QD) = qd0;
+#pragma unroll
+        for (int r = 0; r < NGR; ++r) {
+            const int g = 1 + sub + r * LPE;
+            if (g < M::NG) {
+                s(g * GF + F_Q) = q0[r];
+                s(g * GF + F_QD) = qd0[r];
+            }
         }
     } else {
         for (int g = 1 + sub; g < M::NG; g += LPE) {
@@ -806,6 +828,18 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         // and the velocity limit of group 1 + sub, the composite of group sub
         if (1 + sub < M::NG) vlim1 = PR(TG_PROP_VELOCITY, bounded(gi[(1 + sub) * GIW + GI_DOF], 0, 1 << 16));
         load_inertia(cin1);
+    }
+    // one-round trees: every schedule step's joint placement too (constant
+    // over the launch: the epilogue's in-place seat moves come after the last
+    // substep), so pass 1a waits for them once per launch, not once per substep
+#ifndef TG_KIN_ONCE
+#define TG_KIN_ONCE 1   // developer switch: 0 = per-substep prefetch ring (A/B)
+#endif
+    constexpr bool KIN1 = NR1 == 1 && TG_KIN_ONCE;
+    float kin1[KIN1 ? M::NSTEP : 1][12];
+    if constexpr (KIN1) {
+#pragma unroll
+        for (int t = 0; t < M::NSTEP; ++t) load_kin(pdsc(t).x, kin1[t]);
     }
     // an epilogue's inputs it wants in flight for the whole step (P::prefetch)
     float xpre[P::NPRE > 0 ? P::NPRE : 1];
@@ -1030,6 +1064,10 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
         // fully unrolled, inputs two steps ahead in a 3-deep ring (renamed
         // registers, no copies: the wait for step t's inputs leaves steps
         // t + 1 and t + 2 in flight)
+        if constexpr (KIN1) {
+#pragma unroll
+            for (int t = 0; t < M::NSTEP; ++t) body1(pdsc(t), kin1[t]);
+        } else {
         float kr[3][12];
         I4 dr[3];
         dr[0] = pdsc(0);
@@ -1045,6 +1083,7 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                 load_kin(dr[(t + 2) % 3].x, kr[(t + 2) % 3]);
             }
             body1(dr[t % 3], kr[t % 3]);
+        }
         }
 #ifdef TG_DUMMY_STEPS
         // developer ablation: TG_DUMMY_STEPS dependent LDS round trips with no
@@ -1833,7 +1872,9 @@ __global__ __launch_bounds__(EPB * M::LPE) void step_par_kernel(StepArgs a, type
                 }
             }
             } else {   // 8-lane envs: the row velocity by an 8-lane reduction (two broadcasts
-                       // and a select measured slower than the three DPP levels)
+                       // and a select measured slower than the three DPP levels; W and the
+                       // row velocities in every lane, kept incrementally as for 16 lanes:
+                       // Gogoro +2.7 %, GogoroPaper +10 %, round 3)
             // projected Gauss-Seidel with patch friction, all LPE lanes of the env:
             // each lane holds W's columns j = sub + LPE*jj and the full multiplier
             // vector in registers; a row's W*lambda is an 8-lane reduction, so
