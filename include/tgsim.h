@@ -249,6 +249,34 @@ uint64_t tg_compiled_model_hashes(uint64_t *out, int32_t cap); /* returns count 
 int tg_model_jit(uint64_t model_hash, const char *struct_name, const char *model_source, const char *include_dir,
                  const char *cache_dir);
 
+/* gym.load_asset of a URDF without a Python host (gogoro_new.py:198-213, the
+ * locked joints of :257-262): csrc/model_load.cpp parses the file (links
+ * depth-first from the root, children in joint-declaration order, DOFs = the
+ * non-fixed joints in that order, fixed and `locked_joints` merged into rigid
+ * groups, collision boxes / spheres, a mesh collision as the torus fitted to
+ * its OBJ profile when `mesh_root` names the mesh directory) and builds the
+ * tg_model_desc and the specialisation's constexpr source exactly as the
+ * Python host (model/urdf.py, abi.model_arrays, model/codegen.py) does.
+ * tg_model_parse stops there (no device needed); tg_model_load then runs
+ * tg_model_jit for it (a no-op for a compiled-in model).  `name`: the model
+ * name (NULL: the file's stem).  The desc arrays live in the tg_model until
+ * tg_model_free; errors: tg_model_last_error(). */
+typedef struct tg_model tg_model;
+int tg_model_parse(const char *urdf_path, const char *name, const char *const *locked_joints, int32_t num_locked,
+                   const char *mesh_root, tg_model **out);
+int tg_model_load(const char *urdf_path, const char *name, const char *const *locked_joints, int32_t num_locked,
+                  const char *mesh_root, const char *cache_dir, tg_model **out);
+int tg_model_get_desc(const tg_model *model, tg_model_desc *desc);   /* pointers into the model */
+const char *tg_model_dof_name(const tg_model *model, int32_t dof);   /* gym.get_asset_dof_names order */
+const char *tg_model_link_name(const tg_model *model, int32_t link); /* gym.get_asset_rigid_body_names */
+/* gym.get_asset_dof_properties' URDF part (lower, upper, effort, velocity;
+ * +-3.4e38 for an unlimited joint) */
+int tg_model_dof_limits(const tg_model *model, int32_t dof, float *lower, float *upper, float *effort,
+                        float *velocity);
+const char *tg_model_source(const tg_model *model);   /* the constexpr traits text (codegen.emit) */
+const char *tg_model_last_error(void);
+void tg_model_free(tg_model *model);
+
 /* Composite-cache instrumentation (no reference counterpart; tests): copies
  * the per-env composite cache [N, KC] (the group composites and placements
  * the step kernel reads, built from the lock windows and mass scales) to the

@@ -49,6 +49,18 @@ SIGNATURES = {
     "tg_read_kernel_timing": [_VP, C.POINTER(C.c_double), C.POINTER(C.c_int64)],
     "tg_compiled_model_hashes": [C.POINTER(C.c_uint64), C.c_int32],
     "tg_model_jit": [C.c_uint64, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p],
+    # native URDF loading (csrc/model_load.cpp)
+    "tg_model_parse": [C.c_char_p, C.c_char_p, C.POINTER(C.c_char_p), C.c_int32, C.c_char_p, C.POINTER(C.c_void_p)],
+    "tg_model_load": [C.c_char_p, C.c_char_p, C.POINTER(C.c_char_p), C.c_int32, C.c_char_p, C.c_char_p,
+                      C.POINTER(C.c_void_p)],
+    "tg_model_get_desc": [C.c_void_p, C.c_void_p],
+    "tg_model_dof_name": [C.c_void_p, C.c_int32],
+    "tg_model_link_name": [C.c_void_p, C.c_int32],
+    "tg_model_dof_limits": [C.c_void_p, C.c_int32, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float),
+                            C.POINTER(C.c_float)],
+    "tg_model_source": [C.c_void_p],
+    "tg_model_last_error": [],
+    "tg_model_free": [C.c_void_p],
     "tg_gogoro_step": [_VP, C.POINTER(abi.tg_gogoro_params), C.POINTER(abi.tg_gogoro_buffers), _VP, C.c_int32,
                        _VP, _VP, _VP, _VP, _VP, C.c_uint64, C.c_uint64],
     "tg_gogoro_pre_physics": [_VP, C.POINTER(abi.tg_gogoro_params), C.POINTER(abi.tg_gogoro_buffers), _VP, _VP,
@@ -74,7 +86,9 @@ SIGNATURES = {
 }
 
 
-RESTYPES = {"tg_last_error": C.c_char_p, "tg_compiled_model_hashes": C.c_uint64, "tg_philox4x32_10": None}
+RESTYPES = {"tg_last_error": C.c_char_p, "tg_compiled_model_hashes": C.c_uint64, "tg_philox4x32_10": None,
+            "tg_model_dof_name": C.c_char_p, "tg_model_link_name": C.c_char_p, "tg_model_source": C.c_char_p,
+            "tg_model_last_error": C.c_char_p, "tg_model_free": None}
 
 
 def lib() -> C.CDLL:

@@ -40,6 +40,8 @@ UNITS = {
     "tgsim_api.cpp": ["-O2", "-x", "hip"],
     # run-time specialisations (hipRTC) of the articulation kernels
     "jit.cpp": ["-O2", "-x", "hip"],
+    # native URDF loading (tg_model_parse / tg_model_load): host C++ only
+    "model_load.cpp": ["-O2"],
 }
 
 

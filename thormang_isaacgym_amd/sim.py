@@ -81,6 +81,46 @@ def ensure_specialisation(model: Model, desc: abi.ModelDesc | None = None) -> bo
     return True
 
 
+class NativeModel:
+    """gym.load_asset through the C ABI alone (tg_model_load, csrc/model_load.cpp):
+    the library parses the URDF, builds the tg_model_desc and the
+    specialisation's traits and (``jit=True``) compiles them with hipRTC -- what
+    a caller without Python gets; ``Sim`` accepts it in place of a ``Model``.
+    The descriptor arrays live in the library until the object is freed."""
+
+    def __init__(self, path: str, locked=(), mesh_root: str | None = None, name: str | None = None,
+                 jit: bool = True):
+        L = lib()
+        h = C.c_void_p()
+        names = (C.c_char_p * max(len(locked), 1))(*[n.encode() for n in locked])
+        args = [path.encode(), name.encode() if name else None, names, len(locked),
+                mesh_root.encode() if mesh_root else None]
+        rc = L.tg_model_load(*args, jit_cache_dir().encode(), C.byref(h)) if jit else \
+            L.tg_model_parse(*args, C.byref(h))
+        if rc != 0:
+            raise RuntimeError(f"tg_model_load({path}): {L.tg_model_last_error().decode()} (rc {rc})")
+        self._h = h
+        self.desc = abi.tg_model_desc()
+        check(L.tg_model_get_desc(h, C.byref(self.desc)), "tg_model_get_desc")
+        self.hash = int(self.desc.model_hash)
+        self.num_bodies, self.num_dof = self.desc.num_links, self.desc.num_dofs
+        self.num_groups, self.num_shapes = self.desc.num_groups, self.desc.num_shapes
+        self.dof_names = [L.tg_model_dof_name(h, i).decode() for i in range(self.num_dof)]
+        self.link_names = [L.tg_model_link_name(h, i).decode() for i in range(self.num_bodies)]
+        S = self.num_shapes
+        self.arrays = {"shape_friction": np.ctypeslib.as_array(self.desc.shape_friction, (S,)).astype(np.float32)
+                       if S else np.zeros(0, np.float32)}
+        self.jit = jit and self.hash not in compiled_model_hashes()
+
+    def source(self) -> str:
+        return lib().tg_model_source(self._h).decode()
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().tg_model_free(self._h)
+            self._h = None
+
+
 def _ptr(t: torch.Tensor | None):
     return None if t is None else C.c_void_p(t.data_ptr())
 
@@ -98,14 +138,19 @@ class Sim:
         self.device = torch.device(device)
         self.model = model
         self.num_envs = N = int(num_envs)
-        self.desc = abi.ModelDesc(model)
-        if jit_hash is not None:
-            self.desc.hash = int(jit_hash)
-            self.desc.desc.model_hash = int(jit_hash)
         self.params = params
-        self.D, self.G, self.L, self.S = model.num_dof, model.num_groups, model.num_bodies, len(model.shapes)
         torch.cuda.set_device(self.device)
-        self.jit = ensure_specialisation(model, self.desc)
+        if isinstance(model, NativeModel):   # loaded (and compiled) by the library itself
+            self.desc = model
+            self.D, self.G, self.L, self.S = model.num_dof, model.num_groups, model.num_bodies, model.num_shapes
+            self.jit = model.jit
+        else:
+            self.desc = abi.ModelDesc(model)
+            if jit_hash is not None:
+                self.desc.hash = int(jit_hash)
+                self.desc.desc.model_hash = int(jit_hash)
+            self.D, self.G, self.L, self.S = model.num_dof, model.num_groups, model.num_bodies, len(model.shapes)
+            self.jit = ensure_specialisation(model, self.desc)
         h = C.c_void_p()
         check(lib().tg_sim_create(C.byref(self.desc.desc), C.byref(params), N, self.device.index or 0, C.byref(h)),
               "tg_sim_create")
