@@ -1089,6 +1089,7 @@ namespace tg {
 struct WalkPost {
     static constexpr bool on = true;
     static constexpr int NPRE = 0;
+    static constexpr bool PM_OUT = true;   // stores the pre-physics' actions / targets (pm_in_step) below
     using Args = WalkPostArgs;
     static __device__ __forceinline__ float clampw(float x, float lo, float hi) {
         return x < lo ? lo : (x > hi ? hi : x);
@@ -1130,6 +1131,10 @@ struct WalkPost {
                 if (a.pm_in_step) {   // the pre-physics ran inside this kernel (pass 2a's targets)
                     act[r] = pm_clamp(a, a.pm_actions[eD + d]);
                     pt[r] = pm_target(a, d, act[r]);
+                    if (owner) {   // pre_physics_step's outputs (a reset below zeroes the actions again)
+                        a.pm_act_out[eD + d] = act[r];
+                        a.pm_tgt_out[eD + d] = pt[r];
+                    }
                 } else {
                     act[r] = b.actions[eD + d];
                     pt[r] = b.pos_target[eD + d];
@@ -1217,7 +1222,7 @@ struct WalkPost {
                     o[13 + d] = clampw((q[r] - dpos[r]) * p.dof_pos_scale, -co, co);
                     o[13 + D + d] = clampw(qd[r] * p.dof_vel_scale, -co, co);
                     o[13 + 2 * D + d] = clampw(act[r], -co, co);
-                    b.last_actions[eD + d] = act[r];   // (pm_in_step: actions / targets stored at kernel start)
+                    b.last_actions[eD + d] = act[r];   // (pm_in_step: actions / targets stored above)
                 }
                 rate += (act[r] - la[r]) * (act[r] - la[r]);
                 vel2 += qd[r] * qd[r];
@@ -1396,6 +1401,7 @@ template <class M> __device__ __forceinline__ void tl_update(float *c, const flo
 // and fp32 operations (gogoro_math.h) as post_kernel.
 struct GogoroPost {
     static constexpr bool on = true;
+    static constexpr bool PM_OUT = false;
     using Args = GogoroPostArgs;
     // the translating-lock extension of an env the previous step reset (its
     // reset happens in this epilogue), LPE lanes x NPRE floats, loaded at

@@ -419,6 +419,7 @@ struct NoPost {
     struct Args {};
     static constexpr bool on = false;
     static constexpr int NPRE = 0;   // floats per lane an epilogue prefetches at kernel start
+    static constexpr bool PM_OUT = false;   // the epilogue stores the walk pre-physics outputs itself
 };
 
 // inverse of the group -> dof map: group of dof d, -1 for a locked dof
@@ -523,6 +524,39 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
     const bool owner = chunk * EPB + le < a.N;
     TG_PROF_INIT
 
+    // the per-block tables, copied from the model's constants.  When every
+    // table fits one entry per thread (every compiled model), all the loads are
+    // issued before the first LDS store: one memory round trip instead of one
+    // per table (the stores would otherwise pin each table's loads behind the
+    // previous one's)
+    constexpr int NT = EPB * M::LPE;
+    constexpr bool ONE = M::NG <= NT && M::NSTEP * LPE <= NT && PackTab<M>::NPW * LPE <= NT &&
+                         M::NCG * M::MAXD <= NT && 32 <= NT;
+    if constexpr (ONE) {
+        const int ig = tid < M::NG ? tid : 0, idd = tid < M::NSTEP * LPE ? tid : 0,
+                  ipk = tid < PackTab<M>::NPW * LPE ? tid : 0, icp = tid < M::NCG * M::MAXD ? tid : 0;
+        int gv[GIW];
+        gv[GI_PARENT] = M::parent[ig];
+        gv[GI_DOF] = M::gdof[ig];
+        gv[GI_JT] = M::jtype[ig];
+        gv[GI_NCH] = M::nchild[ig];
+#pragma unroll
+        for (int c = 0; c < M::MAXC; ++c) gv[GI_CH + c] = M::child[ig][c];
+        const I4 dv = DescTab<M>::tab.d[idd];
+        const int pv = PackTab<M>::tab.v[ipk];
+        const int cv = M::cpath[icp / M::MAXD][icp % M::MAXD];
+        if (tid < M::NG) {
+#pragma unroll
+            for (int k = 0; k < GIW; ++k) tab[PL::T_GI + tid * GIW + k] = gv[k];
+        }
+        if (tid < M::NSTEP * LPE) {
+            int *p = tab + PL::T_DESC + 4 * tid;
+            p[0] = dv.x; p[1] = dv.y; p[2] = dv.z; p[3] = dv.w;
+        }
+        if (tid < PackTab<M>::NPW * LPE) tab[PL::T_PACK + tid] = pv;
+        if (tid < 32) tab[PL::T_ZERO + tid] = 0;
+        if (tid < M::NCG * M::MAXD) tab[PL::T_CPATH + tid] = cv;
+    } else {
     for (int i = tid; i < M::NG; i += EPB * LPE) {
         int *p = tab + PL::T_GI + i * GIW;
         p[GI_PARENT] = M::parent[i];
@@ -539,7 +573,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
     for (int i = tid; i < PackTab<M>::NPW * LPE; i += EPB * LPE) tab[PL::T_PACK + i] = PackTab<M>::tab.v[i];
     for (int i = tid; i < 32; i += EPB * LPE) tab[PL::T_ZERO + i] = 0;
     for (int i = tid; i < M::NCG * M::MAXD; i += EPB * LPE) tab[PL::T_CPATH + i] = M::cpath[i / M::MAXD][i % M::MAXD];
-
+    }
     const LE s{lds_raw + (le % alias_slots<M>(EPB)) * PL::ES};
     const size_t N = a.N;
     const int D = a.D;
@@ -611,7 +645,10 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
     // the walk pre-physics (tg_walk_step): the env's clamped actions and drive
     // targets written once, lane = dof mod LPE; pass 2a reads the targets back
     // like pos_tgt (the barrier below orders them within the workgroup)
-    if (a.pm_in_step && owner) {
+    // (an epilogue that stores them itself, WalkPost, skips this: its
+    // targets come from the actions where pass 2a loads them, and the kernel
+    // start then waits on no store)
+    if (!P::PM_OUT && a.pm_in_step && owner) {
         for (int d = sub; d < D; d += LPE) {
             const unsigned ed = (unsigned)e * (unsigned)D + (unsigned)d;
             const float c = pm_clamp(a, a.pm_actions[ed]);
@@ -700,10 +737,29 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             }
         }
     } else {
-        for (int g = 1 + sub; g < M::NG; g += LPE) {
-            const int d = bounded(gi[g * GIW + GI_DOF], 0, 1 << 16);
-            s(g * GF + F_Q) = dofs[2 * d];
-            s(g * GF + F_QD) = dofs[2 * d + 1];
+        // every round's dof index, then every load, then the stores: one
+        // memory round trip (a store between them would pin the next round's
+        // loads behind it)
+        int dix[NGR > 0 ? NGR : 1];
+        float qv[NGR > 0 ? NGR : 1], qdv[NGR > 0 ? NGR : 1];
+#pragma unroll
+        for (int r = 0; r < NGR; ++r) {
+            const int g = min(1 + sub + r * LPE, M::NG - 1);
+            if constexpr (group_dof_offset<M>() != -1000) dix[r] = group_dof<M>(g);
+            else dix[r] = bounded(gi[g * GIW + GI_DOF], 0, 1 << 16);
+        }
+#pragma unroll
+        for (int r = 0; r < NGR; ++r) {
+            qv[r] = dofs[2 * dix[r]];
+            qdv[r] = dofs[2 * dix[r] + 1];
+        }
+#pragma unroll
+        for (int r = 0; r < NGR; ++r) {
+            const int g = 1 + sub + r * LPE;
+            if (g < M::NG) {
+                s(g * GF + F_Q) = qv[r];
+                s(g * GF + F_QD) = qdv[r];
+            }
         }
     }
     if (sub == 0) {   // the root group's pose in its own frame (never rewritten)
@@ -784,8 +840,11 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
         x[5] = PR(TG_PROP_LOWER, d);
         x[6] = PR(TG_PROP_UPPER, d);
         const unsigned ed = (unsigned)e * (unsigned)D + (unsigned)d;
-        // the walk pre-physics inside the step (tg_walk_step): its targets, written above
-        x[7] = at_u32<float>(a.pm_in_step ? a.pm_tgt_out : a.pos_tgt, ed * 4u);
+        // the walk pre-physics inside the step (tg_walk_step): its targets, formed here from the actions
+        // (one load from whichever buffer is live: the actions when the
+        // pre-physics runs in this kernel, the stored targets otherwise)
+        const float tv = at_u32<float>(a.pm_in_step ? a.pm_actions : a.pos_tgt, ed * 4u);
+        x[7] = a.pm_in_step ? pm_target(a, d, pm_clamp(a, tv)) : tv;
         x[8] = at_u32<float>(a.vel_tgt, ed * 4u);
         if constexpr (PL::TPON) {   // the Gogoro pre-physics inside the step (tg_gogoro_step)
             if ((M::FUSED & 2) && a.gp_in_step) {
