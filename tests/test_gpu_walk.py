@@ -15,7 +15,7 @@ def _cuda():
 def test_gpu_walk_matches_oracle_env():
     _cuda()
     from tests.gpu_harness import walk_env_vs_oracle
-    err = walk_env_vs_oracle(num_envs=32, steps=60, seed=5)
+    err = walk_env_vs_oracle(num_envs=32, steps=200, seed=5)
     print(err)
     assert err["obs0"] < 1e-5, err
     assert err["obs"] < 1e-3 and err["rew"] < 1e-3, err
@@ -49,7 +49,8 @@ def test_gpu_walk_step_matches_oracle_along_1000_steps():
     step is compared from identical inputs.  Free-running, fp32-vs-fp64
     trajectories of falling humanoids drift past 1e-3 after a few hundred steps
     (ground impacts are chaotic), so the free-running comparison
-    is kept to 60 steps (test_gpu_walk_matches_oracle_env)."""
+    is kept to 200 steps (test_gpu_walk_matches_oracle_env; the drift study
+    puts the GPU's first 1e-3 excursion at step 364)."""
     _cuda()
     from tests.gpu_harness import walk_forced
     err = walk_forced(num_envs=32, steps=1000, seed=8)
