@@ -25,9 +25,9 @@ def test_gpu_walk_matches_oracle_env():
 def test_gpu_walk_dr_pushes_match_oracle_env():
     _cuda()
     from tests.gpu_harness import walk_env_vs_oracle
-    err = walk_env_vs_oracle(num_envs=32, steps=40, seed=6, task="ThormangWalkDR")
+    err = walk_env_vs_oracle(num_envs=32, steps=200, seed=7, task="ThormangWalkDR")
     print(err)
-    assert err["obs"] < 2e-3 and err["rew"] < 2e-3, err
+    assert err["obs"] < 1e-3 and err["rew"] < 1e-3, err
     assert err["reset_equal"], err
 
 
