@@ -773,7 +773,7 @@ std::string emit(const tg_model &m) {
     std::vector<int> shape_cg;
     for (int g : sgroup) shape_cg.push_back((int)(std::find(cgroups.begin(), cgroups.end(), g) - cgroups.begin()));
     const char *pm = std::getenv("TG_PAIR_MIN_GROUPS");
-    const int SL = 8, EPB = 16, PAIR = G >= (pm ? std::atoi(pm) : 16) ? 1 : 0, LPE = SL * (1 + PAIR);
+    const int SL = 8, EPB = 16, PAIR = G >= (pm ? std::atoi(pm) : 2) ? 1 : 0, LPE = SL * (1 + PAIR);
     const auto sched = lane_schedule(gpar, SL);
     std::vector<std::vector<int>> children(G);
     for (int c = 0; c < G; ++c)

@@ -189,15 +189,16 @@ template <class M> struct ParLayout {
     static constexpr int WB_J = WB_A + WCM * 6 * M::NCG;    // [WCM][K]
     static constexpr int WB_M = WB_J + WCM * (K > 0 ? K : 1);   // [WCM][WCM]
     static constexpr int TOTAL = WOOD ? WB_M + WCM * WCM : TOTAL0;
-    // env stride.  Lane-pair trees (Thormang): 2 mod 4 floats, so the two envs
+    // env stride.  Large trees (Thormang): 2 mod 4 floats, so the two envs
     // of a 32-lane b32/b64 bank group fall on disjoint bank classes (bank
     // conflicts 27 % -> 17 % of LDS cycles, kernel -0.25 %; the env base is
-    // then 8-byte aligned and 16-byte moves become b64 pairs).  The 8-lane
-    // scooters keep 16-byte strides (2 mod 4 measured +1.9 %; profiles/r3/lds_*)
+    // then 8-byte aligned and 16-byte moves become b64 pairs).  The scooters
+    // keep 16-byte strides (2 mod 4 measured +1.9 % on 8 lanes per env and
+    // +2.5 % / +1.5 % Gogoro / paper on lane pairs; profiles/r3/lds_*, ablations_r3)
 #ifdef TG_ES_PAD   // developer experiment: extra floats per env (LDS bank pattern)
     static constexpr int ESPAD = TG_ES_PAD;
 #else
-    static constexpr int ESPAD = M::PAIR ? 2 : 0;
+    static constexpr int ESPAD = M::NG >= 16 ? 2 : 0;
 #endif
     static constexpr int ES = ((TOTAL + 3) & ~3) + ESPAD;
     template <int EPB> static constexpr size_t bytes() { return ((size_t)EPB * ES + T_TOTAL) * 4; }

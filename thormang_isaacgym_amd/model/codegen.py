@@ -40,7 +40,7 @@ def shape_rows(kind: int) -> int:
 
 LANES_PER_ENV = 8   # schedule lanes per env of the tree-parallel step kernel (csrc/step_par.h)
 # trees with at least this many groups run on lane pairs (16 lanes per env)
-PAIR_MIN_GROUPS = int(os.environ.get("TG_PAIR_MIN_GROUPS", "16"))
+PAIR_MIN_GROUPS = int(os.environ.get("TG_PAIR_MIN_GROUPS", "2"))
 
 
 def lane_schedule(parent, lanes):
@@ -169,9 +169,11 @@ def emit(m: Model, cname: str) -> str:
     # 8 schedule lanes x 16 envs per workgroup for every model: Thormang fills a
     # CU's LDS with 16 envs; for the scooter 8 lanes also beat 2/4 (more
     # Delassus columns in parallel) and 16 envs beat 8 (measured).
-    # Large trees (PAIR) run every schedule slot on a lane pair (sub, sub + 8)
-    # that splits each group's update: 16 lanes per env, 4 wavefronts per
-    # workgroup, so 4096 envs put one wavefront on every SIMD.
+    # Every tree with a joint group (PAIR) runs each schedule slot on a lane
+    # pair (sub, sub + 8) that splits each group's update: 16 lanes per env, 4
+    # wavefronts per workgroup, so 4096 envs put one wavefront on every SIMD
+    # (the scooters too since round 3: Gogoro +4 %, GogoroPaper +6 % over 8
+    # lanes per env, which left half the SIMDs idle; single-body models keep 8).
     SL, EPB = LANES_PER_ENV, 16
     PAIR = 1 if G >= PAIR_MIN_GROUPS else 0
     LPE = SL * (1 + PAIR)
