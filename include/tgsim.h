@@ -148,6 +148,11 @@ typedef struct tg_sim_params {
     int32_t fix_base;             /* AssetOptions.fix_base_link            */
     float env_spacing;            /* create_env spacing (env origins grid) */
     int32_t envs_per_row;
+    int32_t solver_type;          /* physx.solver_type: 0 PGS, 1 TGS (IsaacGym's default).  TGS runs
+                                     the position iterations as sub-steps of h / contact_iterations:
+                                     before each sweep a normal row's target is re-formed from its
+                                     separation advanced by the row's accumulated displacement, and
+                                     the positions integrate the mean of the sweeps' multipliers */
 } tg_sim_params;
 
 /* zero-copy device views (gymtorch.wrap_tensor equivalents) */

@@ -568,12 +568,23 @@ typedef struct {
     V3 r;            /* application point in group frame (linear rows) */
     V3 d;            /* world direction (force) or axis (moment) */
     real target;     /* normal rows: velocity lower bound */
+    real phi;        /* normal rows: separation at the start of the substep */
 } Row;
 typedef struct {
     int n0, nn;      /* first normal row, number of normal rows */
     int f0;          /* first of the 3 friction rows */
     real mu, reff;
 } Patch;
+
+/* a normal row's velocity lower bound over a step dt at separation phi: the
+ * speculative approach bound -(phi - rest)/dt above the rest offset, the
+ * Baumgarte push-out capped by max_depenetration_velocity below it */
+static real row_target(const tg_sim_params *sp, real phi, real dt) {
+    const real rest = sp->rest_offset;
+    if (phi > rest) return -(phi - rest) / dt;
+    real t = sp->baumgarte * (rest - phi) / dt;
+    return t > sp->max_depenetration_velocity ? sp->max_depenetration_velocity : t;
+}
 
 static void row_force(const Work *w, const Row *r, real lam, V6 *fi) {
     V3 dl, rxd;
@@ -734,12 +745,8 @@ static int collect_rows(const Env *e, Work *w, real h, Row *rows, Patch *patches
             for (int j = 0; j < 3; ++j) rel[j] = pts[k][j] - w->pw[g][j];
             m3T_v(w->Rw[g], rel, r->r);
             memcpy(r->d, n, sizeof(V3));
-            real rest = e->sp->rest_offset;
-            if (phi > rest) r->target = -(phi - rest) / h;
-            else {
-                r->target = e->sp->baumgarte * (rest - phi) / h;
-                if (r->target > e->sp->max_depenetration_velocity) r->target = e->sp->max_depenetration_velocity;
-            }
+            r->phi = phi;
+            r->target = row_target(e->sp, phi, h);
             real wv = (margin - phi) / margin;
             wk[k] = wv < 0 ? 0 : (wv > 1 ? 1 : wv);
             wsum += wk[k];
@@ -856,6 +863,46 @@ static void solve_contacts(const Env *e, Work *w, real h, real *qds, V6 v0s, rea
     }
     memset(lam, 0, sizeof(real) * K);
     for (int i = 0; i < K; ++i) target[i] = rows[i].target;
+    const int tgs = e->sp->solver_type == 1 && e->sp->contact_iterations > 0;
+    if (tgs) {
+        /* TGS: the N position iterations are sub-steps of hs = h / N.  Before
+         * each sweep a normal row's target is re-formed over hs from its
+         * separation advanced by the row's displacement so far (hs times its
+         * velocity after every earlier sweep, the linearised motion of the
+         * sub-steps); the positions integrate the mean of the N sweeps'
+         * multipliers (the mean sub-step velocity, velocity being affine in
+         * the multipliers); the velocity iterations continue from the last
+         * sweep's multipliers with the push-out removed. */
+        const int N = e->sp->contact_iterations;
+        const real hs = h / N;
+        real disp[3 * MAXC], lbar[3 * MAXC];
+        for (int i = 0; i < K; ++i) disp[i] = lbar[i] = 0;
+        for (int it = 0; it < N; ++it) {
+            for (int i = 0; i < K; ++i)
+                if (rows[i].type == ROW_NORMAL) target[i] = row_target(e->sp, rows[i].phi + disp[i], hs);
+            pgs_sweeps(K, npatch, patches, rows, target, W, vfree, lam, 1);
+            for (int i = 0; i < K; ++i) {
+                lbar[i] += lam[i];
+                if (rows[i].type == ROW_NORMAL) {
+                    real v = vfree[i];
+                    for (int j = 0; j < K; ++j) v += W[i][j] * lam[j];
+                    disp[i] += hs * v;
+                }
+            }
+        }
+        for (int i = 0; i < K; ++i) {
+            if (rows[i].type == ROW_NORMAL) target[i] = row_target(e->sp, rows[i].phi + disp[i], hs);
+            target[i] = target[i] < 0 ? target[i] : 0;
+            lbar[i] /= N;
+        }
+        real lamv[3 * MAXC];
+        memcpy(lamv, lam, sizeof(real) * K);
+        if (e->sp->velocity_iterations > 0)
+            pgs_sweeps(K, npatch, patches, rows, target, W, vfree, lamv, e->sp->velocity_iterations);
+        apply_impulses(e, w, rows, K, lamv, qdv, v0v);
+        apply_impulses(e, w, rows, K, lbar, qds, v0s);
+        return;
+    }
     pgs_sweeps(K, npatch, patches, rows, target, W, vfree, lam, e->sp->contact_iterations);
     if (e->sp->velocity_iterations > 0) {
         real lamv[3 * MAXC];

@@ -126,8 +126,27 @@ def balance_policy(obs):
     return np.clip(4.0 * roll + 0.8 * droll, -1.0, 1.0)[:, None].astype(np.float32)
 
 
-def gogoro_env_vs_oracle(num_envs=64, steps=20, seed=0, policy=None, max_steps=1000, dr=False, fix_base=False):
-    """Free-running GPU Gogoro env vs the oracle env on the same draws."""
+def within(err, key="obs", tol=1e-3, factor=4.0):
+    """The parity bar: the GPU-vs-fp64-oracle error under ``tol`` -- or, when
+    the run carries the rounding control (``err[key + "_f32"]``: the fp32 build
+    of the same oracle on the same inputs, as for the TGS-configured Gogoro
+    tasks, whose sub-stepped contact targets amplify rounding, DESIGN.md §2
+    "Solver type") and that control itself departs from fp64 by more, under
+    ``factor`` times the control (the GPU runs about 2x the fp32 build's
+    rounding at the 99.9th percentile in either solver)."""
+    c = err.get(key + "_f32")
+    return err[key] < (tol if c is None else max(tol, factor * c))
+
+
+def tgs_configured(cfg):
+    return int(cfg["sim"].get("physx", {}).get("solver_type", 1)) == 1
+
+
+def gogoro_env_vs_oracle(num_envs=64, steps=20, seed=0, policy=None, max_steps=1000, dr=False, fix_base=False,
+                         control=None):
+    """Free-running GPU Gogoro env vs the oracle env on the same draws; with
+    ``control`` (default: when the cfg asks for TGS) the fp32 oracle build
+    runs the same free-running episode beside the fp64 one (``within``)."""
     import torch
     from thormang_isaacgym_amd.tasks import gogoro as gmod
     cfg = parity_cfg(num_envs, max_steps=max_steps, dr=dr)
@@ -137,15 +156,27 @@ def gogoro_env_vs_oracle(num_envs=64, steps=20, seed=0, policy=None, max_steps=1
     finally:
         gmod.DEBUGFIXBASE = saved
     orc = OracleGogoro(parity_cfg(num_envs, max_steps=max_steps, dr=dr), NumpyDraws(seed), fix_base=fix_base)
+    if control is None:
+        control = tgs_configured(cfg)
+    ctl = OracleGogoro(parity_cfg(num_envs, max_steps=max_steps, dr=dr), NumpyDraws(seed), fix_base=fix_base,
+                       precision="f32") if control else None
     err = {"obs": 0.0, "rew": 0.0, "reset_equal": True, "timeout_equal": True, "root": 0.0, "steps": steps,
            "resets": 0}
+    if ctl is not None:
+        err["obs_f32"] = err["rew_f32"] = 0.0
     obs_np = orc.a["obs_buf"].copy()
     for t in range(steps):
         if dr:
             sync_dr(orc, env)
+            if ctl is not None:
+                sync_dr(ctl, env)
         act = policy(obs_np) if policy is not None else np.zeros((num_envs, 1), np.float32)
         obs_d, rew, reset, extras = env.step(torch.from_numpy(act).to("cuda:0"))
         o_obs, o_rew, o_reset, o_to = orc.step(act[:, 0])
+        if ctl is not None:
+            c_obs, c_rew = ctl.step(act[:, 0])[:2]
+            err["obs_f32"] = max(err["obs_f32"], float(np.abs(c_obs - o_obs).max()))
+            err["rew_f32"] = max(err["rew_f32"], float(np.abs(c_rew - o_rew).max()))
         g_obs = obs_d["obs"].cpu().numpy()
         err["obs"] = max(err["obs"], float(np.abs(g_obs - o_obs).max()))
         err["rew"] = max(err["rew"], float(np.abs(rew.cpu().numpy() - o_rew).max()))
@@ -153,7 +184,7 @@ def gogoro_env_vs_oracle(num_envs=64, steps=20, seed=0, policy=None, max_steps=1
         err["reset_equal"] &= bool(np.array_equal(reset.cpu().numpy(), o_reset))
         err["timeout_equal"] &= bool(np.array_equal(extras["time_outs"].cpu().numpy().astype(np.uint8), o_to))
         err["resets"] += int(o_reset.sum())
-        if err["obs"] >= 1e-3 and "first_bad_step" not in err:
+        if not within(err) and "first_bad_step" not in err:
             err["first_bad_step"] = t
         obs_np = o_obs.copy()
     err["resets_seen"] = int(orc.a["progress_buf"].min())
@@ -185,19 +216,30 @@ def sync_dr(orc, env):
               "gravity": np.asarray(sim.gravity, np.float32)}
 
 
-def forced_step_errors(env, orc, act_fn, steps, act_to_orc=lambda a: a):
+def forced_step_errors(env, orc, act_fn, steps, act_to_orc=lambda a: a, ctl=None):
     """1-step GPU-vs-oracle errors along a GPU trajectory (oracle re-synced from
-    the GPU state before every step).  Returns max errors and exact-match flags."""
+    the GPU state before every step).  Returns max errors and exact-match flags;
+    with ``ctl`` (the fp32 oracle build, re-synced alike) also its one-step
+    errors against the fp64 oracle (``within``)."""
     import torch
     err = {"obs": 0.0, "rew": 0.0, "root": 0.0, "reset_equal": True, "timeout_equal": True, "steps": steps,
            "resets": 0}
+    if ctl is not None:
+        err["obs_f32"] = err["rew_f32"] = 0.0
     obs = orc.a["obs_buf"].copy()
     for t in range(steps):
         sync_oracle_from_gpu(orc, env)
         sync_dr(orc, env)
+        if ctl is not None:
+            sync_oracle_from_gpu(ctl, env)
+            sync_dr(ctl, env)
         act = act_fn(obs)
         obs_d, rew, reset, extras = env.step(torch.from_numpy(act).to("cuda:0"))
         o_obs, o_rew, o_reset, o_to = orc.step(act_to_orc(act))
+        if ctl is not None:
+            c_obs, c_rew = ctl.step(act_to_orc(act))[:2]
+            err["obs_f32"] = max(err["obs_f32"], float(np.abs(c_obs - o_obs).max()))
+            err["rew_f32"] = max(err["rew_f32"], float(np.abs(c_rew - o_rew).max()))
         g_obs = obs_d["obs"].cpu().numpy()
         err["obs"] = max(err["obs"], float(np.abs(g_obs - o_obs).max()))
         err["rew"] = max(err["rew"], float(np.abs(rew.cpu().numpy() - o_rew).max()))
@@ -213,7 +255,9 @@ def gogoro_forced(num_envs=64, steps=1000, seed=0, max_steps=300, dr=False):
     cfg = parity_cfg(num_envs, max_steps=max_steps, dr=dr)
     env = make_gpu_gogoro(cfg, NumpyDraws(seed))
     orc = OracleGogoro(parity_cfg(num_envs, max_steps=max_steps, dr=dr), NumpyDraws(seed))
-    err = forced_step_errors(env, orc, balance_policy, steps, act_to_orc=lambda a: a[:, 0])
+    ctl = OracleGogoro(parity_cfg(num_envs, max_steps=max_steps, dr=dr), NumpyDraws(seed),
+                       precision="f32") if tgs_configured(cfg) else None
+    err = forced_step_errors(env, orc, balance_policy, steps, act_to_orc=lambda a: a[:, 0], ctl=ctl)
     if dr:
         err["gravity"] = list(env.sim.gravity)
         err["mass_scale_range"] = [float(env.sim.body_mass_scale.min()), float(env.sim.body_mass_scale.max())]

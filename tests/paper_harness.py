@@ -38,8 +38,9 @@ def fixture_cfg(f):
 
 
 class OraclePaper:
-    def __init__(self, cfg, draws, switches, root_origins=None, threads=8):
+    def __init__(self, cfg, draws, switches, root_origins=None, threads=8, precision="f64"):
         self.cfg, self.src, self.sw, self.threads = cfg, draws, switches, threads
+        self.L = lib(precision)   # f32: the rounding control of the TGS parity tests
         self.model = m = load_v12()
         self.n = n = cfg["env"]["numEnvs"]
         self.D = D = m.num_dof
@@ -71,12 +72,12 @@ class OraclePaper:
             self.b.body_force = None
         rd = reset_draws(draws, np.arange(n), n, switches["RANDOM_DAMPING"], switches["CENTER_ROBOT"])
         for e in range(n):
-            lib().oracle_paper_reset_env(C.byref(self.p), C.byref(self.b), e, ptr(np.ascontiguousarray(rd[e])))
+            self.L.oracle_paper_reset_env(C.byref(self.p), C.byref(self.b), e, ptr(np.ascontiguousarray(rd[e])))
         self.desc = self.sp = None
         self.head_id = [l.name for l in m.links].index("head_p_link")
 
     def pre(self, actions):
-        lib().oracle_paper_pre_physics(C.byref(self.p), C.byref(self.b),
+        self.L.oracle_paper_pre_physics(C.byref(self.p), C.byref(self.b),
                                        ptr(np.ascontiguousarray(actions, np.float32)))
 
     def post(self):
@@ -84,7 +85,7 @@ class OraclePaper:
         ids = np.nonzero(a["reset_buf"])[0]
         rd, nd, sd, yd, pd = post_draws(self.src, ids, a["progress_buf"].copy(), int(self.p.speed_freq_update),
                                         self.sw["PUSH_ROBOT"], self.sw["RANDOM_DAMPING"], self.sw["CENTER_ROBOT"])
-        lib().oracle_paper_post_physics(C.byref(self.p), C.byref(self.b), ptr(rd), ptr(nd), ptr(sd), ptr(yd), ptr(pd))
+        self.L.oracle_paper_post_physics(C.byref(self.p), C.byref(self.b), ptr(rd), ptr(nd), ptr(sd), ptr(yd), ptr(pd))
         if self.sw["PUSH_ROBOT"]:   # apply_rigid_body_force_tensors of the [N*L, 3] perturbations (:449-457)
             if self.desc is None:
                 self.desc = abi.ModelDesc(self.model)
@@ -92,7 +93,7 @@ class OraclePaper:
             f = np.zeros((self.n, L, 3), np.float32)
             f[:, self.head_id] = a["perturbation"]
             self._forces = f
-            lib().oracle_rigid_body_force_wrench(C.byref(self.desc.desc), self.n, ptr(a["root"]), ptr(a["dof_state"]),
+            self.L.oracle_rigid_body_force_wrench(C.byref(self.desc.desc), self.n, ptr(a["root"]), ptr(a["dof_state"]),
                                                  None, ptr(f), None, 0, ptr(a["body_force"]))
         return a["obs_buf"], a["rew_buf"], a["reset_buf"], a["timeout_buf"]
 
@@ -112,4 +113,4 @@ class OraclePaper:
         a = self.a
         force = a["body_force"] if self.sw["PUSH_ROBOT"] else None
         physics_step(self.desc, self.sp, a["root"], a["dof_state"], a["dof_props"], a["pos_target"], a["vel_target"],
-                     force=force, threads=self.threads)
+                     force=force, threads=self.threads, L=self.L)

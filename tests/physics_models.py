@@ -11,9 +11,10 @@ from thormang_isaacgym_amd.abi import ModelDesc, default_dof_props, sim_params_f
 from thormang_isaacgym_amd.model.kat_models import box_body, chain, free_body, pendulum, sphere_body, urdf_model  # noqa: F401
 
 
-def sim(m, n=1, dt=0.01, substeps=1, gravity=(0, 0, -9.81), **ao):
+def sim(m, n=1, dt=0.01, substeps=1, gravity=(0, 0, -9.81), solver_type=0, **ao):
     sp = sim_params_from_cfg({"dt": dt, "substeps": substeps, "gravity": list(gravity),
-                              "physx": {"rest_offset": 0.0, "max_depenetration_velocity": 1.0}},
+                              "physx": {"rest_offset": 0.0, "max_depenetration_velocity": 1.0,
+                                        "solver_type": solver_type}},
                              dict(dict(angular_damping=0.0, linear_damping=0.0, contact_iterations=16), **ao), n)
     desc = ModelDesc(m)
     D = m.num_dof

@@ -100,15 +100,18 @@ def test_gpu_matches_oracle_on_kat_models(name):
     assert worst < 2e-3, worst
 
 
+@pytest.mark.parametrize("solver", [0, 1])
 @pytest.mark.parametrize("shape", ["sphere", "box"])
-def test_gpu_contact_matches_oracle_and_rests(shape):
+def test_gpu_contact_matches_oracle_and_rests(shape, solver):
+    """Bodies dropped onto the plane, 200 free-running steps, under PGS
+    (solver_type 0) and TGS (1: the 16 position iterations as sub-steps)."""
     m = pm.sphere_body(0.1) if shape == "sphere" else pm.box_body()
 
     def setup(rs, root, dof, props, pt, vt):
         root[:, 2] = rs.uniform(0.12, 0.4, root.shape[0])
         root[:, 7:9] = rs.normal(0, 0.5, (root.shape[0], 2))
 
-    worst, g, root, dof = side_by_side(m, 200, setup=setup, dt=0.01, substeps=2)
+    worst, g, root, dof = side_by_side(m, 200, setup=setup, dt=0.01, substeps=2, solver_type=solver)
     z_rest = 0.1 if shape == "sphere" else 0.05
     gr = g.root_state.cpu().numpy()
     assert np.abs(gr[:, 2] - z_rest).max() < 3e-3

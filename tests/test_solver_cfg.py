@@ -27,14 +27,23 @@ def _cfg_sim():
 
 def test_gogoro_cfg_warns_on_each_unhonoured_key():
     with pytest.warns(SolverCfgWarning) as rec:
-        sim_params_from_cfg(_cfg_sim())
+        sp = sim_params_from_cfg(_cfg_sim())
     msg = " ".join(str(w.message) for w in rec)
-    for k in ("solver_type", "contact_offset", "bounce_threshold_velocity"):
-        assert k in msg, k
-    # resource knobs and honoured keys are not reported
+    assert "contact_offset" in msg
+    # resource knobs, honoured keys (solver_type 1 = TGS since round 3) and the
+    # inert bounce threshold (restitution 0 everywhere) are not reported
     for k in ("num_threads", "num_subscenes", "max_gpu_contact_pairs", "num_position_iterations",
-              "num_velocity_iterations", "rest_offset", "max_depenetration_velocity"):
+              "num_velocity_iterations", "rest_offset", "max_depenetration_velocity", "solver_type",
+              "bounce_threshold_velocity"):
         assert f"{k}:" not in msg, k
+    assert sp.solver_type == 1
+
+
+def test_solver_type_mapping():
+    assert sim_params_from_cfg({"dt": 0.01, "physx": {}}, warn=False).solver_type == 1   # IsaacGym's default: TGS
+    assert sim_params_from_cfg({"dt": 0.01, "physx": {"solver_type": 0}}, warn=False).solver_type == 0
+    assert "solver_type" in abi.unhonoured_physx_keys({"solver_type": 2})
+    assert "solver_type" not in abi.unhonoured_physx_keys({"solver_type": 1})
 
 
 def test_honoured_keys_do_not_warn():
@@ -74,27 +83,36 @@ def _drop_tilted_box(physx, steps=40):
 BASE = {"num_position_iterations": 8, "rest_offset": 0.0, "max_depenetration_velocity": 1.0}
 
 
+@pytest.mark.parametrize("solver", [0, 1])
 @pytest.mark.parametrize("key,value", [("num_position_iterations", 1), ("num_velocity_iterations", 0),
                                        ("rest_offset", 0.01), ("max_depenetration_velocity", 0.05)])
-def test_honoured_key_changes_the_result(key, value):
-    a = _drop_tilted_box(BASE)
-    b = _drop_tilted_box(dict(BASE, **{key: value}))
+def test_honoured_key_changes_the_result(key, value, solver):
+    a = _drop_tilted_box(dict(BASE, solver_type=solver))
+    b = _drop_tilted_box(dict(BASE, solver_type=solver, **{key: value}))
     assert np.abs(a - b).max() > 1e-5, (key, a, b)
 
 
-def _push_out(viters, steps=1):
-    """A box resting 4 mm INSIDE the ground: the biased sweeps push it out."""
+def test_solver_type_changes_the_result():
+    a = _drop_tilted_box(dict(BASE, solver_type=0))
+    b = _drop_tilted_box(dict(BASE, solver_type=1))
+    assert np.abs(a - b).max() > 1e-5, (a, b)
+
+
+def _push_out(viters, steps=1, solver=0, depth=0.004, vz=0.0, baumgarte=0.5):
+    """A box resting ``depth`` INSIDE the ground (negative: above it) moving
+    at ``vz``: the biased sweeps push it out."""
     m = pm.box_body(mu=0.8)
     physx = {"num_position_iterations": 8, "num_velocity_iterations": viters, "rest_offset": 0.0,
-             "max_depenetration_velocity": 10.0}
+             "max_depenetration_velocity": 10.0, "solver_type": solver}
     sp = sim_params_from_cfg({"dt": 0.01, "substeps": 1, "gravity": [0, 0, 0], "physx": physx},
-                             dict(angular_damping=0.0, linear_damping=0.0, ground_friction=0.8, baumgarte=0.5), 1,
-                             warn=False)
+                             dict(angular_damping=0.0, linear_damping=0.0, ground_friction=0.8,
+                                  baumgarte=baumgarte), 1, warn=False)
     desc = ModelDesc(m)
     props = default_dof_props(m, 1)
     root = np.zeros((1, 13), np.float32)
-    root[0, 2] = 0.05 - 0.004   # box half height 0.05 (kat_models.box_body) - 4 mm
+    root[0, 2] = 0.05 - depth   # box half height 0.05 (kat_models.box_body) - depth
     root[0, 6] = 1.0
+    root[0, 9] = vz
     z0 = float(root[0, 2])
     dof = np.zeros((0, 2), np.float32)
     z = np.zeros((1, 0), np.float32)
@@ -118,3 +136,33 @@ def test_velocity_iterations_drop_the_push_out_from_the_stored_velocity():
     # corner rows are solved one after another), monotonically
     v = [abs(_push_out(k)[1][9]) for k in (1, 4, 8)]
     assert r0[9] > v[0] > v[1] > v[2] > abs(r1[9])
+
+
+def test_tgs_sub_steps_recover_more_of_the_penetration():
+    """solver_type 1 (TGS): the 8 position iterations are sub-steps of h/8,
+    each re-forming the push-out target from the separation its predecessors
+    left, so one step recovers about 1 - (1 - baumgarte)^8 of a 4 mm
+    penetration where the PGS's converged push-out recovers baumgarte of it;
+    the positions move by the mean sub-step velocity, and the velocity
+    iterations leave nothing stored."""
+    z0, rp = _push_out(16, solver=0)
+    _, rt = _push_out(16, solver=1)
+    dp, dt = rp[2] - z0, rt[2] - z0
+    assert 0.0019 < dp < 0.0021                   # PGS: baumgarte x depth
+    # TGS: most of it; one Gauss-Seidel sweep per sub-step over the 4 coupled
+    # corner rows overshoots the rest offset by a few per cent at most
+    assert 0.0035 < dt < 0.0042, dt
+    assert abs(rt[9]) < 1e-6 and np.abs(rt[10:13]).max() < 1e-6
+
+
+def test_tgs_speculative_landing_stores_no_approach_velocity():
+    """A box 1 mm above the ground falling at 1 m/s (one 10 ms substep):
+    both solvers stop it at the ground over the step, but the PGS stores the
+    speculative approach velocity -(gap)/h while TGS's last sub-step has
+    reached the ground and stores (almost) none."""
+    z0, rp = _push_out(0, solver=0, depth=-0.001, vz=-1.0)
+    _, rt = _push_out(0, solver=1, depth=-0.001, vz=-1.0)
+    for r in (rp, rt):
+        assert abs((r[2] - z0) + 0.001) < 2e-4, r[2] - z0   # moved down by about the gap
+    assert abs(rp[9] + 0.1) < 1e-3, rp[9]                   # PGS: -gap/h stored
+    assert abs(rt[9]) < 0.02, rt[9]                         # TGS: at rest at the ground

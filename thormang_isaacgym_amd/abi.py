@@ -45,7 +45,7 @@ class tg_sim_params(C.Structure):
         ("ground_friction", C.c_float), ("baumgarte", C.c_float), ("limit_stiffness", C.c_float),
         ("limit_damping", C.c_float), ("contact_iterations", C.c_int32),
         ("velocity_iterations", C.c_int32), ("fix_base", C.c_int32),
-        ("env_spacing", C.c_float), ("envs_per_row", C.c_int32),
+        ("env_spacing", C.c_float), ("envs_per_row", C.c_int32), ("solver_type", C.c_int32),
     ]
 
 
@@ -222,9 +222,14 @@ def default_dof_props(m: Model, num_envs: int) -> np.ndarray:
 PHYSX_RESOURCE_KEYS = frozenset({
     "num_threads", "num_subscenes", "use_gpu", "default_buffer_size_multiplier", "max_gpu_contact_pairs",
     "contact_collection"})
-#: physx keys honoured by the solver (DESIGN.md §4 "Solver cfg")
+#: physx keys honoured by the solver (DESIGN.md §4 "Solver cfg"); solver_type
+#: 0 (PGS) and 1 (TGS) are both implemented, other values warn
 PHYSX_HONOURED_KEYS = frozenset({"num_position_iterations", "num_velocity_iterations", "rest_offset",
                                  "max_depenetration_velocity"})
+#: physx keys that cannot change a result of these tasks in PhysX either:
+#: bounce_threshold_velocity only gates restitution, and every material here
+#: (and in the reference, which sets none) has restitution 0
+PHYSX_INERT_KEYS = frozenset({"bounce_threshold_velocity"})
 
 
 class SolverCfgWarning(UserWarning):
@@ -234,28 +239,23 @@ class SolverCfgWarning(UserWarning):
 def unhonoured_physx_keys(physx: dict, asset_opts: dict | None = None) -> Dict[str, str]:
     """The ``sim.physx`` keys (``vec_task.py:470-482`` sets them on PhysX's
     params) that would change a PhysX result but not this solver's, each with
-    the reason.  ``solver_type`` 1 (TGS): the contact solve is velocity-level
-    projected Gauss-Seidel -- ``num_position_iterations`` sweeps with a
-    Baumgarte push-out capped by ``max_depenetration_velocity``, then
-    ``num_velocity_iterations`` bias-free sweeps (PhysX's split, honoured) --
-    without TGS's per-sub-iteration integration of the bias;
-    ``contact_offset``: contacts are speculative within the asset option
-    ``contact_margin`` instead; ``bounce_threshold_velocity``: no restitution
-    model (every material has restitution 0, as the reference sets none, so a
-    PhysX run would not bounce either).  Unknown keys are reported too."""
+    the reason.  ``solver_type`` 0 (PGS) and 1 (TGS, the position iterations
+    as sub-steps with re-formed contact targets, DESIGN.md §4 "Solver cfg")
+    are honoured, any other value is reported; ``contact_offset``: contacts
+    are speculative within the asset option ``contact_margin`` instead;
+    ``bounce_threshold_velocity`` is inert (``PHYSX_INERT_KEYS``).  Unknown
+    keys are reported too."""
     ao = asset_opts or {}
     out: Dict[str, str] = {}
     for k, v in physx.items():
-        if k in PHYSX_RESOURCE_KEYS or k in PHYSX_HONOURED_KEYS:
+        if k in PHYSX_RESOURCE_KEYS or k in PHYSX_HONOURED_KEYS or k in PHYSX_INERT_KEYS:
             continue
         if k == "solver_type":
-            if int(v) == 1:
-                out[k] = "TGS requested; the contact solve is velocity-level projected Gauss-Seidel"
+            if int(v) not in (0, 1):
+                out[k] = f"{v} is neither PGS (0) nor TGS (1); TGS is used"
         elif k == "contact_offset":
             out[k] = (f"{v} ignored; contacts are speculative within contact_margin "
                       f"{float(ao.get('contact_margin', 0.05))}")
-        elif k == "bounce_threshold_velocity":
-            out[k] = "no restitution model (restitution 0 everywhere), the threshold has no effect"
         else:
             out[k] = "unknown physx key, ignored"
     return out
@@ -295,6 +295,8 @@ def sim_params_from_cfg(cfg_sim: dict, asset_opts: dict | None = None, num_envs:
     sp.contact_iterations = int(ao.get("contact_iterations", max(1, int(physx.get("num_position_iterations", 4)))))
     # IsaacGym's default num_velocity_iterations is 1; an asset option overrides it
     sp.velocity_iterations = int(ao.get("velocity_iterations", max(0, int(physx.get("num_velocity_iterations", 1)))))
+    # IsaacGym's default solver_type is 1 (TGS)
+    sp.solver_type = 0 if int(physx.get("solver_type", 1)) == 0 else 1
     sp.fix_base = int(bool(ao.get("fix_base_link", False)))
     sp.env_spacing = float(env_spacing)
     sp.envs_per_row = max(1, int(math.sqrt(num_envs)))

@@ -1070,6 +1070,23 @@ template <class M> __device__ __forceinline__ constexpr int row_base(int s) {
     for (int k = 0; k < s; ++k) base += M::shape_nrows[k] + 3;
     return base;
 }
+// row k is a normal row (lane-dependent k): compares against the model's row ranges
+template <class M> __device__ __forceinline__ bool row_normal(int k) {
+    bool r = false;
+    int base = 0;
+#pragma unroll
+    for (int sh = 0; sh < M::NS; ++sh) {
+        r = (k >= base && k < base + M::shape_nrows[sh]) ? true : r;
+        base += M::shape_nrows[sh] + 3;
+    }
+    return r;
+}
+// a normal row's velocity lower bound over a step dt at separation phi: the
+// speculative approach bound above the rest offset, the Baumgarte push-out
+// capped by max_depenetration_velocity below it (oracle/physics_ref.c row_target)
+__device__ __forceinline__ float contact_target(const StepArgs &a, float phi, float dt) {
+    return phi > a.rest ? -(phi - a.rest) / dt : fminf(a.baumgarte * (a.rest - phi) / dt, a.max_depen);
+}
 
 }  // namespace tg
 

@@ -1571,8 +1571,13 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
         if constexpr (M::NS > 0) {
             // velocity iterations (sim.physx.num_velocity_iterations): the
             // positions integrate the biased sweeps' velocity (F_QDS, v0s),
-            // the stored velocity is the bias-free one (F_QD, v0v)
-            const bool vit = a.viters > 0;
+            // the stored velocity is the bias-free one (F_QD, v0v).  TGS
+            // (solver_type 1): the position iterations are sub-steps of
+            // h / iters, the positions integrate the mean of their
+            // multipliers, the stored velocity the last (or the velocity
+            // iterations'); either way two multiplier sets (vit)
+            const bool tgs = a.tgs != 0;
+            const bool vit = a.viters > 0 || tgs;
             // contact-group world poses and free velocities (one lane per contact group)
             for (int c = sub; c < M::NCG; c += LPE) {
                 // the group and its path (groups, joint types) selected from the
@@ -1685,7 +1690,8 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     }
                     // row Jacobian in the root frame: (r x d, d), r = the point about the root origin
                     stsv(s, ro, SV{cross(mulT(R, pts[k] - pos), dl), dl});
-                    s(ro + 6) = phi > a.rest ? -(phi - a.rest) / h : fminf(a.baumgarte * (a.rest - phi) / h, a.max_depen);
+                    // (TGS: the separation itself, the PGS forms the sub-step targets)
+                    s(ro + 6) = a.tgs ? phi : contact_target(a, phi, h);
                     s(ro + 7) = 1.f;
                     wk[k] = fminf(fmaxf((a.margin - phi) / a.margin, 0.f), 1.f);
                     wsum += wk[k];
@@ -1841,23 +1847,33 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             // vector in registers, no LDS traffic in the sweeps)
             {
                 constexpr int JL = (K + LPE - 1) / LPE;
-                float wr[JL][K], rv[JL], tg[K], onr[K], wd[K], lam[K];
+                // (the lane's own rows: W rows, velocities, targets; TGS: their
+                // separations and displacements)
+                float wr[JL][K], rv[JL], tgo[JL], phio[JL], dsp[JL], onr[K], wd[K], lam[K], lbar[K];
+                bool nrm[JL];
+                const float hs = tgs ? h / (float)a.iters : h;   // (TGS sub-step)
 #pragma unroll
                 for (int jj = 0; jj < JL; ++jj) {
                     const int k = sub + LPE * jj;
 #pragma unroll
                     for (int c = 0; c < K; ++c) wr[jj][c] = k < K ? s(PL::W + k * K + c) : 0.f;
                     rv[jj] = k < K ? s(PL::VFREE + k) : 0.f;
+                    // slot 6: the target (PGS; 0 on friction rows) or the separation (TGS)
+                    const float t6 = k < K ? s(PL::ROW + k * 8 + 6) : 0.f;
+                    nrm[jj] = k < K && row_normal<M>(k);
+                    phio[jj] = t6;
+                    dsp[jj] = 0.f;
+                    tgo[jj] = (tgs && nrm[jj]) ? contact_target(a, t6, hs) : t6;
                 }
 #pragma unroll
                 for (int i = 0; i < K; ++i) {
-                    tg[i] = s(PL::ROW + i * 8 + 6);
                     onr[i] = s(PL::ROW + i * 8 + 7);
                     wd[i] = 1.0f / s(PL::W + i * K + i);   // (the inverse diagonal, formed once)
                     lam[i] = 0.f;
+                    lbar[i] = 0.f;
                 }
-                auto row_v = [&](int i) {   // vfree_i + (W lambda)_i, from its owner lane
-                    return env_bcast<LPE>(rv[i / LPE], i % LPE, sub);
+                auto row_e = [&](int i) {   // target_i - (vfree_i + (W lambda)_i), from its owner lane
+                    return env_bcast<LPE>(tgo[i / LPE] - rv[i / LPE], i % LPE, sub);
                 };
                 auto set_lam = [&](int i, float v) {
                     const float d = v - lam[i];
@@ -1870,7 +1886,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
 #pragma unroll
                 for (int jj = 0; jj < JL; ++jj) vfr[jj] = rv[jj];
 #endif
-                auto sweeps = [&](int n_it) {
+                auto sweeps = [&](int n_it, bool sub_steps) {
 #pragma unroll 1
                 for (int it = 0; it < n_it; ++it) {
 #ifdef TG_PGS_REFRESH
@@ -1890,8 +1906,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                         for (int k = 0; k < 4; ++k) {
                             if (k >= nr) break;
                             const int i = rb + k;
-                            const float vi = row_v(i);
-                            const float l = lam[i] + (tg[i] - vi) * wd[i];
+                            const float l = lam[i] + row_e(i) * wd[i];
                             const float li = onr[i] * fmaxf(l, 0.f);
                             set_lam(i, li);
                             Nsum += li;
@@ -1899,32 +1914,46 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                         const int f = rb + nr;
                         const float mu = s(PL::SHP + 2 * sh), reff = s(PL::SHP + 2 * sh + 1);
                         // tangent 1, then tangent 2 with the cone projection of the
-                        // pair, then the torsional row clamped
-                        set_lam(f, lam[f] - row_v(f) * wd[f]);
+                        // pair, then the torsional row clamped (friction targets 0)
+                        set_lam(f, lam[f] + row_e(f) * wd[f]);
                         {
-                            const float l0 = lam[f], l1 = lam[f + 1] - row_v(f + 1) * wd[f + 1];
+                            const float l0 = lam[f], l1 = lam[f + 1] + row_e(f + 1) * wd[f + 1];
                             const float lt = sqrtf(l0 * l0 + l1 * l1), lim = mu * Nsum;
                             const float sc = lt > lim ? (lt > 0.f ? lim / lt : 0.f) : 1.f;
                             set_lam(f, l0 * sc);
                             set_lam(f + 1, l1 * sc);
                         }
                         const float lim3 = mu * Nsum * reff;
-                        set_lam(f + 2, fminf(fmaxf(lam[f + 2] - row_v(f + 2) * wd[f + 2], -lim3), lim3));
+                        set_lam(f + 2, fminf(fmaxf(lam[f + 2] + row_e(f + 2) * wd[f + 2], -lim3), lim3));
+                    }
+                    if (sub_steps) {
+                        // TGS: each normal row advances by hs times its velocity after
+                        // the sweep, its next target is re-formed from that
+                        // separation; the multipliers accumulate for their mean
+#pragma unroll
+                        for (int jj = 0; jj < JL; ++jj) {
+                            dsp[jj] += hs * rv[jj];
+                            tgo[jj] = nrm[jj] ? contact_target(a, phio[jj] + dsp[jj], hs) : tgo[jj];
+                        }
+#pragma unroll
+                        for (int i = 0; i < K; ++i) lbar[i] += lam[i];
                     }
                 }
                 };
-                sweeps(a.iters);   // position iterations: push-out bias in the normal targets
+                sweeps(a.iters, tgs);   // position iterations: push-out bias in the normal targets
                 if (vit) {
-                    // velocity iterations (PhysX): the biased multipliers park in the
-                    // dead Delassus slots (W is in registers now), the normal targets
-                    // lose the push-out (min(target, 0)), and the sweeps continue
+                    // two multiplier sets: the positions' (the biased multipliers,
+                    // TGS their mean over the sub-steps) park in the dead Delassus
+                    // slots (W is in registers now); the velocity iterations lose
+                    // the push-out (min(target, 0)) and continue from the last sweep
                     if (lead) {
+                        const float inv = 1.0f / (float)(a.iters > 0 ? a.iters : 1);
 #pragma unroll
-                        for (int i = 0; i < K; ++i) s(PL::W + i) = lam[i];
+                        for (int i = 0; i < K; ++i) s(PL::W + i) = tgs ? lbar[i] * inv : lam[i];
                     }
 #pragma unroll
-                    for (int i = 0; i < K; ++i) tg[i] = fminf(tg[i], 0.f);
-                    sweeps(a.viters);
+                    for (int jj = 0; jj < JL; ++jj) tgo[jj] = fminf(tgo[jj], 0.f);
+                    if (a.viters > 0) sweeps(a.viters, false);
                 }
                 if (lead) {
 #pragma unroll
@@ -1941,7 +1970,8 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             // every lane computes the same update (no LDS traffic in the sweeps)
             {
                 constexpr int JL = (K + LPE - 1) / LPE;
-                float wc[K][JL], vf[K], tg[K], onr[K], wd[K], lam[K], my[JL];
+                float wc[K][JL], vf[K], tg[K], onr[K], wd[K], lam[K], my[JL], phi[K], dsp[K], lbar[K];
+                const float hs = tgs ? h / (float)a.iters : h;   // (TGS sub-step)
 #pragma unroll
                 for (int i = 0; i < K; ++i) {
 #pragma unroll
@@ -1950,7 +1980,10 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                         wc[i][jj] = j < K ? s(PL::W + i * K + j) : 0.f;
                     }
                     vf[i] = s(PL::VFREE + i);
-                    tg[i] = s(PL::ROW + i * 8 + 6);
+                    phi[i] = s(PL::ROW + i * 8 + 6);   // the target (PGS) or the separation (TGS)
+                    dsp[i] = 0.f;
+                    lbar[i] = 0.f;
+                    tg[i] = (tgs && row_normal<M>(i)) ? contact_target(a, phi[i], hs) : phi[i];
                     onr[i] = s(PL::ROW + i * 8 + 7);
                     wd[i] = 1.0f / s(PL::W + i * K + i);   // (the inverse diagonal, formed once)
                     lam[i] = 0.f;
@@ -1969,7 +2002,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     for (int jj = 0; jj < JL; ++jj)
                         if (sub + LPE * jj == i) my[jj] = v;
                 };
-                auto sweeps = [&](int n_it) {
+                auto sweeps = [&](int n_it, bool sub_steps) {
 #pragma unroll 1
                 for (int it = 0; it < n_it; ++it) {
 #pragma unroll
@@ -2004,17 +2037,28 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                         const float lim3 = mu * Nsum * reff;
                         set_lam(f + 2, fminf(fmaxf(lam[f + 2], -lim3), lim3));
                     }
+                    if (sub_steps) {   // TGS (as the 16-lane sweeps)
+#pragma unroll
+                        for (int i = 0; i < K; ++i) {
+                            if (row_normal<M>(i)) {
+                                dsp[i] += hs * row_v(i);
+                                tg[i] = contact_target(a, phi[i] + dsp[i], hs);
+                            }
+                            lbar[i] += lam[i];
+                        }
+                    }
                 }
                 };
-                sweeps(a.iters);   // position iterations (biased), then the bias-free velocity iterations
+                sweeps(a.iters, tgs);   // position iterations (biased), then the bias-free velocity iterations
                 if (vit) {
-                    if (lead) {
+                    if (lead) {   // the positions' multipliers (TGS: the sub-steps' mean)
+                        const float inv = 1.0f / (float)(a.iters > 0 ? a.iters : 1);
 #pragma unroll
-                        for (int i = 0; i < K; ++i) s(PL::W + i) = lam[i];   // the biased multipliers
+                        for (int i = 0; i < K; ++i) s(PL::W + i) = tgs ? lbar[i] * inv : lam[i];
                     }
 #pragma unroll
                     for (int i = 0; i < K; ++i) tg[i] = fminf(tg[i], 0.f);
-                    sweeps(a.viters);
+                    if (a.viters > 0) sweeps(a.viters, false);
                 }
                 if (lead) {
 #pragma unroll
@@ -2232,7 +2276,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
         // ---- velocity limits + integration: the positions with the biased
         // sweeps' velocity (F_QDS, v0s), the stored velocity the bias-free one
         // (F_QD, v0v) when velocity iterations ran
-        const bool vst = M::NS > 0 && a.viters > 0;
+        const bool vst = M::NS > 0 && (a.viters > 0 || a.tgs);
 #pragma unroll
         for (int r = 0; r < (M::NG + LPE - 1) / LPE; ++r) {
             const int g = 1 + sub + r * LPE;

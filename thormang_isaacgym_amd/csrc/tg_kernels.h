@@ -59,6 +59,7 @@ struct StepArgs {
     float gx, gy, gz;
     float lin_damp, ang_damp, max_depen, rest, margin, ground_mu, baumgarte, lim_k, lim_c;
     int iters, viters, fix_base;   // biased (position) and bias-free (velocity) PGS sweeps
+    int tgs;                       // solver_type 1: position iterations as sub-steps (step_par.h PGS)
     float *root;              // [N,13]
     float *dof;               // [N*D,2]
     const float *pos_tgt;     // [N,D]

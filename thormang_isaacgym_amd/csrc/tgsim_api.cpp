@@ -168,6 +168,7 @@ tg::StepArgs step_args(tg_sim *s) {
     a.iters = p.contact_iterations;
     a.viters = p.velocity_iterations;
     a.fix_base = p.fix_base;
+    a.tgs = p.solver_type == 1 && p.contact_iterations > 0;
     a.root = s->root;
     a.dof = s->dof;
     a.pos_tgt = s->pos_tgt;
