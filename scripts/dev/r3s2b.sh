@@ -1,7 +1,7 @@
 # developer session: the GPU suite after the TGS / rounding-control changes, then A/B against the pre-TGS library
 set -u
 cd $GRAFT_REPO_ROOT
-OUT=gpurun_out/s5; mkdir -p $OUT
+OUT=${OUT:-gpurun_out/s5}; mkdir -p $OUT
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -rf > $OUT/tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; grep -E "passed|failed|FAIL" $OUT/tests.log | tail -15; [ $rc -le 1 ] || exit $rc

@@ -965,6 +965,16 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 stsv(s, PL::WB_R + 6 * sub, ar);
 #pragma unroll
                 for (int c = 0; c < M::NCG; ++c) stsv(s, PL::WB_A + 6 * (M::NCG * sub + c), acc[M::cgroup[c]]);
+            } else if (sub < WCM) {
+                // the unused response slots (wn < WCM): zeros, because the
+                // fixed-size WCM sums below multiply them by zero weights, and
+                // 0 x whatever an earlier kernel left in this LDS is NaN when
+                // that was a NaN pattern (ragged-batch Gogoro runs hit it)
+#pragma unroll
+                for (int g = 0; g < 8; ++g) s(PL::WB_G + 8 * sub + g) = 0.f;
+                stsv(s, PL::WB_R + 6 * sub, sv0());
+#pragma unroll
+                for (int c = 0; c < M::NCG; ++c) stsv(s, PL::WB_A + 6 * (M::NCG * sub + c), sv0());
             }
             TG_SYNC();
             // (2) every lane: the clamped system M = K^-1 - E^T G (wn x wn), the
@@ -1845,13 +1855,17 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             // velocity reaches every lane of the env by one DPP row broadcast,
             // and every lane computes the same update (the full multiplier
             // vector in registers, no LDS traffic in the sweeps)
-            {
+            // (instantiated per solver: the PGS build carries none of the TGS
+            // state -- one more live array in this section cost the walk 1 us)
+            auto pgs16 = [&](auto TC) {
+                constexpr bool T = decltype(TC)::value != 0;
                 constexpr int JL = (K + LPE - 1) / LPE;
+                constexpr int JT = T ? JL : 1, KT = T ? K : 1;
                 // (the lane's own rows: W rows, velocities, targets; TGS: their
                 // separations and displacements)
-                float wr[JL][K], rv[JL], tgo[JL], phio[JL], dsp[JL], onr[K], wd[K], lam[K], lbar[K];
-                bool nrm[JL];
-                const float hs = tgs ? h / (float)a.iters : h;   // (TGS sub-step)
+                float wr[JL][K], rv[JL], tgo[JL], phio[JT], dsp[JT], onr[K], wd[K], lam[K], lbar[KT];
+                bool nrm[JT];
+                const float hs = T ? h / (float)a.iters : h;   // (TGS sub-step)
 #pragma unroll
                 for (int jj = 0; jj < JL; ++jj) {
                     const int k = sub + LPE * jj;
@@ -1860,17 +1874,21 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     rv[jj] = k < K ? s(PL::VFREE + k) : 0.f;
                     // slot 6: the target (PGS; 0 on friction rows) or the separation (TGS)
                     const float t6 = k < K ? s(PL::ROW + k * 8 + 6) : 0.f;
-                    nrm[jj] = k < K && row_normal<M>(k);
-                    phio[jj] = t6;
-                    dsp[jj] = 0.f;
-                    tgo[jj] = (tgs && nrm[jj]) ? contact_target(a, t6, hs) : t6;
+                    if constexpr (T) {
+                        nrm[jj] = k < K && row_normal<M>(k);
+                        phio[jj] = t6;
+                        dsp[jj] = 0.f;
+                        tgo[jj] = nrm[jj] ? contact_target(a, t6, hs) : t6;
+                    } else {
+                        tgo[jj] = t6;
+                    }
                 }
 #pragma unroll
                 for (int i = 0; i < K; ++i) {
                     onr[i] = s(PL::ROW + i * 8 + 7);
                     wd[i] = 1.0f / s(PL::W + i * K + i);   // (the inverse diagonal, formed once)
                     lam[i] = 0.f;
-                    lbar[i] = 0.f;
+                    if constexpr (T) lbar[i] = 0.f;
                 }
                 auto row_e = [&](int i) {   // target_i - (vfree_i + (W lambda)_i), from its owner lane
                     return env_bcast<LPE>(tgo[i / LPE] - rv[i / LPE], i % LPE, sub);
@@ -1886,7 +1904,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
 #pragma unroll
                 for (int jj = 0; jj < JL; ++jj) vfr[jj] = rv[jj];
 #endif
-                auto sweeps = [&](int n_it, bool sub_steps) {
+                auto sweeps = [&](int n_it, auto SUBC) {
 #pragma unroll 1
                 for (int it = 0; it < n_it; ++it) {
 #ifdef TG_PGS_REFRESH
@@ -1926,7 +1944,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                         const float lim3 = mu * Nsum * reff;
                         set_lam(f + 2, fminf(fmaxf(lam[f + 2] + row_e(f + 2) * wd[f + 2], -lim3), lim3));
                     }
-                    if (sub_steps) {
+                    if constexpr (T && decltype(SUBC)::value != 0) {
                         // TGS: each normal row advances by hs times its velocity after
                         // the sweep, its next target is re-formed from that
                         // separation; the multipliers accumulate for their mean
@@ -1940,7 +1958,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     }
                 }
                 };
-                sweeps(a.iters, tgs);   // position iterations: push-out bias in the normal targets
+                sweeps(a.iters, IntC<1>{});   // position iterations: push-out bias in the normal targets
                 if (vit) {
                     // two multiplier sets: the positions' (the biased multipliers,
                     // TGS their mean over the sub-steps) park in the dead Delassus
@@ -1949,17 +1967,22 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     if (lead) {
                         const float inv = 1.0f / (float)(a.iters > 0 ? a.iters : 1);
 #pragma unroll
-                        for (int i = 0; i < K; ++i) s(PL::W + i) = tgs ? lbar[i] * inv : lam[i];
+                        for (int i = 0; i < K; ++i) {
+                            if constexpr (T) s(PL::W + i) = lbar[i] * inv;
+                            else s(PL::W + i) = lam[i];
+                        }
                     }
 #pragma unroll
                     for (int jj = 0; jj < JL; ++jj) tgo[jj] = fminf(tgo[jj], 0.f);
-                    if (a.viters > 0) sweeps(a.viters, false);
+                    if (a.viters > 0) sweeps(a.viters, IntC<0>{});
                 }
                 if (lead) {
 #pragma unroll
                     for (int i = 0; i < K; ++i) s(PL::LAM + i) = lam[i];
                 }
-            }
+            };
+            if (tgs) pgs16(IntC<1>{});
+            else pgs16(IntC<0>{});
             } else {   // 8-lane envs: the row velocity by an 8-lane reduction (two broadcasts
                        // and a select measured slower than the three DPP levels; W and the
                        // row velocities in every lane, kept incrementally as for 16 lanes:
