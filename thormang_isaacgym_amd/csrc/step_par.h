@@ -1863,7 +1863,10 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 constexpr int JT = T ? JL : 1, KT = T ? K : 1;
                 // (the lane's own rows: W rows, velocities, targets; TGS: their
                 // separations and displacements)
-                float wr[JL][K], rv[JL], tgo[JL], phio[JT], dsp[JT], onr[K], wd[K], lam[K], lbar[KT];
+                // PGS: every lane holds every row's target (tg), as before TGS;
+                // TGS: the owner lane holds its rows' moving targets (tgo)
+                float wr[JL][K], rv[JL], tgo[JT], tg[T ? 1 : K], phio[JT], dsp[JT], onr[K], wd[K], lam[K],
+                    lbar[KT];
                 bool nrm[JT];
                 const float hs = T ? h / (float)a.iters : h;   // (TGS sub-step)
 #pragma unroll
@@ -1872,27 +1875,30 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
 #pragma unroll
                     for (int c = 0; c < K; ++c) wr[jj][c] = k < K ? s(PL::W + k * K + c) : 0.f;
                     rv[jj] = k < K ? s(PL::VFREE + k) : 0.f;
-                    // slot 6: the target (PGS; 0 on friction rows) or the separation (TGS)
-                    const float t6 = k < K ? s(PL::ROW + k * 8 + 6) : 0.f;
-                    if constexpr (T) {
+                    if constexpr (T) {   // slot 6: the separation (TGS; 0 on friction rows)
+                        const float t6 = k < K ? s(PL::ROW + k * 8 + 6) : 0.f;
                         nrm[jj] = k < K && row_normal<M>(k);
                         phio[jj] = t6;
                         dsp[jj] = 0.f;
                         tgo[jj] = nrm[jj] ? contact_target(a, t6, hs) : t6;
-                    } else {
-                        tgo[jj] = t6;
                     }
                 }
 #pragma unroll
                 for (int i = 0; i < K; ++i) {
+                    if constexpr (!T) tg[i] = s(PL::ROW + i * 8 + 6);   // the target (0 on friction rows)
                     onr[i] = s(PL::ROW + i * 8 + 7);
                     wd[i] = 1.0f / s(PL::W + i * K + i);   // (the inverse diagonal, formed once)
                     lam[i] = 0.f;
                     if constexpr (T) lbar[i] = 0.f;
                 }
-                auto row_e = [&](int i) {   // target_i - (vfree_i + (W lambda)_i), from its owner lane
-                    return env_bcast<LPE>(tgo[i / LPE] - rv[i / LPE], i % LPE, sub);
+                // target_i - (vfree_i + (W lambda)_i) of a normal row, the row
+                // velocity from its owner lane (TGS: the difference formed there)
+                auto row_e = [&](int i) {
+                    if constexpr (T) return env_bcast<LPE>(tgo[i / LPE] - rv[i / LPE], i % LPE, sub);
+                    else return tg[i] - env_bcast<LPE>(rv[i / LPE], i % LPE, sub);
                 };
+                // a friction row's (target 0): -(vfree_i + (W lambda)_i)
+                auto row_f = [&](int i) { return -env_bcast<LPE>(rv[i / LPE], i % LPE, sub); };
                 auto set_lam = [&](int i, float v) {
                     const float d = v - lam[i];
                     lam[i] = v;
@@ -1933,16 +1939,16 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                         const float mu = s(PL::SHP + 2 * sh), reff = s(PL::SHP + 2 * sh + 1);
                         // tangent 1, then tangent 2 with the cone projection of the
                         // pair, then the torsional row clamped (friction targets 0)
-                        set_lam(f, lam[f] + row_e(f) * wd[f]);
+                        set_lam(f, lam[f] + row_f(f) * wd[f]);
                         {
-                            const float l0 = lam[f], l1 = lam[f + 1] + row_e(f + 1) * wd[f + 1];
+                            const float l0 = lam[f], l1 = lam[f + 1] + row_f(f + 1) * wd[f + 1];
                             const float lt = sqrtf(l0 * l0 + l1 * l1), lim = mu * Nsum;
                             const float sc = lt > lim ? (lt > 0.f ? lim / lt : 0.f) : 1.f;
                             set_lam(f, l0 * sc);
                             set_lam(f + 1, l1 * sc);
                         }
                         const float lim3 = mu * Nsum * reff;
-                        set_lam(f + 2, fminf(fmaxf(lam[f + 2] + row_e(f + 2) * wd[f + 2], -lim3), lim3));
+                        set_lam(f + 2, fminf(fmaxf(lam[f + 2] + row_f(f + 2) * wd[f + 2], -lim3), lim3));
                     }
                     if constexpr (T && decltype(SUBC)::value != 0) {
                         // TGS: each normal row advances by hs times its velocity after
@@ -1972,8 +1978,13 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                             else s(PL::W + i) = lam[i];
                         }
                     }
+                    if constexpr (T) {
 #pragma unroll
-                    for (int jj = 0; jj < JL; ++jj) tgo[jj] = fminf(tgo[jj], 0.f);
+                        for (int jj = 0; jj < JL; ++jj) tgo[jj] = fminf(tgo[jj], 0.f);
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < K; ++i) tg[i] = fminf(tg[i], 0.f);
+                    }
                     if (a.viters > 0) sweeps(a.viters, IntC<0>{});
                 }
                 if (lead) {
