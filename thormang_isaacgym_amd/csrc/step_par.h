@@ -1893,6 +1893,15 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 }
                 // target_i - (vfree_i + (W lambda)_i) of a normal row, the row
                 // velocity from its owner lane (TGS: the difference formed there)
+                // the shapes' patch friction and torsion radius, in registers for
+                // all the sweeps (read from LDS inside the sweep, each was a
+                // round trip on the Gauss-Seidel chain)
+                float smu[M::NS], sre[M::NS];
+#pragma unroll
+                for (int sh = 0; sh < M::NS; ++sh) {
+                    smu[sh] = s(PL::SHP + 2 * sh);
+                    sre[sh] = s(PL::SHP + 2 * sh + 1);
+                }
                 auto row_e = [&](int i) {
                     if constexpr (T) return env_bcast<LPE>(tgo[i / LPE] - rv[i / LPE], i % LPE, sub);
                     else return tg[i] - env_bcast<LPE>(rv[i / LPE], i % LPE, sub);
@@ -1936,7 +1945,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                             Nsum += li;
                         }
                         const int f = rb + nr;
-                        const float mu = s(PL::SHP + 2 * sh), reff = s(PL::SHP + 2 * sh + 1);
+                        const float mu = smu[sh], reff = sre[sh];
                         // tangent 1, then tangent 2 with the cone projection of the
                         // pair, then the torsional row clamped (friction targets 0)
                         set_lam(f, lam[f] + row_f(f) * wd[f]);
@@ -2024,6 +2033,15 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 }
 #pragma unroll
                 for (int jj = 0; jj < JL; ++jj) my[jj] = 0.f;
+                // the shapes' patch friction and torsion radius, in registers for
+                // all the sweeps (read from LDS inside the sweep, each was a
+                // round trip on the Gauss-Seidel chain)
+                float smu[M::NS], sre[M::NS];
+#pragma unroll
+                for (int sh = 0; sh < M::NS; ++sh) {
+                    smu[sh] = s(PL::SHP + 2 * sh);
+                    sre[sh] = s(PL::SHP + 2 * sh + 1);
+                }
                 auto row_v = [&](int i) {   // vfree_i + (W lambda)_i
                     float part = 0.f;
 #pragma unroll
@@ -2054,7 +2072,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                             Nsum += li;
                         }
                         const int f = rb + nr;
-                        const float mu = s(PL::SHP + 2 * sh), reff = s(PL::SHP + 2 * sh + 1);
+                        const float mu = smu[sh], reff = sre[sh];
 #pragma unroll
                         for (int t = 0; t < 3; ++t) {
                             const int i = f + t;
