@@ -1865,8 +1865,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 // separations and displacements)
                 // PGS: every lane holds every row's target (tg), as before TGS;
                 // TGS: the owner lane holds its rows' moving targets (tgo)
-                float wr[JL][K], rv[JL], tgo[JT], tg[T ? 1 : K], phio[JT], dsp[JT], onr[K], wd[K], lam[K],
-                    lbar[KT];
+                float wr[JL][K], rv[JL], tgo[JT], tg[T ? 1 : K], phio[JT], dsp[JT], wd[K], lam[K], lbar[KT];
                 bool nrm[JT];
                 const float hs = T ? h / (float)a.iters : h;   // (TGS sub-step)
 #pragma unroll
@@ -1886,7 +1885,6 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
 #pragma unroll
                 for (int i = 0; i < K; ++i) {
                     if constexpr (!T) tg[i] = s(PL::ROW + i * 8 + 6);   // the target (0 on friction rows)
-                    onr[i] = s(PL::ROW + i * 8 + 7);
                     wd[i] = 1.0f / s(PL::W + i * K + i);   // (the inverse diagonal, formed once)
                     lam[i] = 0.f;
                     if constexpr (T) lbar[i] = 0.f;
@@ -1902,12 +1900,14 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     smu[sh] = s(PL::SHP + 2 * sh);
                     sre[sh] = s(PL::SHP + 2 * sh + 1);
                 }
-                auto row_e = [&](int i) {
-                    if constexpr (T) return env_bcast<LPE>(tgo[i / LPE] - rv[i / LPE], i % LPE, sub);
-                    else return tg[i] - env_bcast<LPE>(rv[i / LPE], i % LPE, sub);
+                // row i's velocity vfree_i + (W lambda)_i, from its owner lane
+                auto row_v = [&](int i) { return env_bcast<LPE>(rv[i / LPE], i % LPE, sub); };
+                // a normal row's target (TGS: the owner's moving target, broadcast
+                // off the Gauss-Seidel chain: it changes once per sweep)
+                auto row_t = [&](int i) {
+                    if constexpr (T) return env_bcast<LPE>(tgo[i / LPE], i % LPE, sub);
+                    else return tg[i];
                 };
-                // a friction row's (target 0): -(vfree_i + (W lambda)_i)
-                auto row_f = [&](int i) { return -env_bcast<LPE>(rv[i / LPE], i % LPE, sub); };
                 auto set_lam = [&](int i, float v) {
                     const float d = v - lam[i];
                     lam[i] = v;
@@ -1939,8 +1939,11 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                         for (int k = 0; k < 4; ++k) {
                             if (k >= nr) break;
                             const int i = rb + k;
-                            const float l = lam[i] + row_e(i) * wd[i];
-                            const float li = onr[i] * fmaxf(l, 0.f);
+                            // lam + (target - v) / W_ii with the target term formed
+                            // first: one dependent FMA after the row velocity
+                            // arrives (every row slot 7, the on flag, is 1)
+                            const float ci = lam[i] + row_t(i) * wd[i];
+                            const float li = fmaxf(ci - row_v(i) * wd[i], 0.f);
                             set_lam(i, li);
                             Nsum += li;
                         }
@@ -1948,16 +1951,18 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                         const float mu = smu[sh], reff = sre[sh];
                         // tangent 1, then tangent 2 with the cone projection of the
                         // pair, then the torsional row clamped (friction targets 0)
-                        set_lam(f, lam[f] + row_f(f) * wd[f]);
+                        set_lam(f, lam[f] - row_v(f) * wd[f]);
                         {
-                            const float l0 = lam[f], l1 = lam[f + 1] + row_f(f + 1) * wd[f + 1];
-                            const float lt = sqrtf(l0 * l0 + l1 * l1), lim = mu * Nsum;
-                            const float sc = lt > lim ? (lt > 0.f ? lim / lt : 0.f) : 1.f;
+                            // the cone scale lim / |l| by one reciprocal square root
+                            // (|l| > lim >= 0 makes |l|^2 > 0)
+                            const float l0 = lam[f], l1 = lam[f + 1] - row_v(f + 1) * wd[f + 1];
+                            const float n2 = l0 * l0 + l1 * l1, lim = mu * Nsum;
+                            const float sc = n2 > lim * lim ? lim * rsqrtf(n2) : 1.f;
                             set_lam(f, l0 * sc);
                             set_lam(f + 1, l1 * sc);
                         }
                         const float lim3 = mu * Nsum * reff;
-                        set_lam(f + 2, fminf(fmaxf(lam[f + 2] + row_f(f + 2) * wd[f + 2], -lim3), lim3));
+                        set_lam(f + 2, fminf(fmaxf(lam[f + 2] - row_v(f + 2) * wd[f + 2], -lim3), lim3));
                     }
                     if constexpr (T && decltype(SUBC)::value != 0) {
                         // TGS: each normal row advances by hs times its velocity after
