@@ -572,7 +572,10 @@ typedef struct {
 } Row;
 typedef struct {
     int n0, nn;      /* first normal row, number of normal rows */
-    int f0;          /* first of the 3 friction rows */
+    int f0;          /* first of the friction rows: t1, t2, then torsion when nf == 3 */
+    int nf;          /* friction rows: 3, or 2 for a one-point patch (torus, sphere), whose
+                        torsion radius is 0 -- PhysX applies no torsional friction without a
+                        torsional patch radius either */
     real mu, reff;
 } Patch;
 
@@ -776,7 +779,8 @@ static int collect_rows(const Env *e, Work *w, real h, Row *rows, Patch *patches
         V3 rel, rl;
         for (int j = 0; j < 3; ++j) rel[j] = cen[j] - w->pw[g][j];
         m3T_v(w->Rw[g], rel, rl);
-        for (int t = 0; t < 3; ++t) {
+        P->nf = np == 1 ? 2 : 3;
+        for (int t = 0; t < P->nf; ++t) {
             Row *r = &rows[nr++];
             r->g = g; r->type = ROW_T1 + t; r->angular = (t == 2); r->patch = np_; r->target = 0;
             memcpy(r->r, rl, sizeof rl);
@@ -816,8 +820,10 @@ static void pgs_sweeps(int K, int npatch, const Patch *patches, const Row *rows,
                 lam[f] *= sc;
                 lam[f + 1] *= sc;
             }
-            real lt3 = lam[f + 2] - ROWV(f + 2) / W[f + 2][f + 2], lim3 = P->mu * N * P->reff;
-            lam[f + 2] = lt3 > lim3 ? lim3 : (lt3 < -lim3 ? -lim3 : lt3);
+            if (P->nf == 3) {
+                real lt3 = lam[f + 2] - ROWV(f + 2) / W[f + 2][f + 2], lim3 = P->mu * N * P->reff;
+                lam[f + 2] = lt3 > lim3 ? lim3 : (lt3 < -lim3 ? -lim3 : lt3);
+            }
         }
     }
 #undef ROWV

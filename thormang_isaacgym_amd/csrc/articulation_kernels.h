@@ -1045,12 +1045,19 @@ template <class M> __global__ __launch_bounds__(64 * COMPOSE_WPB) void rb_force_
 }
 
 // ---------------------------------------------------------------- contact row layout
-// rows of shape s: shape_nrows[s] normal rows, then friction t1, t2 and torsion
+// rows of shape s: shape_nrows[s] normal rows, then friction t1, t2 and --
+// for a patch of several points -- torsion.  A one-point patch (torus,
+// sphere) has no torsional friction: its torsion radius is the points' mean
+// distance from their centroid, 0 (PhysX, too, applies none without a
+// torsional patch radius, which the reference does not set)
+template <class M> __device__ __forceinline__ constexpr int shape_nfric(int s) {
+    return M::shape_nrows[s] == 1 ? 2 : 3;
+}
 template <class M> __device__ __forceinline__ constexpr int row_shape(int i) {
     int base = 0;
     for (int s = 0; s < M::NS; ++s) {
-        if (i < base + M::shape_nrows[s] + 3) return s;
-        base += M::shape_nrows[s] + 3;
+        if (i < base + M::shape_nrows[s] + shape_nfric<M>(s)) return s;
+        base += M::shape_nrows[s] + shape_nfric<M>(s);
     }
     return 0;
 }
@@ -1061,13 +1068,13 @@ template <class M> __device__ __forceinline__ int row_cg(int i) {
 #pragma unroll
     for (int sh = 0; sh < M::NS; ++sh) {
         r = i >= base ? M::shape_cg[sh] : r;
-        base += M::shape_nrows[sh] + 3;
+        base += M::shape_nrows[sh] + shape_nfric<M>(sh);
     }
     return r;
 }
 template <class M> __device__ __forceinline__ constexpr int row_base(int s) {
     int base = 0;
-    for (int k = 0; k < s; ++k) base += M::shape_nrows[k] + 3;
+    for (int k = 0; k < s; ++k) base += M::shape_nrows[k] + shape_nfric<M>(k);
     return base;
 }
 // row k is a normal row (lane-dependent k): compares against the model's row ranges
@@ -1077,7 +1084,7 @@ template <class M> __device__ __forceinline__ bool row_normal(int k) {
 #pragma unroll
     for (int sh = 0; sh < M::NS; ++sh) {
         r = (k >= base && k < base + M::shape_nrows[sh]) ? true : r;
-        base += M::shape_nrows[sh] + 3;
+        base += M::shape_nrows[sh] + shape_nfric<M>(sh);
     }
     return r;
 }

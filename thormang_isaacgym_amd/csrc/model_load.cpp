@@ -832,7 +832,7 @@ std::string emit(const tg_model &m) {
     const int NSA = std::max(S, 1);
     std::vector<int> nrows_or = nrows_n.empty() ? std::vector<int>{0} : nrows_n;
     int nrows = 0;
-    for (int n : nrows_n) nrows += n + 3;
+    for (int n : nrows_n) nrows += n + (n == 1 ? 2 : 3);   // (one-point shapes: no torsion row)
     std::vector<std::string> L_;
     auto add = [&](const std::string &x) { L_.push_back(x); };
     auto I = [](long v) { return std::to_string(v); };
@@ -852,7 +852,7 @@ std::string emit(const tg_model &m) {
     add("  static constexpr int ag_mask[1] = {0};");
     add("  static constexpr int ash_shape[1] = {0};");
     add("  static constexpr int ash_mask[1] = {0};");
-    add("  static constexpr int NROWS = " + I(nrows) + ";  // contact rows (normals + 3 friction per shape)");
+    add("  static constexpr int NROWS = " + I(nrows) + ";  // contact rows (normals + 3 friction per shape, 2 for one-point shapes)");
     add("  static constexpr int parent[" + I(G) + "] = " + iarr(gp) + ";");
     add("  static constexpr int gdof[" + I(G) + "] = " + iarr(gdof) + ";");
     add("  static constexpr int jtype[" + I(G) + "] = " + iarr(gtype) + ";");

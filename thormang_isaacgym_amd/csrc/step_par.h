@@ -1730,7 +1730,8 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 const V3 t2 = cross(n, t1);
                 const V3 rl = mulT(R, cen - pos);
                 const float fon = 1.f;
-                for (int t = 0; t < 3; ++t) {
+                const int nf = nr == 1 ? 2 : 3;   // (shape_nfric: no torsion row for a one-point patch)
+                for (int t = 0; t < nf; ++t) {
                     const int ro = PL::ROW + (rb + nr + t) * 8;
                     const V3 dt = mulT(R, t == 0 ? t1 : (t == 1 ? t2 : n));
                     stsv(s, ro, t == 2 ? SV{dt, v3(0, 0, 0)} : SV{cross(rl, dt), dt});   // torsion row: angular
@@ -1961,8 +1962,10 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                             set_lam(f, l0 * sc);
                             set_lam(f + 1, l1 * sc);
                         }
-                        const float lim3 = mu * Nsum * reff;
-                        set_lam(f + 2, fminf(fmaxf(lam[f + 2] - row_v(f + 2) * wd[f + 2], -lim3), lim3));
+                        if (shape_nfric<M>(sh) == 3) {   // torsion (several-point patches)
+                            const float lim3 = mu * Nsum * reff;
+                            set_lam(f + 2, fminf(fmaxf(lam[f + 2] - row_v(f + 2) * wd[f + 2], -lim3), lim3));
+                        }
                     }
                     if constexpr (T && decltype(SUBC)::value != 0) {
                         // TGS: each normal row advances by hs times its velocity after
@@ -2079,7 +2082,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                         const int f = rb + nr;
                         const float mu = smu[sh], reff = sre[sh];
 #pragma unroll
-                        for (int t = 0; t < 3; ++t) {
+                        for (int t = 0; t < shape_nfric<M>(sh); ++t) {
                             const int i = f + t;
                             const float vi = row_v(i);
                             set_lam(i, lam[i] - vi * wd[i]);
@@ -2091,8 +2094,10 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                                 set_lam(f + 1, l1 * sc);
                             }
                         }
-                        const float lim3 = mu * Nsum * reff;
-                        set_lam(f + 2, fminf(fmaxf(lam[f + 2], -lim3), lim3));
+                        if (shape_nfric<M>(sh) == 3) {
+                            const float lim3 = mu * Nsum * reff;
+                            set_lam(f + 2, fminf(fmaxf(lam[f + 2], -lim3), lim3));
+                        }
                     }
                     if (sub_steps) {   // TGS (as the 16-lane sweeps)
 #pragma unroll

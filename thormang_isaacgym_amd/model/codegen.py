@@ -219,7 +219,7 @@ def emit(m: Model, cname: str) -> str:
         f"  static constexpr int ag_mask[{max(len(tlc['ag']), 1)}] = {_arr([x[1] for x in tlc['ag']] or [0])};",
         f"  static constexpr int ash_shape[{max(len(tlc['ashape']), 1)}] = {_arr([x[0] for x in tlc['ashape']] or [0])};",
         f"  static constexpr int ash_mask[{max(len(tlc['ashape']), 1)}] = {_arr([x[1] for x in tlc['ashape']] or [0])};",
-        f"  static constexpr int NROWS = {sum(n + 3 for n in nrows_n)};  // contact rows (normals + 3 friction per shape)",
+        f"  static constexpr int NROWS = {sum(n + (2 if n == 1 else 3) for n in nrows_n)};  // contact rows (normals + 3 friction per shape, 2 for one-point shapes)",
         f"  static constexpr int parent[{G}] = {_arr(a['group_parent'])};",
         f"  static constexpr int gdof[{G}] = {_arr(gdof)};",
         f"  static constexpr int jtype[{G}] = {_arr(gtype)};",
