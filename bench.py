@@ -263,6 +263,14 @@ def post_physics_only(num_envs: int) -> dict:
             "sample": f"observations + reward of {num_envs} envs x {n} calls, one thread = {dt:.2f} s"}
 
 
+def solver_desc(env) -> str:
+    """The contact solve the step ran (the cfg's sim.physx, as tg_sim_params holds it)."""
+    sp = env.sim.get_sim_params()
+    kind = "TGS" if sp.solver_type == 1 else "PGS"
+    return (f"{kind}: {sp.contact_iterations} position iterations"
+            f"{' (sub-steps)' if sp.solver_type == 1 else ''} + {sp.velocity_iterations} velocity iterations")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -362,7 +370,8 @@ def main():
         "config": {"workload": f"{args.task} {N} envs/GPU, {'Perlin terrain' if args.terrain else 'flat ground'}, "
                                f"dt {sim_cfg['dt']} s x "
                                f"{sim_cfg.get('substeps', 2)} substeps ({1.0 / sim_cfg['dt']:.1f} Hz control)",
-                   "num_envs_per_gpu": N, "parallelism": f"env-dp{world}"},
+                   "num_envs_per_gpu": N, "parallelism": f"env-dp{world}",
+                   "contact_solver": solver_desc(env)},
         "dist": {"backend": "nccl (RCCL)" if rccl_world else None, "world_size": rccl_world or 1,
                  "collectives_in_timed_region": "barrier + max-over-ranks all_reduce of the elapsed time"
                  if rccl_world else None},

@@ -334,3 +334,44 @@ def test_gpu_native_urdf_load_through_the_c_abi_alone():
         worst = max(worst, float(np.abs(g.root_state.cpu().numpy() - root).max()),
                     float(np.abs(g.dof_state.cpu().numpy() - dof).max()))
     assert np.isfinite(worst) and worst < 2e-3, worst
+
+
+def test_gpu_solver_type_switches_at_runtime():
+    """gym.set_sim_params (tg_set_sim_params) switches the contact solve
+    between PGS (solver_type 0) and TGS (1) from the next simulate on: boxes
+    landing with some penetration, teacher-forced, each step against the
+    oracle under the solver it ran (pose 1e-4, velocity 5e-3, as the contact
+    tests), and the two solvers give different results from one state."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs the MI355X")
+    m = pm.box_body()
+    n = 16
+    desc, sp, root, dof, props, pt, vt = pm.sim(m, n=n, dt=0.01, substeps=2)
+    rs = np.random.default_rng(3)
+    root[:, 2] = rs.uniform(0.046, 0.06, n)          # half height 0.05: some start 4 mm inside
+    root[:, 7:9] = rs.normal(0, 0.5, (n, 2))
+    root[:, 9] = -0.5
+    g = gpu_sim(m, sp, n, root, dof, props, pt, vt)
+    after = {}
+    for solver in (0, 1, 0, 1, 1, 0):
+        spg = g.get_sim_params()
+        spg.solver_type = solver
+        g.set_sim_params(spg)
+        so = type(sp).from_buffer_copy(sp)
+        so.solver_type = solver
+        r = g.root_state.cpu().numpy().copy()
+        d = g.dof_state.cpu().numpy().copy()
+        r0 = r.copy()
+        physics_step(desc, so, r, d, props, pt, vt)
+        g.simulate()
+        gr = g.root_state.cpu().numpy()
+        assert np.abs(gr[:, :7] - r[:, :7]).max() < 1e-4, solver
+        assert np.abs(gr[:, 7:] - r[:, 7:]).max() < 5e-3, solver
+        after.setdefault(solver, (r0, gr.copy()))
+    # the same start state under the other solver differs
+    r0, g0 = after[0]
+    so = type(sp).from_buffer_copy(sp)
+    so.solver_type = 1
+    r1 = r0.copy()
+    physics_step(desc, so, r1, dof.copy(), props, pt, vt)
+    assert np.abs(r1[:, 7:] - g0[:, 7:]).max() > 1e-3
