@@ -1890,8 +1890,6 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     lam[i] = 0.f;
                     if constexpr (T) lbar[i] = 0.f;
                 }
-                // target_i - (vfree_i + (W lambda)_i) of a normal row, the row
-                // velocity from its owner lane (TGS: the difference formed there)
                 // the shapes' patch friction and torsion radius, in registers for
                 // all the sweeps (read from LDS inside the sweep, each was a
                 // round trip on the Gauss-Seidel chain)
