@@ -288,10 +288,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # developer rehearsal of the N > 1 path on a one-GPU box (not a scaling
+    # number): TG_BENCH_DIST_BACKEND=gloo with TG_BENCH_SHARE_GPU=1 puts every
+    # rank on cuda:0 (RCCL refuses two ranks on one device)
+    backend = os.environ.get("TG_BENCH_DIST_BACKEND", "nccl")
+    if os.environ.get("TG_BENCH_SHARE_GPU"):
+        local = 0
     rccl_world = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group(backend="nccl", init_method="env://")
+        dist.init_process_group(backend=backend, init_method="env://")
         rccl_world = dist.get_world_size()   # what RCCL itself reports (the SCALE runs are checked on it)
         if rccl_world != world:
             raise RuntimeError(f"WORLD_SIZE {world} but the process group has {rccl_world} ranks")
@@ -323,7 +329,7 @@ def main():
     env.sim.read_kernel_timing()
     windowed = args.task in ONE_LAUNCH_TASKS
     env.sim.set_kernel_timing(-TIMING_WINDOW if windowed else TIMING_PERIOD)
-    elapsed = timed_region(step, args.steps, world, dev, torch.cuda.synchronize)
+    elapsed = timed_region(step, args.steps, world, dev if backend == "nccl" else "cpu", torch.cuda.synchronize)
     # a short timed region (the driver's --steps 20) samples only a launch or
     # two: keep stepping, after the clock has stopped, until MIN_KERNEL_SAMPLES
     # launches are timed, so kernel_ms is never a one- or two-sample figure
@@ -372,7 +378,9 @@ def main():
                                f"{sim_cfg.get('substeps', 2)} substeps ({1.0 / sim_cfg['dt']:.1f} Hz control)",
                    "num_envs_per_gpu": N, "parallelism": f"env-dp{world}",
                    "contact_solver": solver_desc(env)},
-        "dist": {"backend": "nccl (RCCL)" if rccl_world else None, "world_size": rccl_world or 1,
+        "dist": {"backend": ("nccl (RCCL)" if backend == "nccl" else
+                             f"{backend} (rehearsal{', ranks share cuda:0' if os.environ.get('TG_BENCH_SHARE_GPU') else ''})")
+                 if rccl_world else None, "world_size": rccl_world or 1,
                  "collectives_in_timed_region": "barrier + max-over-ranks all_reduce of the elapsed time"
                  if rccl_world else None},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
