@@ -302,6 +302,14 @@ int tg_composite(tg_sim *sim, float *out, int32_t recompose);
 void tg_philox4x32_10(const uint32_t *ctr, const uint32_t *key, uint32_t *out);
 int tg_rng_fill(tg_sim *sim, int32_t kind, uint64_t seed, uint64_t counter, float *out, int32_t n);
 
+/* Debug instrumentation (no reference counterpart): fills the LDS of every CU
+ * with a 32-bit pattern (a NaN, say) through a dummy launch on the sim's
+ * stream.  LDS is not cleared between kernels, so a later step that read LDS
+ * it had not written would see the pattern: the stale-LDS tests step two
+ * identical envs, one with a fill before every step, and require bit-identical
+ * results. */
+int tg_debug_fill_lds(tg_sim *sim, uint32_t pattern);
+
 /* Benchmark instrumentation (no reference counterpart): with period > 0,
  * tg_simulate brackets every period-th articulation step kernel launch with HIP
  * events on the sim stream (an event pair serialises the queue for ~5 us each

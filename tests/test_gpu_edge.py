@@ -121,3 +121,33 @@ def test_gpu_rb_forces_survive_a_declined_fused_walk_step():
     assert torch.isfinite(r0).all()
     assert float((r0 - r1).abs().max()) < 1e-5, float((r0 - r1).abs().max())
     assert float((r0[:, 7] - r2[:, 7]).abs().min()) > 1e-2   # the push acted
+
+
+@pytest.mark.parametrize("task", ["Gogoro", "GogoroPaper", "ThormangWalk", "ThormangWalkDR"])
+def test_gpu_steps_read_no_stale_lds(task):
+    """No kernel of a step reads LDS it has not written this launch (round 3:
+    the Woodbury update once multiplied an unwritten slot by zero, and a NaN
+    left there by an earlier kernel poisoned whole envs): an env steps 40
+    random actions; a second env from the same seed (tia.make re-seeds torch,
+    so the DR draws repeat) steps them again with every CU's LDS filled with
+    a NaN or FLT_MAX pattern (tg_debug_fill_lds) before every step, and the
+    results must be bit-identical.  48 envs: a partial last workgroup."""
+    _cuda()
+    import thormang_isaacgym_amd as tia
+    n, steps = 48, 40
+    g = torch.Generator(device="cuda:0").manual_seed(4)
+    acts = [torch.rand(n, 64, device="cuda:0", generator=g) * 2 - 1 for _ in range(steps)]
+    runs = []
+    for fill in (False, True):
+        env = tia.make(seed=11, task=task, num_envs=n, sim_device="cuda:0", rl_device="cuda:0")
+        out = []
+        for t in range(steps):
+            if fill:
+                env.sim.debug_fill_lds(0x7FC00000 if t % 2 == 0 else 0x7F7FFFFF)
+            o, r, d, _ = env.step(acts[t][:, :env.num_actions].contiguous())
+            out.append((o["obs"].clone(), r.clone(), d.clone(), env.root_tensor.clone()))
+        runs.append(out)
+        del env
+    for t, (a, b) in enumerate(zip(*runs)):
+        assert all(torch.equal(x, y) for x, y in zip(a, b)), (task, t)
+    assert torch.isfinite(runs[1][-1][0]).all()

@@ -43,6 +43,7 @@ SIGNATURES = {
     "tg_sync": [_VP],
     "tg_philox4x32_10": [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)],
     "tg_rng_fill": [_VP, C.c_int32, C.c_uint64, C.c_uint64, _VP, C.c_int32],
+    "tg_debug_fill_lds": [_VP, C.c_uint32],
     "tg_composite": [_VP, _VP, C.c_int32],
     "tg_last_error": [],
     "tg_set_kernel_timing": [_VP, C.c_int32],

@@ -11,6 +11,7 @@
 // Arithmetic follows the reference's fp32 operation order (this TU is built
 // with -ffp-contract=off) so results match oracle/gogoro_task.c and the
 // golden fixtures to fp32 rounding of the transcendental functions.
+#include <atomic>
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -378,6 +379,36 @@ __global__ void rng_fill_kernel(int kind, uint32_t k0, uint32_t k1, uint32_t c_l
         float *o = out + 2 * (size_t)i;
         o[0] = gauss(x.x, x.y); o[1] = gauss(x.z, x.w);
     }
+}
+
+// ---------------------------------------------------------------- stale-LDS test hook (tg_debug_fill_lds)
+// Every workgroup takes the whole 160 KB LDS of its CU and writes the pattern
+// into every dword; with several workgroups per CU launched, every CU's LDS
+// leaves the launch holding the pattern (LDS is not cleared between kernels)
+constexpr int FILL_LDS_BYTES = 160 * 1024;
+__global__ __launch_bounds__(256) void fill_lds_kernel(uint32_t pattern, uint32_t *sink) {
+    extern __shared__ uint32_t lds_fill[];
+    for (int i = threadIdx.x; i < FILL_LDS_BYTES / 4; i += blockDim.x) lds_fill[i] = pattern;
+    __syncthreads();
+    // one read back so the stores are not dead (the sink is never written in practice)
+    if (lds_fill[(threadIdx.x * 37) % (FILL_LDS_BYTES / 4)] != pattern && sink) sink[0] = 1u;
+}
+
+int launch_fill_lds(uint32_t pattern, hipStream_t stream) {
+    static std::atomic<uint64_t> attr_set{0};
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return TG_ERR_HIP;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+        return TG_ERR_HIP;
+    const uint64_t bit = 1ull << dev;
+    if (!(attr_set.load(std::memory_order_acquire) & bit)) {
+        if (hipFuncSetAttribute((const void *)fill_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                FILL_LDS_BYTES) != hipSuccess)
+            return TG_ERR_HIP;
+        attr_set.fetch_or(bit, std::memory_order_acq_rel);
+    }
+    hipLaunchKernelGGL(fill_lds_kernel, dim3(4 * ncu), dim3(256), FILL_LDS_BYTES, stream, pattern, nullptr);
+    return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
 }
 
 int launch_rng_fill(int kind, uint64_t seed, uint64_t counter, float *out, int n, hipStream_t stream) {

@@ -200,6 +200,7 @@ int launch_scatter_field(float *dst, const float *src, const int32_t *ids, int n
 int launch_mark_dirty(uint8_t *dirty, const int32_t *ids, int n, hipStream_t stream);
 // tg_rng_fill test hook (gogoro_task.hip): n Philox blocks, counter (i, c_lo, c_hi, 0)
 int launch_rng_fill(int kind, uint64_t seed, uint64_t counter, float *out, int n, hipStream_t stream);
+int launch_fill_lds(uint32_t pattern, hipStream_t stream);
 
 #endif   // __HIPCC_RTC__
 

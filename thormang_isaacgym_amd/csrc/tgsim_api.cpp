@@ -763,6 +763,13 @@ int tg_rng_fill(tg_sim *s, int32_t kind, uint64_t seed, uint64_t counter, float 
     return TG_OK;
 }
 
+int tg_debug_fill_lds(tg_sim *s, uint32_t pattern) {
+    if (int rc = check_sim(s)) return rc;
+    win_touch(s);
+    if (int rc = tg::launch_fill_lds(pattern, s->stream)) return fail(rc, "LDS fill launch failed");
+    return TG_OK;
+}
+
 int tg_gogoro_pre_physics(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_buffers *b, const float *actions,
                           const float *pre_draws, uint64_t counter) {
     if (int rc = check_sim(s)) return rc;

@@ -278,6 +278,11 @@ class Sim:
     def simulate(self):
         check(lib().tg_simulate(self._h), "simulate")
 
+    def debug_fill_lds(self, pattern: int = 0x7FC00000):
+        """tg_debug_fill_lds: every CU's LDS filled with ``pattern`` (default a
+        quiet NaN) on this sim's stream -- the stale-LDS tests' probe."""
+        check(lib().tg_debug_fill_lds(self._h, C.c_uint32(pattern)), "debug_fill_lds")
+
     def get_sim_params(self) -> abi.tg_sim_params:
         """gym.get_sim_params (vec_task.py:650): a copy of the live params."""
         sp = abi.tg_sim_params()
