@@ -112,3 +112,18 @@ def test_gpu_gogoro_free_base_random_actions_free_running():
     assert err["resets"] >= 64
     assert within(err) and within(err, "rew"), err
     assert err["reset_equal"] and err["timeout_equal"], err
+
+
+def test_gpu_walk_random_actions_free_running_600_steps():
+    """The headline walk free-running with falls and re-spawns: 64 envs,
+    random actions U(-0.3, 0.3), 600 steps -- the drift study's workload
+    (`scripts/parity_drift.py walk`, profiles/r3/drift_walk.txt: the GPU and
+    the fp32 oracle build both leave the 1e-3 band near step 700, chaos after
+    the falls), at the north_star bar up to there."""
+    _cuda()
+    from tests.gpu_harness import walk_env_vs_oracle
+    err = walk_env_vs_oracle(num_envs=64, steps=600, seed=21, amp=0.3)
+    print(err)
+    assert err["resets"] > 0, err            # envs fall and re-spawn along the way
+    assert within(err) and within(err, "rew"), err
+    assert err["reset_equal"] and err["timeout_equal"], err
