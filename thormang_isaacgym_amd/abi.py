@@ -233,7 +233,7 @@ PHYSX_INERT_KEYS = frozenset({"bounce_threshold_velocity"})
 
 
 class SolverCfgWarning(UserWarning):
-    """A cfg ``sim.physx`` key whose PhysX meaning the PGS solver does not reproduce."""
+    """A cfg ``sim.physx`` key whose PhysX meaning the contact solver does not reproduce."""
 
 
 def unhonoured_physx_keys(physx: dict, asset_opts: dict | None = None) -> Dict[str, str]:
@@ -276,7 +276,7 @@ def sim_params_from_cfg(cfg_sim: dict, asset_opts: dict | None = None, num_envs:
     if warn:
         bad = unhonoured_physx_keys(physx, asset_opts)
         if bad:
-            warnings.warn("sim.physx keys not reproduced by the PGS solver: " +
+            warnings.warn("sim.physx keys not reproduced by the contact solver: " +
                           "; ".join(f"{k}: {r}" for k, r in bad.items()), SolverCfgWarning, stacklevel=2)
     ao = asset_opts or {}
     sp = tg_sim_params()
