@@ -901,6 +901,22 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
 #pragma unroll
         for (int t = 0; t < M::NSTEP; ++t) load_kin(pdsc(t).x, kin1[t]);
     }
+    // the lane's contact shape (sh = sub): its pose in the contact group's
+    // frame (composite cache) and its friction, constant over the launch --
+    // loaded once here instead of inside every substep's contact setup, where
+    // the loads sat on the chain (Gogoro: a quarter of the kernel was contact
+    // setup, profiles/r3/section_prof_gogoro_final.txt)
+#ifndef TG_SHAPE_ONCE
+#define TG_SHAPE_ONCE 1   // developer switch: 0 = loads inside the contact setup (A/B)
+#endif
+    constexpr bool SHP1 = TG_SHAPE_ONCE && M::NS > 0 && M::NS <= LPE;
+    float shp1[SHP1 ? 12 : 1], smu1 = 0.f;
+    if constexpr (SHP1) {
+        const int sh = sub < M::NS ? sub : 0;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) shp1[k] = CP(CL::shape(sh) + k);
+        smu1 = a.shape_mu[(size_t)e * M::NS + sh];
+    }
     // an epilogue's inputs it wants in flight for the whole step (P::prefetch)
     float xpre[P::NPRE > 0 ? P::NPRE : 1];
     if constexpr (P::NPRE > 0) P::template prefetch<M, LPE>(pa, a, e, sub, xpre);
@@ -1635,10 +1651,17 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 const M3 Rwg = ldm3(s, PL::CGP + 12 * cgi);
                 const V3 pwg = ldv3(s, PL::CGP + 12 * cgi + 9);
                 M3 Rsl;
+                V3 cl;
+                if constexpr (SHP1) {   // (sh == sub: loaded at kernel start)
 #pragma unroll
-                for (int k = 0; k < 9; ++k) Rsl.a[k] = CP(CL::shape(sh) + k);
+                    for (int k = 0; k < 9; ++k) Rsl.a[k] = shp1[k];
+                    cl = v3(shp1[9], shp1[10], shp1[11]);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) Rsl.a[k] = CP(CL::shape(sh) + k);
+                    cl = v3(CP(CL::shape(sh) + 9), CP(CL::shape(sh) + 10), CP(CL::shape(sh) + 11));
+                }
                 const M3 Rs = mul(Rwg, Rsl);
-                const V3 cl = v3(CP(CL::shape(sh) + 9), CP(CL::shape(sh) + 10), CP(CL::shape(sh) + 11));
                 const V3 cw = pwg + mul(Rwg, cl);
                 V3 pts[4];
                 const int nr = M::shape_nrows[sh];
@@ -1717,7 +1740,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     const V3 dt = d - dot(d, n) * n;   // in the contact plane
                     re += (wsum > 0.f ? wk[k] / wsum : 1.f / nr) * sqrtf(dot(dt, dt));
                 }
-                s(PL::SHP + 2 * sh) = 0.5f * (a.shape_mu[(size_t)e * M::NS + sh] + gmu);
+                s(PL::SHP + 2 * sh) = 0.5f * ((SHP1 ? smu1 : a.shape_mu[(size_t)e * M::NS + sh]) + gmu);
                 s(PL::SHP + 2 * sh + 1) = re;
                 // tangents: rolling direction (axis x n) for tori, else world x in the plane
                 V3 t1 = v3(1, 0, 0);
