@@ -904,8 +904,8 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
     // the lane's contact shape (sh = sub): its pose in the contact group's
     // frame (composite cache) and its friction, constant over the launch --
     // loaded once here instead of inside every substep's contact setup, where
-    // the loads sat on the chain (Gogoro: a quarter of the kernel was contact
-    // setup, profiles/r3/section_prof_gogoro_final.txt)
+    // the loads sat on the chain (Gogoro 45.4 -> 45.1 us, GogoroPaper 36.9 ->
+    // 36.5 us, A/B twice)
 #ifndef TG_SHAPE_ONCE
 #define TG_SHAPE_ONCE 1   // developer switch: 0 = loads inside the contact setup (A/B)
 #endif
