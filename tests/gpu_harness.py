@@ -427,28 +427,39 @@ def n_resets(orc):
 
 
 def walk_env_vs_oracle(num_envs=32, steps=30, seed=0, task="ThormangWalk", dr=False, fix_base=False,
-                       spawn_height=None, amp=0.3):
+                       spawn_height=None, amp=0.3, control=False):
     """Free-running GPU walk env vs the oracle env on the same draws and
-    actions U(-amp, amp) (amp 0: the PD-held default pose)."""
+    actions U(-amp, amp) (amp 0: the PD-held default pose); with ``control``
+    the fp32 oracle build runs the same episode beside the fp64 one
+    (``within``)."""
     import torch
     mk = lambda: walk_cfg(num_envs, task, dr=dr, fix_base=fix_base, spawn_height=spawn_height)
     env = make_gpu_walk(mk(), NumpyDraws(seed))
     orc = OracleWalk(mk(), NumpyDraws(seed))
+    ctl = OracleWalk(mk(), NumpyDraws(seed), precision="f32") if control else None
     rs = np.random.default_rng(seed + 100)
     err = {"obs": 0.0, "rew": 0.0, "reset_equal": True, "timeout_equal": True, "root": 0.0, "steps": steps}
+    if ctl is not None:
+        err["obs_f32"] = err["rew_f32"] = 0.0
     err["obs0"] = float(np.abs(env.obs_buf.cpu().numpy() - orc.a["obs_buf"]).max())
     for t in range(steps):
         if dr:
             sync_dr(orc, env)
+            if ctl is not None:
+                sync_dr(ctl, env)
         act = rs.uniform(-amp, amp, (num_envs, orc.D)).astype(np.float32)
         obs_d, rew, reset, extras = env.step(torch.from_numpy(act).to("cuda:0"))
         o_obs, o_rew, o_reset, o_to = orc.step(act)
+        if ctl is not None:
+            c_obs, c_rew = ctl.step(act)[:2]
+            err["obs_f32"] = max(err["obs_f32"], float(np.abs(c_obs - o_obs).max()))
+            err["rew_f32"] = max(err["rew_f32"], float(np.abs(c_rew - o_rew).max()))
         err["obs"] = max(err["obs"], float(np.abs(obs_d["obs"].cpu().numpy() - o_obs).max()))
         err["rew"] = max(err["rew"], float(np.abs(rew.cpu().numpy() - o_rew).max()))
         err["root"] = max(err["root"], float(np.abs(env.root_tensor.cpu().numpy() - orc.a["root"]).max()))
         err["reset_equal"] &= bool(np.array_equal(reset.cpu().numpy(), o_reset))
         err["timeout_equal"] &= bool(np.array_equal(extras["time_outs"].cpu().numpy().astype(np.uint8), o_to))
-        if err["obs"] >= 1e-3 and "first_bad_step" not in err:
+        if not within(err) and "first_bad_step" not in err:
             err["first_bad_step"] = t
     err["resets"] = int(n_resets(orc))
     err["min_height"] = float(orc.a["root"][:, 2].min())

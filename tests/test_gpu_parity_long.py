@@ -119,10 +119,15 @@ def test_gpu_walk_random_actions_free_running_600_steps():
     random actions U(-0.3, 0.3), 600 steps -- the drift study's workload
     (`scripts/parity_drift.py walk`, profiles/r3/drift_walk.txt: the GPU and
     the fp32 oracle build both leave the 1e-3 band near step 700, chaos after
-    the falls), at the north_star bar up to there."""
+    the falls), at the north_star bar up to there.  The fp32 oracle build runs
+    beside it as the rounding control: a numerically harmless kernel change
+    moves this chaotic trajectory (storing two rotation columns and forming the
+    third by a cross product left 1e-3 at step 211), so the bar is 1e-3 or 4x
+    the control's own departure (tests/gpu_harness.within); on the current
+    kernel the GPU stays within 1e-3 (9.2e-4 obs, 9.3e-4 reward)."""
     _cuda()
     from tests.gpu_harness import walk_env_vs_oracle
-    err = walk_env_vs_oracle(num_envs=64, steps=600, seed=21, amp=0.3)
+    err = walk_env_vs_oracle(num_envs=64, steps=600, seed=21, amp=0.3, control=True)
     print(err)
     assert err["resets"] > 0, err            # envs fall and re-spawn along the way
     assert within(err) and within(err, "rew"), err

@@ -127,34 +127,8 @@ __device__ __forceinline__ void stsi(const LE &s, int o, const SI &I) {
 // scratch float x of the contact phase, laid over the groups' I^A slots
 __device__ __forceinline__ int scr(int x) { return (x / 21) * GF + F_IA + x % 21; }
 // group g's pose in the root frame: rotation (group -> root) and origin
-// (TG_R2: only the rotation's columns 1 and 2 -- the joint axis -- are stored;
-// a reader forms column 0 as their cross product, trading six FMAs for three
-// LDS floats written and read per group: a tree step costs its LDS traffic)
-#ifndef TG_R2
-#define TG_R2 1   // developer switch: 0 = all nine entries stored (A/B)
-#endif
-__device__ __forceinline__ M3 ldR(const LE &s, int g) {
-#if TG_R2
-    const int o = g * GF + F_RT;
-    const V3 c1 = v3(s(o + 3), s(o + 4), s(o + 5)), c2 = v3(s(o + 6), s(o + 7), s(o + 8));
-    const V3 c0 = cross(c1, c2);
-    return M3{{c0.x, c1.x, c2.x, c0.y, c1.y, c2.y, c0.z, c1.z, c2.z}};
-#else
-    return transpose(ldm3(s, g * GF + F_RT));
-#endif
-}
-__device__ __forceinline__ void stR(const LE &s, int g, const M3 &R) {
-#if TG_R2
-    const int o = g * GF + F_RT;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        s(o + 3 + i) = R.a[3 * i + 1];
-        s(o + 6 + i) = R.a[3 * i + 2];
-    }
-#else
-    stm3(s, g * GF + F_RT, transpose(R));
-#endif
-}
+__device__ __forceinline__ M3 ldR(const LE &s, int g) { return transpose(ldm3(s, g * GF + F_RT)); }
+__device__ __forceinline__ void stR(const LE &s, int g, const M3 &R) { stm3(s, g * GF + F_RT, transpose(R)); }
 
 // per-group model table in LDS (ints; axis as float bits), built once per block
 enum : int { GI_PARENT = 0, GI_DOF = 1, GI_JT = 2, GI_NCH = 3, GI_CH = 4 };
