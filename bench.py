@@ -279,6 +279,8 @@ def main():
     ap.add_argument("--task", default="ThormangWalk")
     ap.add_argument("--num-envs", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--solver-type", type=int, choices=(0, 1), default=None,
+                    help="override the task cfg's sim.physx.solver_type (0 PGS, 1 TGS) for an A/B line")
     ap.add_argument("--terrain", action="store_true",
                     help="Gogoro only: the reference's USE_TERAIN Perlin terrain (gogoro_new.py:26)")
     args = ap.parse_args()
@@ -307,6 +309,8 @@ def main():
     import thormang_isaacgym_amd as tia
     from thormang_isaacgym_amd.cfg import load_task_cfg
     cfg = load_task_cfg(args.task, num_envs=args.num_envs, sim_device=dev)
+    if args.solver_type is not None:
+        cfg["sim"]["physx"]["solver_type"] = args.solver_type
     if args.terrain:
         from thormang_isaacgym_amd.tasks import gogoro as gogoro_task
         gogoro_task.USE_TERAIN = True

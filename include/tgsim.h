@@ -222,7 +222,9 @@ int tg_simulate(tg_sim *sim);
 /* gym.get_sim_params / gym.set_sim_params (vec_task.py:243,650-660; the
  * reference reads the params back, edits them and writes them again for its
  * gravity randomisation).  set takes effect at the next tg_simulate; the env
- * grid (env_spacing, envs_per_row) is fixed at creation and ignored here.
+ * grid (env_spacing, envs_per_row) and the asset option fix_base are fixed at
+ * creation and ignored here.  solver_type must be 0 (PGS) or 1 (TGS), here
+ * and in tg_sim_create (TG_ERR_ARG otherwise).
  * substeps may be 0 in set: simulate then integrates nothing and a step
  * passes the state through unchanged -- the parity tests use it to replay
  * the reference's recorded post-simulate states through the fused step. */

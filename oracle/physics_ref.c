@@ -896,8 +896,14 @@ static void solve_contacts(const Env *e, Work *w, real h, real *qds, V6 v0s, rea
                 }
             }
         }
+        /* the bias-free targets: a normal row's from its final separation over
+         * the whole substep h (not hs): the velocity the velocity iterations
+         * leave is the one the next substep starts from, and a speculative
+         * bound over hs gave it a gain of N/h on the residual gap -- 1e-6 of
+         * state became 1.3e-3 of roll rate at the spawn landings (DESIGN.md §2
+         * "TGS conditioning", scripts/dev/tgs_landing_study.py) */
         for (int i = 0; i < K; ++i) {
-            if (rows[i].type == ROW_NORMAL) target[i] = row_target(e->sp, rows[i].phi + disp[i], hs);
+            if (rows[i].type == ROW_NORMAL) target[i] = row_target(e->sp, rows[i].phi + disp[i], h);
             target[i] = target[i] < 0 ? target[i] : 0;
             lbar[i] /= N;
         }

@@ -126,16 +126,19 @@ def balance_policy(obs):
     return np.clip(4.0 * roll + 0.8 * droll, -1.0, 1.0)[:, None].astype(np.float32)
 
 
-def within(err, key="obs", tol=1e-3, factor=4.0):
-    """The parity bar: the GPU-vs-fp64-oracle error under ``tol`` -- or, when
-    the run carries the rounding control (``err[key + "_f32"]``: the fp32 build
-    of the same oracle on the same inputs, as for the TGS-configured Gogoro
-    tasks, whose sub-stepped contact targets amplify rounding, DESIGN.md §2
-    "Solver type") and that control itself departs from fp64 by more, under
-    ``factor`` times the control (the GPU runs about 2x the fp32 build's
-    rounding at the 99.9th percentile in either solver)."""
+def within(err, key="obs", tol=1e-3, factor=2.0):
+    """The parity bar, north_star's: the GPU-vs-fp64-oracle error under
+    ``tol`` = 1e-3.  The one exception is a run that carries the rounding
+    control (``err[key + "_f32"]``: the fp32 build of the same oracle on the
+    same inputs) whose control *itself* leaves the 1e-3 band -- a trajectory
+    on which fp32 rounding alone is amplified past the bar (a falling
+    humanoid).  Only then the bar is ``factor`` (2) times the control's own
+    departure, the GPU-vs-fp32-build ratio measured at the 99.9th percentile
+    (DESIGN.md §2).  A control under 1e-3 leaves the bar at 1e-3."""
     c = err.get(key + "_f32")
-    return err[key] < (tol if c is None else max(tol, factor * c))
+    if c is None or c <= tol:
+        return err[key] < tol
+    return err[key] < factor * c
 
 
 def tgs_configured(cfg):
@@ -400,11 +403,13 @@ class OracleWalk:
         return a["obs_buf"], a["rew_buf"], a["reset_buf"], a["timeout_buf"]
 
 
-def walk_cfg(num_envs, task="ThormangWalk", dr=False, fix_base=False, spawn_height=None):
+def walk_cfg(num_envs, task="ThormangWalk", dr=False, fix_base=False, spawn_height=None, solver_type=None):
     """Walk cfg of the parity runs: the task's own DR (mass, friction) off
     unless dr=True (then the oracle is handed the GPU env's draws, sync_dr);
-    pushes follow the task cfg."""
+    pushes follow the task cfg; ``solver_type`` overrides the cfg's."""
     cfg = load_task_cfg(task, num_envs=num_envs)
+    if solver_type is not None:
+        cfg["sim"]["physx"]["solver_type"] = int(solver_type)
     cfg["task"]["randomize"] = bool(dr)
     if fix_base:
         cfg["env"]["asset"] = dict(cfg["env"].get("asset", {}), fix_base_link=True)
@@ -427,13 +432,14 @@ def n_resets(orc):
 
 
 def walk_env_vs_oracle(num_envs=32, steps=30, seed=0, task="ThormangWalk", dr=False, fix_base=False,
-                       spawn_height=None, amp=0.3, control=False):
+                       spawn_height=None, amp=0.3, control=False, solver_type=None):
     """Free-running GPU walk env vs the oracle env on the same draws and
     actions U(-amp, amp) (amp 0: the PD-held default pose); with ``control``
     the fp32 oracle build runs the same episode beside the fp64 one
     (``within``)."""
     import torch
-    mk = lambda: walk_cfg(num_envs, task, dr=dr, fix_base=fix_base, spawn_height=spawn_height)
+    mk = lambda: walk_cfg(num_envs, task, dr=dr, fix_base=fix_base, spawn_height=spawn_height,
+                          solver_type=solver_type)
     env = make_gpu_walk(mk(), NumpyDraws(seed))
     orc = OracleWalk(mk(), NumpyDraws(seed))
     ctl = OracleWalk(mk(), NumpyDraws(seed), precision="f32") if control else None

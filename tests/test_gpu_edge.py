@@ -151,3 +151,43 @@ def test_gpu_steps_read_no_stale_lds(task):
     for t, (a, b) in enumerate(zip(*runs)):
         assert all(torch.equal(x, y) for x, y in zip(a, b)), (task, t)
     assert torch.isfinite(runs[1][-1][0]).all()
+
+
+def test_gpu_shared_cache_is_invisible_to_property_writes(monkeypatch):
+    """The shared composite cache (every env reads env 0's composite block
+    while all blocks are equal) must not change what a DOF property write
+    does.  A ThormangWalk env starts uniform, steps, then has one
+    env's stiffness changed through set_dof_properties_indexed, another env's
+    damping written through the zero-copy dof_props view with no refresh, and
+    a third env's stiffness through the view plus refresh; the states over the
+    following steps must be bit-identical to a run with the cache off
+    (TG_NO_SHARED_CACHE=1, read at sim creation), and differ from a run
+    without the writes in exactly those envs."""
+    _cuda()
+    import thormang_isaacgym_amd as tia
+    from thormang_isaacgym_amd.abi import TG_PROP_DAMPING, TG_PROP_STIFFNESS
+    n, steps = 64, 30
+    g = torch.Generator(device="cuda:0").manual_seed(9)
+    acts = [torch.rand(n, 33, device="cuda:0", generator=g) * 0.6 - 0.3 for _ in range(steps)]
+    runs = []
+    for off, writes in (("0", True), ("1", True), ("0", False)):
+        monkeypatch.setenv("TG_NO_SHARED_CACHE", off)
+        env = tia.make(seed=13, task="ThormangWalk", num_envs=n, sim_device="cuda:0", rl_device="cuda:0")
+        sim, out = env.sim, []
+        for t in range(steps):
+            if writes and t == 5:
+                vals = sim.dof_props[TG_PROP_STIFFNESS].clone()
+                vals[3] *= 0.5
+                sim.set_dof_properties_indexed(TG_PROP_STIFFNESS, vals, torch.tensor([3], device="cuda:0"))
+                sim.dof_props[TG_PROP_DAMPING, 7] *= 3.0          # view write, no refresh
+            if writes and t == 12:
+                sim.dof_props[TG_PROP_STIFFNESS, 11] *= 0.3       # view write + refresh
+                sim.refresh()
+            env.step(acts[t])
+            out.append(torch.cat([sim.root_state, sim.dof_state.view(n, -1)], 1).clone())
+        runs.append(out)
+        del env
+    for t, (a, b) in enumerate(zip(runs[0], runs[1])):
+        assert torch.equal(a, b), t
+    moved = (runs[0][-1] != runs[2][-1]).any(1).nonzero().flatten().tolist()
+    assert {3, 7, 11} <= set(moved), moved

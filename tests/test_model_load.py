@@ -19,6 +19,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 URDF = os.path.join(HERE, "golden", "urdf", "loader_tree.urdf")
 MESHES = os.path.join(HERE, "golden", "urdf")
 REF = "/root/reference/assets/urdf/gogoro"
+TG_ERR_MODEL = -3   # include/tgsim.h
 
 ARRAYS = [("link_parent", "num_links", 1, np.int32), ("link_group", "num_links", 1, np.int32),
           ("link_dof", "num_links", 1, np.int32), ("link_jtype", "num_links", 1, np.int32),
@@ -112,6 +113,65 @@ def test_native_loader_reports_errors():
     assert b"not found" in L.tg_model_last_error()
     bad = os.path.join(HERE, "golden", "urdf", "tyre.obj")   # not XML
     assert L.tg_model_parse(bad.encode(), None, None, 0, None, C.byref(h)) != 0
+
+
+MINI = """<robot name="r">
+  <link name="R"><inertial><mass value="{m}"/><inertia ixx="1" ixy="0" ixz="0" iyy="1" iyz="0" izz="1"/></inertial></link>
+  <link name="B"/><link name="C"/>
+  <joint name="rb" type="revolute"><parent link="R"/><child link="B"/><limit effort="1" velocity="1" lower="-1" upper="1"/></joint>
+  {extra}
+</robot>"""
+
+
+def _parse_text(tmp_path, text):
+    p = tmp_path / "m.urdf"
+    p.write_text(text)
+    L = lib()
+    h = C.c_void_p()
+    rc = L.tg_model_parse(str(p).encode(), None, None, 0, None, C.byref(h))
+    if rc == 0:
+        L.tg_model_free(h)
+    return rc, L.tg_model_last_error().decode()
+
+
+def test_native_loader_rejects_malformed_urdfs(tmp_path):
+    """a joint cycle (R->B, B->C, C->B), a link with two parent
+    joints, a malformed number and runaway element nesting each return
+    TG_ERR_MODEL with a message, instead of overflowing the stack or reading
+    the value as 0 as strtod did."""
+    ok = '<joint name="bc" type="fixed"><parent link="B"/><child link="C"/></joint>'
+    assert _parse_text(tmp_path, MINI.format(m="1.5", extra=ok))[0] == 0
+    cyc = ok + '<joint name="cb" type="fixed"><parent link="C"/><child link="B"/></joint>'
+    rc, msg = _parse_text(tmp_path, MINI.format(m="1.5", extra=cyc))
+    assert rc == TG_ERR_MODEL and "more than one joint" in msg, msg
+    rc, msg = _parse_text(tmp_path, MINI.format(m="1.5kg", extra=ok))
+    assert rc == TG_ERR_MODEL and "malformed number" in msg and "1.5kg" in msg, msg
+    rc, msg = _parse_text(tmp_path, MINI.format(m="", extra=ok))
+    assert rc == TG_ERR_MODEL and "malformed number" in msg, msg
+    deep = "<a>" * 5000 + "</a>" * 5000
+    rc, msg = _parse_text(tmp_path, MINI.format(m="1", extra=deep))
+    assert rc == TG_ERR_MODEL and "nested deeper" in msg, msg
+
+
+def test_native_loader_number_parsing_ignores_the_host_locale(tmp_path):
+    """A C / JNI host that set LC_NUMERIC to a comma-decimal locale still gets
+    0.5 for "0.5" (the parser reads in the classic locale)."""
+    import locale
+    ok = '<joint name="bc" type="fixed"><parent link="B"/><child link="C"/></joint>'
+    p = tmp_path / "m.urdf"
+    p.write_text(MINI.format(m="0.5", extra=ok))
+    saved = locale.setlocale(locale.LC_NUMERIC)
+    for name in ("de_DE.UTF-8", "de_DE.utf8", "fr_FR.UTF-8", "C"):
+        try:
+            locale.setlocale(locale.LC_NUMERIC, name)
+            break
+        except locale.Error:
+            continue
+    try:
+        a, _ = native(str(p))
+    finally:
+        locale.setlocale(locale.LC_NUMERIC, saved)
+    assert abs(a["link_inertia"][0] - 0.5) < 1e-7, a["link_inertia"][:10]
 
 
 @pytest.mark.skipif(not os.path.exists(REF), reason="reference assets not present (build container only)")

@@ -545,18 +545,17 @@ template <class M> __device__ __forceinline__ void compose_env(const StepArgs &a
     TG_CPROF(3)
 }
 
-// After a full compose: is every env's composite block and dof-property row
-// the same as env 0's?  One wavefront per env; a mismatch clears the flag
-// (set to 1 before the launch).  NaN compares unequal: never uniform.
+// After a full compose: is every env's composite block the same as env 0's?
+// One wavefront per env; a mismatch clears the flag (set to 1 before the
+// launch).  NaN compares unequal: never uniform.  (The DOF property rows are
+// not shared: the step kernel reads each env's own, so writes through the
+// dof_props view need no re-check.)
 template <class M> __global__ __launch_bounds__(64) void uniform_check_kernel(StepArgs a) {
     const int e = blockIdx.x, lane = threadIdx.x;
     if (e == 0 || e >= a.N) return;
     bool bad = false;
     const float *c = a.comp + (size_t)e * M::KC;
     for (int k = lane; k < M::KC; k += 64) bad |= c[k] != a.comp[k];
-    const size_t ND = (size_t)a.N * a.D;
-    for (int f = 0; f < TG_NUM_PROPS; ++f)
-        for (int d = lane; d < a.D; d += 64) bad |= a.props[f * ND + (size_t)e * a.D + d] != a.props[f * ND + d];
     if (__any(bad) && lane == 0) atomicExch(a.cuni, 0);
 }
 

@@ -102,6 +102,14 @@ std::string source_text(const char *struct_name, const char *model_source) {
     return s;
 }
 
+// the flags of the compiled-in articulation unit (build_ext.py UNITS); part of
+// the on-disk cache key (jit_compile), so a flag-only change never reuses a
+// code object built under other semantics
+const char *const JIT_OPTS[] = {"--offload-arch=gfx950", "-std=c++17", "-O3", "-ffast-math",
+                                "-ffp-contract=fast-honor-pragmas", "-munsafe-fp-atomics", "-fno-slp-vectorize",
+                                "-DTG_JIT=1"};
+constexpr int N_JIT_OPTS = (int)(sizeof JIT_OPTS / sizeof JIT_OPTS[0]);
+
 int compile(const std::string &src, const std::string &incdir, JitCode &out, std::string &err) {
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, src.c_str(), "tgjit_model.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
@@ -110,10 +118,10 @@ int compile(const std::string &src, const std::string &incdir, JitCode &out, std
     }
     for (int k = 0; k < NK; ++k) hiprtcAddNameExpression(prog, KERNEL_EXPR[k]);
     const std::string inc = "-I" + incdir;
-    // the flags of the compiled-in articulation unit (build_ext.py UNITS)
-    const char *opts[] = {"--offload-arch=gfx950", "-std=c++17", "-O3", "-ffast-math",
-                          "-ffp-contract=fast-honor-pragmas", "-munsafe-fp-atomics", "-fno-slp-vectorize", "-DTG_JIT=1", inc.c_str()};
-    const hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof opts / sizeof opts[0]), opts);
+    const char *opts[N_JIT_OPTS + 1];
+    for (int k = 0; k < N_JIT_OPTS; ++k) opts[k] = JIT_OPTS[k];
+    opts[N_JIT_OPTS] = inc.c_str();
+    const hiprtcResult rc = hiprtcCompileProgram(prog, N_JIT_OPTS + 1, opts);
     if (rc != HIPRTC_SUCCESS) {
         size_t n = 0;
         hiprtcGetProgramLogSize(prog, &n);
@@ -224,6 +232,11 @@ int jit_compile(uint64_t hash, const char *struct_name, const char *model_source
         }
         digest = fnv1a(digest, t);
     }
+    // the compile flags and the hipRTC version are part of the key too
+    for (int k = 0; k < N_JIT_OPTS; ++k) digest = fnv1a(digest, JIT_OPTS[k]);
+    int rtc_major = 0, rtc_minor = 0;
+    (void)hiprtcVersion(&rtc_major, &rtc_minor);
+    digest = fnv1a(digest, ("hiprtc " + std::to_string(rtc_major) + "." + std::to_string(rtc_minor)).c_str());
     {
         std::lock_guard<std::mutex> lk(g_mu);
         if (g_code.count(hash)) return 0;

@@ -28,6 +28,7 @@
 #include <cstring>
 #include <fstream>
 #include <functional>
+#include <locale>
 #include <map>
 #include <set>
 #include <sstream>
@@ -112,7 +113,10 @@ struct XmlReader {
             }
         }
     }
+    int depth = 0;
+    static constexpr int kMaxDepth = 256;   // nesting bound: no stack exhaustion on hostile input
     bool element(XNode &n) {   // at '<' of a start tag
+        if (++depth > kMaxDepth) return fail("elements nested deeper than " + std::to_string(kMaxDepth));
         ++p;
         const size_t b = p;
         while (p < s.size() && !std::isspace((unsigned char)s[p]) && s[p] != '>' && s[p] != '/') ++p;
@@ -123,6 +127,7 @@ struct XmlReader {
             if (s[p] == '/') {
                 if (p + 1 >= s.size() || s[p + 1] != '>') return fail("bad tag end in <" + n.tag);
                 p += 2;
+                --depth;
                 return true;
             }
             if (s[p] == '>') {
@@ -152,6 +157,7 @@ struct XmlReader {
                 while (!t.empty() && std::isspace((unsigned char)t.back())) t.pop_back();
                 if (t != n.tag) return fail("mismatched </" + t + "> for <" + n.tag + ">");
                 p = e + 1;
+                --depth;
                 return true;
             }
             n.kids.emplace_back();
@@ -199,6 +205,7 @@ bool vec_attr(const XNode *el, const char *key, int n, double dflt, double *out,
     const std::string *v = el->attr(key);
     if (!v) return true;
     std::istringstream is(*v);
+    is.imbue(std::locale::classic());   // '.' decimals whatever LC_NUMERIC the host set
     for (int i = 0; i < n; ++i)
         if (!(is >> out[i])) {
             err = std::string("expected ") + std::to_string(n) + " numbers in " + key + "=\"" + *v + "\"";
@@ -212,10 +219,22 @@ bool vec_attr(const XNode *el, const char *key, int n, double dflt, double *out,
     return true;
 }
 
-double num_attr(const XNode *el, const char *key, double dflt) {
-    if (!el) return dflt;
+// one number attribute (absent: dflt).  Parsed in the classic locale and
+// required to consume the whole value (surrounding blanks aside), as the
+// Python host's float() does: a malformed value is an error, not a silent 0
+bool num_attr(const XNode *el, const char *key, double dflt, double &out, std::string &err) {
+    out = dflt;
+    if (!el) return true;
     const std::string *v = el->attr(key);
-    return v ? std::strtod(v->c_str(), nullptr) : dflt;
+    if (!v) return true;
+    std::istringstream is(*v);
+    is.imbue(std::locale::classic());
+    std::string extra;
+    if (!(is >> out) || (is >> extra)) {
+        err = std::string("malformed number in ") + el->tag + " " + key + "=\"" + *v + "\"";
+        return false;
+    }
+    return true;
 }
 
 // URDF fixed-axis roll-pitch-yaw: R = Rz(y) Ry(p) Rx(r), row-major
@@ -400,7 +419,10 @@ bool build_model(const std::string &path, const std::string &name, const std::ve
             return false;
         }
         children[*pa->attr("link")].push_back(j);
-        child_names.insert(*ch->attr("link"));
+        if (!child_names.insert(*ch->attr("link")).second) {   // a tree: one parent joint per link
+            err = "URDF " + path + ": link " + *ch->attr("link") + " is the child of more than one joint";
+            return false;
+        }
     }
     std::vector<std::string> roots;
     for (const XNode *l : link_order)
@@ -412,6 +434,7 @@ bool build_model(const std::string &path, const std::string &name, const std::ve
     m.name = name;
     // depth-first, children in joint-declaration order (model/urdf.py load_urdf)
     std::function<int(const std::string &, int, int)> dfs;
+    std::set<std::string> visited;
     bool ok = true;
     dfs = [&](const std::string &lname, int parent, int joint) -> int {
         auto it = link_el.find(lname);
@@ -424,9 +447,17 @@ bool build_model(const std::string &path, const std::string &name, const std::ve
         L.name = lname;
         L.parent = parent;
         L.joint = joint;
+        if (!visited.insert(lname).second) {   // (unreachable with one parent per link; kept as the cycle guard)
+            err = "URDF: link " + lname + " reached twice (joint cycle)";
+            ok = false;
+            return -1;
+        }
         if (const XNode *in = it->second->child("inertial")) {
             const XNode *ms = in->child("mass");
-            L.mass = num_attr(ms, "value", 0.0);
+            if (!num_attr(ms, "value", 0.0, L.mass, err)) {
+                ok = false;
+                return -1;
+            }
             const XNode *o = in->child("origin");
             double rpy[3], R[9];
             if (!vec_attr(o, "xyz", 3, 0.0, L.com, err) || !vec_attr(o, "rpy", 3, 0.0, rpy, err)) {
@@ -434,8 +465,13 @@ bool build_model(const std::string &path, const std::string &name, const std::ve
                 return -1;
             }
             const XNode *ia = in->child("inertia");
-            const double ixx = num_attr(ia, "ixx", 0), ixy = num_attr(ia, "ixy", 0), ixz = num_attr(ia, "ixz", 0),
-                         iyy = num_attr(ia, "iyy", 0), iyz = num_attr(ia, "iyz", 0), izz = num_attr(ia, "izz", 0);
+            double ixx, ixy, ixz, iyy, iyz, izz;
+            if (!num_attr(ia, "ixx", 0, ixx, err) || !num_attr(ia, "ixy", 0, ixy, err) ||
+                !num_attr(ia, "ixz", 0, ixz, err) || !num_attr(ia, "iyy", 0, iyy, err) ||
+                !num_attr(ia, "iyz", 0, iyz, err) || !num_attr(ia, "izz", 0, izz, err)) {
+                ok = false;
+                return -1;
+            }
             const double I[9] = {ixx, ixy, ixz, ixy, iyy, iyz, ixz, iyz, izz};
             rpy_to_matrix(rpy, R);
             double RI[9], Rt[9], Iw[9];
@@ -480,11 +516,15 @@ bool build_model(const std::string &path, const std::string &name, const std::ve
             if (nrm == 0.0) nrm = 1.0;
             for (int k = 0; k < 3; ++k) J.axis[k] /= nrm;
             if (const XNode *lim = j->child("limit")) {
-                J.effort = num_attr(lim, "effort", 0.0);
-                J.velocity = num_attr(lim, "velocity", 0.0);
+                if (!num_attr(lim, "effort", 0.0, J.effort, err) || !num_attr(lim, "velocity", 0.0, J.velocity, err)) {
+                    ok = false;
+                    return -1;
+                }
                 if (jt != "continuous" && J.jtype != J_FIXED) {
-                    J.lower = num_attr(lim, "lower", 0.0);
-                    J.upper = num_attr(lim, "upper", 0.0);
+                    if (!num_attr(lim, "lower", 0.0, J.lower, err) || !num_attr(lim, "upper", 0.0, J.upper, err)) {
+                        ok = false;
+                        return -1;
+                    }
                     J.has_limits = true;
                 }
             }
@@ -543,7 +583,7 @@ bool build_model(const std::string &path, const std::string &name, const std::ve
                 m.shapes.push_back(S);
             } else if (g.tag == "sphere") {
                 S.kind = S_SPHERE;
-                S.params[0] = num_attr(&g, "radius", 0.0);
+                if (!num_attr(&g, "radius", 0.0, S.params[0], err)) return false;
                 S.np = 1;
                 m.shapes.push_back(S);
             }

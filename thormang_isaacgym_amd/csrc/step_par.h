@@ -584,8 +584,12 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
 #ifdef TG_EXP_HOT   // developer experiment: every env reads env (e % 64)'s inputs (cache-resident)
     const int ein = e % 64;
 #else
-    // every env reads env 0's composite block and property rows while they are
-    // all equal (a.cuni, uniform_check_kernel): one shared, cache-resident copy
+    // every env reads env 0's composite block while all blocks are equal
+    // (a.cuni, uniform_check_kernel): one shared, cache-resident copy.  The
+    // composites change only through a compose, which re-runs the check; the
+    // DOF property rows are read per env always, so a write through the
+    // zero-copy dof_props view takes effect at the next step as it does
+    // without the shared cache
     const int ein = (a.cuni && *a.cuni) ? 0 : e;
 #endif
     // per-env inputs through 32-bit element offsets from the uniform base
@@ -595,7 +599,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
     // 32-bit vector-offset form, no 64-bit address arithmetic per load)
     auto CP = [&](int k) { return at_u32<float>(comp, (cbase + (unsigned)k) * 4u); };
     auto CP4 = [&](int k) { return at_u32<float4>(comp, (cbase + (unsigned)k) * 4u); };
-    const unsigned ND = (unsigned)N * (unsigned)D, pbase = (unsigned)ein * (unsigned)D;
+    const unsigned ND = (unsigned)N * (unsigned)D, pbase = (unsigned)e * (unsigned)D;
     auto PR = [&](int f, int d) { return at_u32<float>(a.props, ((unsigned)f * ND + pbase + (unsigned)d) * 4u); };
     const bool lead = sub == 0;
 
@@ -2017,8 +2021,14 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                         }
                     }
                     if constexpr (T) {
+                        // TGS: a normal row's bias-free target is re-formed from its
+                        // final separation over the whole substep h, not the sub-step
+                        // hs: the velocity stored here is the one the next substep
+                        // starts from, and a speculative bound over hs gave it a gain
+                        // of N/h on the residual gap (DESIGN.md §2 "TGS conditioning")
 #pragma unroll
-                        for (int jj = 0; jj < JL; ++jj) tgo[jj] = fminf(tgo[jj], 0.f);
+                        for (int jj = 0; jj < JL; ++jj)
+                            tgo[jj] = nrm[jj] ? fminf(-(phio[jj] + dsp[jj] - a.rest) / h, 0.f) : fminf(tgo[jj], 0.f);
                     } else {
 #pragma unroll
                         for (int i = 0; i < K; ++i) tg[i] = fminf(tg[i], 0.f);
@@ -2140,7 +2150,9 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                         for (int i = 0; i < K; ++i) s(PL::W + i) = tgs ? lbar[i] * inv : lam[i];
                     }
 #pragma unroll
-                    for (int i = 0; i < K; ++i) tg[i] = fminf(tg[i], 0.f);
+                    for (int i = 0; i < K; ++i)   // (TGS: over h, as the 16-lane sweeps)
+                        tg[i] = (tgs && row_normal<M>(i)) ? fminf(-(phi[i] + dsp[i] - a.rest) / h, 0.f)
+                                                          : fminf(tg[i], 0.f);
                     if (a.viters > 0) sweeps(a.viters, false);
                 }
                 if (lead) {

@@ -100,11 +100,11 @@ struct StepArgs {
     // gp_in_step: the Gogoro pre-physics (gp) runs at the start of the step
     // kernel (lead lane; values through the env's LDS) instead of in compose
     int gp_in_step;
-    // cuni (or null): a device flag, 1 while every env's composite block and
-    // dof property rows equal env 0's (uniform_check_kernel after each full
-    // compose); the step kernel then reads env 0's copy for every env, so the
-    // per-env cache costs L2 hits, not HBM reads (models whose task kernels
-    // edit composites / properties in place never get the flag)
+    // cuni (or null): a device flag, 1 while every env's composite block
+    // equals env 0's (uniform_check_kernel after each full compose); the step
+    // kernel then reads env 0's block for every env, so the per-env cache
+    // costs L2 hits, not HBM reads (models whose task kernels edit composites
+    // in place never get the flag).  DOF property rows are always per env.
     int *cuni;
     // pp_in_step: the GogoroPaper pre-physics (pp) likewise (models with the
     // pre-physics slots, codegen FUSED bits 2 | 4)

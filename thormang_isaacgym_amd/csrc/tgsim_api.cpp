@@ -218,6 +218,8 @@ int tg_sim_create(const tg_model_desc *m, const tg_sim_params *params, int32_t n
     if (params->substeps <= 0 || !(params->dt > 0.f)) return fail(TG_ERR_ARG, "dt and substeps must be positive");
     if (params->contact_iterations < 0 || params->velocity_iterations < 0)
         return fail(TG_ERR_ARG, "contact / velocity iterations must be >= 0");
+    if (params->solver_type != 0 && params->solver_type != 1)
+        return fail(TG_ERR_ARG, "solver_type must be 0 (PGS) or 1 (TGS), got %d", params->solver_type);
     int kc = tg::model_kc(m->model_hash);
     if (kc < 0)
         return fail(TG_ERR_MODEL,
@@ -636,11 +638,14 @@ int tg_set_sim_params(tg_sim *s, const tg_sim_params *p) {
     if (p->substeps < 0 || !(p->dt > 0.f)) return fail(TG_ERR_ARG, "dt must be positive and substeps >= 0");
     if (p->contact_iterations < 0 || p->velocity_iterations < 0)
         return fail(TG_ERR_ARG, "contact / velocity iterations must be >= 0");
+    if (p->solver_type != 0 && p->solver_type != 1)
+        return fail(TG_ERR_ARG, "solver_type must be 0 (PGS) or 1 (TGS), got %d", p->solver_type);
     const float spacing = s->params.env_spacing;
-    const int32_t per_row = s->params.envs_per_row;
+    const int32_t per_row = s->params.envs_per_row, fix_base = s->params.fix_base;
     s->params = *p;
-    s->params.env_spacing = spacing;   // the env grid is fixed at creation
+    s->params.env_spacing = spacing;   // the env grid is fixed at creation,
     s->params.envs_per_row = per_row;
+    s->params.fix_base = fix_base;     // and so is the asset option fix_base_link
     memcpy(s->gravity, p->gravity, sizeof s->gravity);
     return TG_OK;
 }
