@@ -71,6 +71,11 @@ typedef struct tg_gogoro_params {
     int32_t dof_steer, dof_rear, dof_base_x, dof_base_y, dof_base_z;
     int32_t terrain_spawn;         /* USE_TERAIN: reset z = root_reset[:,2], the per-env terrain
                                       height - 0.03 clamped to [0, 100] (gogoro_new.py:523-534) */
+    int32_t absolute_steer;        /* INCREMENTAL_STEER = False (gogoro_new.py:27,353-356): the
+                                      command is action * max_steering, not the incremented one
+                                      (0, the registered module's value: incremental) */
+    int32_t debug_start_speed;     /* DEBUG_START_SPEED (gogoro_new.py:25,542-545): a reset env
+                                      starts at 1.3 m/s along its spawn heading (0: at rest) */
     uint64_t seed;                 /* Philox key for device draws */
 } tg_gogoro_params;
 

@@ -100,7 +100,8 @@ void oracle_gogoro_reward(int n, const float *buffer_obs, const int64_t *progres
         oracle_gogoro_reward_one(buffer_obs + 6 * e, progress[e], ah + 5 * e, max_len, rew + e, reset + e);
 }
 
-/* Gogoro.pre_physics_step -- tasks/gogoro_new.py:347-369 (INCREMENTAL_STEER = True, :27)
+/* Gogoro.pre_physics_step -- tasks/gogoro_new.py:347-369 (INCREMENTAL_STEER, :27: the
+ * incremented command :351-354, or with p->absolute_steer the absolute one :355-356)
  * plus VecTask.step's action clamp (vec_task.py:327). */
 void oracle_gogoro_pre_physics(const tg_gogoro_params *p, tg_gogoro_buffers *b, const float *actions,
                                const float *pre_draws) {
@@ -110,8 +111,13 @@ void oracle_gogoro_pre_physics(const tg_gogoro_params *p, tg_gogoro_buffers *b, 
         float *ah = b->action_history + 5 * e;
         for (int k = 0; k < 4; ++k) ah[k] = ah[k + 1];
         ah[4] = a;
-        float da = t_clamp(a * p->max_steering_change, -p->max_steering_change, p->max_steering_change);
-        float c = b->curent_command[e] + da;
+        float c;
+        if (p->absolute_steer) {
+            c = a * p->max_steering;
+        } else {
+            float da = t_clamp(a * p->max_steering_change, -p->max_steering_change, p->max_steering_change);
+            c = b->curent_command[e] + da;
+        }
         c = t_clamp(c, -p->max_steering, p->max_steering);
         b->curent_command[e] = c;
         float noise = p->steering_action_noise[0] + pre_draws[e] * p->steering_action_noise[1];
@@ -148,6 +154,10 @@ void oracle_gogoro_reset_env(const tg_gogoro_params *p, tg_gogoro_buffers *b, in
     root[5] = sinf(h);
     root[6] = cosf(h);
     for (int k = 7; k < 13; ++k) root[k] = 0.0f;
+    if (p->debug_start_speed) {   /* DEBUG_START_SPEED, gogoro_new.py:542-545 */
+        root[7] = 1.3f * cosf(rot);
+        root[8] = 1.3f * sinf(rot);
+    }
     for (int d = 0; d < D; ++d) {
         b->dof_state[2 * (e * D + d)] = b->thormang_pose[d];
         b->dof_state[2 * (e * D + d) + 1] = 0.0f;

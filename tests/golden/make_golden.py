@@ -14,6 +14,10 @@ recorder stubs for ``gymapi``/``gymtorch``) and drives:
   synthetic random walk; every torch.rand/randn draw the reference makes is
   recorded (order, size, raw values) so the build can replay them
                                                                 -> gogoro_steps.npz
+* the same loop with the module's two other switches flipped:
+  INCREMENTAL_STEER = False (absolute steering, gogoro_new.py:355-356) and
+  DEBUG_START_SPEED = True (reset envs start at 1.3 m/s, :542-545)
+                                                                -> gogoro_steps_flags.npz
 
 Only data (inputs + outputs) is written; no reference source leaves the
 container.  Re-run:  python tests/golden/make_golden.py
@@ -382,7 +386,18 @@ def fixture_reward(gg, rs):
                 reward=rew.numpy(), reset=reset.numpy().astype(np.int64))
 
 
-def fixture_steps(vt, gg, n_envs=16, T=90, max_steps=30, freq=7, seed=1234):
+def fixture_steps(vt, gg, n_envs=16, T=90, max_steps=30, freq=7, seed=1234, flags=None):
+    saved = {k: getattr(gg, k) for k in (flags or {})}
+    for k, v in (flags or {}).items():
+        setattr(gg, k, v)
+    try:
+        return _fixture_steps(vt, gg, n_envs, T, max_steps, freq, seed, flags or {})
+    finally:
+        for k, v in saved.items():
+            setattr(gg, k, v)
+
+
+def _fixture_steps(vt, gg, n_envs, T, max_steps, freq, seed, flags):
     torch.manual_seed(seed)
     fake_rs = np.random.default_rng(seed + 1)
     act_rs = np.random.default_rng(seed + 2)
@@ -441,7 +456,8 @@ def fixture_steps(vt, gg, n_envs=16, T=90, max_steps=30, freq=7, seed=1234):
     out = {k: np.stack(v) for k, v in rec.items()}
     out.update({f"init_{k}": v for k, v in init.items()})
     out.update(draw_kind=kinds, draw_size=sizes, draw_vals=vals, n_envs=np.int64(n_envs), max_steps=np.int64(max_steps),
-               freq=np.int64(freq), dof_names=np.array(model.dof_names))
+               freq=np.int64(freq), dof_names=np.array(model.dof_names),
+               incremental_steer=np.int64(gg.INCREMENTAL_STEER), debug_start_speed=np.int64(gg.DEBUG_START_SPEED))
     return out
 
 
@@ -451,7 +467,9 @@ def main():
     np.savez_compressed(os.path.join(HERE, "gogoro_obs.npz"), **fixture_obs(gg, rs))
     np.savez_compressed(os.path.join(HERE, "gogoro_reward.npz"), **fixture_reward(gg, rs))
     np.savez_compressed(os.path.join(HERE, "gogoro_steps.npz"), **fixture_steps(vt, gg))
-    for f in ("gogoro_obs.npz", "gogoro_reward.npz", "gogoro_steps.npz"):
+    np.savez_compressed(os.path.join(HERE, "gogoro_steps_flags.npz"),
+                        **fixture_steps(vt, gg, seed=4321, flags=dict(INCREMENTAL_STEER=False, DEBUG_START_SPEED=True)))
+    for f in ("gogoro_obs.npz", "gogoro_reward.npz", "gogoro_steps.npz", "gogoro_steps_flags.npz"):
         print(f, os.path.getsize(os.path.join(HERE, f)))
 
 

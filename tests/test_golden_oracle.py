@@ -72,6 +72,9 @@ class HostGogoro:
         self.D = D = len(names)
         self.cfg = gogoro_cfg(n, int(f["max_steps"]), int(f["freq"]))
         self.p = gogoro_params(self.cfg, self.dni, n)
+        # the module switches the fixture was recorded under (gogoro_new.py:25,27)
+        self.p.absolute_steer = int(not int(f["incremental_steer"]))
+        self.p.debug_start_speed = int(f["debug_start_speed"])
         z = lambda *s, dt=np.float32: np.zeros(s, dt)
         self.a = dict(obs_buf=z(n, 6), rew_buf=z(n), reset_buf=np.ones(n, np.int64), progress_buf=z(n, dt=np.int64),
                       timeout_buf=z(n, dt=np.uint8), action_history=z(n, 5), curent_command=z(n), yaw_command=z(n),
@@ -90,11 +93,14 @@ class HostGogoro:
             lib().oracle_gogoro_reset_env(C.byref(self.p), C.byref(self.b), e, ptr(np.ascontiguousarray(rd[e])))
 
 
-def test_oracle_replays_reference_steps():
+@pytest.mark.parametrize("fixture", ["gogoro_steps.npz", "gogoro_steps_flags.npz"])
+def test_oracle_replays_reference_steps(fixture):
     """Full VecTask.step loop: pre_physics_step -> (recorded physics) ->
     post_physics_step incl. resets, sensor noise, command resampling and
-    timeouts, with the reference's recorded draws replayed in order."""
-    f = load("gogoro_steps.npz")
+    timeouts, with the reference's recorded draws replayed in order.  The
+    second fixture flips the module's INCREMENTAL_STEER and DEBUG_START_SPEED
+    switches (gogoro_new.py:25,27)."""
+    f = load(fixture)
     h = HostGogoro(f)
     a, n = h.a, h.n
     src = RecordedDraws(f["draw_kind"], f["draw_size"], f["draw_vals"])

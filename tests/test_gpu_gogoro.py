@@ -24,14 +24,27 @@ def _cuda():
         pytest.skip("needs the MI355X")
 
 
-def test_gpu_task_kernels_replay_reference_steps():
+def _flags(monkeypatch, f):
+    """The module switches the fixture was recorded under (gogoro_new.py:25,27),
+    read by Gogoro.__init__."""
+    from thormang_isaacgym_amd.tasks import gogoro as gmod
+    monkeypatch.setattr(gmod, "INCREMENTAL_STEER", bool(int(f["incremental_steer"])))
+    monkeypatch.setattr(gmod, "DEBUG_START_SPEED", bool(int(f["debug_start_speed"])))
+
+
+FIXTURES = ["gogoro_steps.npz", "gogoro_steps_flags.npz"]
+
+
+@pytest.mark.parametrize("fixture", FIXTURES)
+def test_gpu_task_kernels_replay_reference_steps(fixture, monkeypatch):
     _cuda()
     from thormang_isaacgym_amd.abi import TG_PROP_DAMPING, TG_PROP_LOWER, TG_PROP_STIFFNESS, TG_PROP_UPPER
     from thormang_isaacgym_amd.tasks.gogoro import Gogoro
     from thormang_isaacgym_amd.tasks.gogoro_draws import RecordedDraws
     from tests.golden.make_golden import gogoro_cfg
 
-    f = np.load(os.path.join(GOLDEN, "gogoro_steps.npz"))
+    f = np.load(os.path.join(GOLDEN, fixture))
+    _flags(monkeypatch, f)
     n = int(f["n_envs"])
     src = RecordedDraws(f["draw_kind"], f["draw_size"], f["draw_vals"])
     state = {"t": 0}
@@ -81,7 +94,8 @@ def test_gpu_task_kernels_replay_reference_steps():
     assert src.i == len(f["draw_kind"])
 
 
-def test_gpu_fused_step_replays_reference_steps():
+@pytest.mark.parametrize("fixture", FIXTURES)
+def test_gpu_fused_step_replays_reference_steps(fixture, monkeypatch):
     """The golden fixture through the TIMED path: ``Gogoro.step`` ->
     tg_gogoro_step, one launch of the step kernel with the pre-physics at its
     start and the GogoroPost epilogue (masked resets with in-place seat
@@ -93,14 +107,16 @@ def test_gpu_fused_step_replays_reference_steps():
     step kernel's semantics: the root state makes a frame round trip through
     the kernel (2e-6), and a locked dof of a non-reset env is stored at the
     centre of its lock window (the simulated state), not the fixture's
-    synthetic value."""
+    synthetic value.  The second fixture flips the module's INCREMENTAL_STEER
+    and DEBUG_START_SPEED switches (absolute steering, reset envs at 1.3 m/s)."""
     _cuda()
     from thormang_isaacgym_amd.abi import TG_PROP_DAMPING, TG_PROP_LOWER, TG_PROP_STIFFNESS, TG_PROP_UPPER
     from thormang_isaacgym_amd.tasks.gogoro import Gogoro
     from thormang_isaacgym_amd.tasks.gogoro_draws import RecordedDraws
     from tests.golden.make_golden import gogoro_cfg
 
-    f = np.load(os.path.join(GOLDEN, "gogoro_steps.npz"))
+    f = np.load(os.path.join(GOLDEN, fixture))
+    _flags(monkeypatch, f)
     n = int(f["n_envs"])
     src = RecordedDraws(f["draw_kind"], f["draw_size"], f["draw_vals"])
 

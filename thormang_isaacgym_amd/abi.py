@@ -73,7 +73,8 @@ class tg_gogoro_params(C.Structure):
         ("max_episode_length", C.c_int64), ("speed_freq_update", C.c_int32), ("yaw_freq_update", C.c_int32),
         ("num_envs", C.c_int32), ("num_dof", C.c_int32),
         ("dof_steer", C.c_int32), ("dof_rear", C.c_int32), ("dof_base_x", C.c_int32), ("dof_base_y", C.c_int32),
-        ("dof_base_z", C.c_int32), ("terrain_spawn", C.c_int32), ("seed", C.c_uint64),
+        ("dof_base_z", C.c_int32), ("terrain_spawn", C.c_int32),
+        ("absolute_steer", C.c_int32), ("debug_start_speed", C.c_int32), ("seed", C.c_uint64),
     ]
 
 

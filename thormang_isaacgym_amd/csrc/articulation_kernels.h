@@ -119,9 +119,14 @@ __device__ __forceinline__ void gogoro_pre_values(const GogoroPre &g, int e, flo
     const float *ah0 = g.action_history + 5 * (size_t)e;
     ah[0] = ah0[1]; ah[1] = ah0[2]; ah[2] = ah0[3]; ah[3] = ah0[4]; ah[4] = a;
     const float m = g.max_steering_change, ms = g.max_steering;
-    float da = a * m;
-    da = da < -m ? -m : (da > m ? m : da);
-    float c = g.curent_command[e] + da;
+    float c;
+    if (g.absolute_steer) {   // INCREMENTAL_STEER = False (gogoro_new.py:355-356)
+        c = a * ms;
+    } else {
+        float da = a * m;
+        da = da < -m ? -m : (da > m ? m : da);
+        c = g.curent_command[e] + da;
+    }
     c = c < -ms ? -ms : (c > ms ? ms : c);
     cmd = c;
     float r;
@@ -1554,6 +1559,10 @@ struct GogoroPost {
             rt[6] = cosf(hh);
 #pragma unroll
             for (int k = 7; k < 13; ++k) rt[k] = 0.0f;
+            if (p.debug_start_speed) {   // DEBUG_START_SPEED (gogoro_new.py:542-545)
+                rt[7] = 1.3f * cosf(rot);
+                rt[8] = 1.3f * sinf(rot);
+            }
             float cv[5];
             cv[0] = n_aff(p.seat_offset_x_range, r[5]);
             cv[1] = n_aff(p.seat_offset_y_range, r[6]);

@@ -29,8 +29,13 @@ __global__ __launch_bounds__(256) void pre_kernel(tg_gogoro_params p, tg_gogoro_
     float *ah = b.action_history + 5 * e;
     float h0 = ah[1], h1 = ah[2], h2 = ah[3], h3 = ah[4];
     ah[0] = h0; ah[1] = h1; ah[2] = h2; ah[3] = h3; ah[4] = a;
-    float da = t_clamp(a * p.max_steering_change, -p.max_steering_change, p.max_steering_change);
-    float c = t_clamp(b.curent_command[e] + da, -p.max_steering, p.max_steering);
+    float c;
+    if (p.absolute_steer) {   // INCREMENTAL_STEER = False (gogoro_new.py:355-356)
+        c = t_clamp(a * p.max_steering, -p.max_steering, p.max_steering);
+    } else {
+        float da = t_clamp(a * p.max_steering_change, -p.max_steering_change, p.max_steering_change);
+        c = t_clamp(b.curent_command[e] + da, -p.max_steering, p.max_steering);
+    }
     b.curent_command[e] = c;
     float r;
     if (pre_draws) r = pre_draws[e];
@@ -63,6 +68,10 @@ __device__ void reset_env(const tg_gogoro_params &p, const tg_gogoro_buffers &b,
     root[6] = cosf(hh);
 #pragma unroll
     for (int k = 7; k < 13; ++k) root[k] = 0.0f;
+    if (p.debug_start_speed) {   // DEBUG_START_SPEED (gogoro_new.py:542-545)
+        root[7] = 1.3f * cosf(rot);
+        root[8] = 1.3f * sinf(rot);
+    }
     float *dof = b.dof_state + 2 * (size_t)e * D;
 #pragma unroll 8
     for (int d = 0; d < D; ++d) {   // unrolled: 8 pose loads in flight instead of one per store
@@ -174,6 +183,10 @@ __global__ __launch_bounds__(64) void post_kernel(tg_gogoro_params p, tg_gogoro_
             rt[6] = cosf(hh);
 #pragma unroll
             for (int k = 7; k < 13; ++k) rt[k] = 0.0f;
+            if (p.debug_start_speed) {   // DEBUG_START_SPEED (gogoro_new.py:542-545)
+                rt[7] = 1.3f * cosf(rot);
+                rt[8] = 1.3f * sinf(rot);
+            }
             float cv[5];
             cv[0] = n_aff(p.seat_offset_x_range, r[5]);
             cv[1] = n_aff(p.seat_offset_y_range, r[6]);

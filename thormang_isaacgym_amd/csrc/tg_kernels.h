@@ -24,6 +24,7 @@ struct GogoroPre {
     const float *pre_draws;   // [N] replayed steering-noise N(0,1) draws, or null (Philox)
     float clip_actions, max_steering_change, max_steering, noise_mean, noise_std;
     int dof_steer, dof_rear;
+    int absolute_steer;       // INCREMENTAL_STEER = False (tg_gogoro_params.absolute_steer)
     uint32_t k0, k1, c_lo, c_hi;
 };
 

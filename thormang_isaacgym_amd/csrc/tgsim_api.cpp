@@ -814,6 +814,7 @@ int tg_gogoro_step(tg_sim *s, const tg_gogoro_params *p, const tg_gogoro_buffers
             g.noise_std = p->steering_action_noise[1];
             g.dof_steer = p->dof_steer;
             g.dof_rear = p->dof_rear;
+            g.absolute_steer = p->absolute_steer;
             g.k0 = (uint32_t)p->seed;
             g.k1 = (uint32_t)(p->seed >> 32);
             g.c_lo = (uint32_t)counter_pre;

@@ -40,8 +40,12 @@ from .gogoro_cfg import ASSET_OPTIONS, check_lock_set, gogoro_params, initial_do
 from .gogoro_draws import post_draws, reset_draws
 from .terrain import Terrain
 
-# module-level switches of the reference (gogoro_new.py:22-27)
+# module-level switches of the reference (gogoro_new.py:22-27), read when an
+# env is created: DEBUG_START_SPEED (:25, :542-545) starts a reset env at
+# 1.3 m/s along its spawn heading; INCREMENTAL_STEER = False (:27, :355-356)
+# makes the command action * max_steering instead of an increment
 DEBUGFIXBASE = False
+DEBUG_START_SPEED = False
 USE_TERAIN = False
 INCREMENTAL_STEER = True
 
@@ -55,8 +59,6 @@ class Gogoro(VecTask):
     draw_source = None
 
     def __init__(self, cfg, rl_device, sim_device, graphics_device_id, headless, virtual_screen_capture, force_render):
-        if not INCREMENTAL_STEER:
-            raise NotImplementedError("only the registered INCREMENTAL_STEER=True behaviour is fused")
         self.curent_step = 0
         self.device = pipeline_device(cfg, sim_device)   # the sim GPU (also for the CPU pipeline)
         self.n_envs = cfg["env"]["numEnvs"]
@@ -119,6 +121,8 @@ class Gogoro(VecTask):
         self.root_reset_tensor[:, 7:13] = 0
         self.curent_perturbations = torch.zeros(self.n_envs, self.num_rgbd, 3, device=self.device)
         self.params = gogoro_params(self.cfg, self.dof_name_to_id, self.n_envs, self.seed)
+        self.params.absolute_steer = int(not INCREMENTAL_STEER)
+        self.params.debug_start_speed = int(bool(DEBUG_START_SPEED))
         if self.terrain is not None:
             self.root_reset_tensor[:, 2] = self._terrain_spawn_z()
             self.params.terrain_spawn = 1
