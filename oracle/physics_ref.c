@@ -877,8 +877,8 @@ static void solve_contacts(const Env *e, Work *w, real h, real *qds, V6 v0s, rea
          * velocity after every earlier sweep, the linearised motion of the
          * sub-steps); the positions integrate the mean of the N sweeps'
          * multipliers (the mean sub-step velocity, velocity being affine in
-         * the multipliers); the velocity iterations continue from the last
-         * sweep's multipliers with the push-out removed. */
+         * the multipliers); the velocity iterations start from that mean
+         * (warm start) with the push-out removed and the targets formed over h. */
         const int N = e->sp->contact_iterations;
         const real hs = h / N;
         real disp[3 * MAXC], lbar[3 * MAXC];
@@ -907,8 +907,16 @@ static void solve_contacts(const Env *e, Work *w, real h, real *qds, V6 v0s, rea
             target[i] = target[i] < 0 ? target[i] : 0;
             lbar[i] /= N;
         }
+        /* the velocity iterations are warm-started from the sub-steps' MEAN
+         * multipliers (the velocity of the step's displacement), not the last
+         * sub-step's: a contact that closes its gap in the last sub-step
+         * leaves that sub-step with the velocity -gap/hs, a gain of N/h on the
+         * gap, which one bias-free sweep does not undo (ThormangWalk one-step
+         * f32-vs-f64 error 1.5e-4 -> 4.2e-5, the PGS level; DESIGN.md §2 "TGS
+         * conditioning").  Without velocity iterations the stored velocity is
+         * the last sub-step's, as the position iterations leave it. */
         real lamv[3 * MAXC];
-        memcpy(lamv, lam, sizeof(real) * K);
+        memcpy(lamv, e->sp->velocity_iterations > 0 ? lbar : lam, sizeof(real) * K);
         if (e->sp->velocity_iterations > 0)
             pgs_sweeps(K, npatch, patches, rows, target, W, vfree, lamv, e->sp->velocity_iterations);
         apply_impulses(e, w, rows, K, lamv, qdv, v0v);

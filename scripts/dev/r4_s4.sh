@@ -1,0 +1,7 @@
+set -u
+mkdir -p gpurun_out/s4
+export PYTHONUNBUFFERED=1
+timeout -k 10 600 python -u scripts/dev/r4_walk_forced.py 1,0 > gpurun_out/s4/forced_default.log 2>&1 || { tail -5 gpurun_out/s4/forced_default.log; exit 1; }
+cat gpurun_out/s4/forced_default.log | grep solver_type | cut -c1-400
+TG_LIB_PATH=thormang_isaacgym_amd/libtgsim_refresh.so timeout -k 10 600 python -u scripts/dev/r4_walk_forced.py 1 > gpurun_out/s4/forced_refresh.log 2>&1 || { tail -5 gpurun_out/s4/forced_refresh.log; exit 1; }
+cat gpurun_out/s4/forced_refresh.log | grep solver_type | cut -c1-400

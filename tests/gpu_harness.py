@@ -323,11 +323,17 @@ def gogoro_terrain(num_envs=64, steps=300, seed=0, max_steps=300, terrain_seed=5
         set_heightfield(None)
 
 
-def walk_forced(num_envs=32, steps=1000, seed=0, task="ThormangWalk", dr=False):
-    env = make_gpu_walk(walk_cfg(num_envs, task, dr=dr), NumpyDraws(seed))
-    orc = OracleWalk(walk_cfg(num_envs, task, dr=dr), NumpyDraws(seed))
+def walk_forced(num_envs=32, steps=1000, seed=0, task="ThormangWalk", dr=False, control=False, solver_type=None):
+    """Teacher-forced walk (the oracle re-synced from the GPU env before every
+    step); with ``control`` the fp32 oracle build is re-synced and stepped
+    beside the fp64 one (``within``)."""
+    mk = lambda: walk_cfg(num_envs, task, dr=dr, solver_type=solver_type)
+    env = make_gpu_walk(mk(), NumpyDraws(seed))
+    orc = OracleWalk(mk(), NumpyDraws(seed))
+    ctl = OracleWalk(mk(), NumpyDraws(seed), precision="f32") if control else None
     rs = np.random.default_rng(seed + 100)
-    return forced_step_errors(env, orc, lambda o: rs.uniform(-0.5, 0.5, (num_envs, orc.D)).astype(np.float32), steps)
+    return forced_step_errors(env, orc, lambda o: rs.uniform(-0.5, 0.5, (num_envs, orc.D)).astype(np.float32), steps,
+                              ctl=ctl)
 
 
 # ----------------------------------------------------------------------------- ThormangWalk

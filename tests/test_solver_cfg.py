@@ -166,3 +166,14 @@ def test_tgs_speculative_landing_stores_no_approach_velocity():
         assert abs((r[2] - z0) + 0.001) < 2e-4, r[2] - z0   # moved down by about the gap
     assert abs(rp[9] + 0.1) < 1e-3, rp[9]                   # PGS: -gap/h stored
     assert abs(rt[9]) < 0.02, rt[9]                         # TGS: at rest at the ground
+
+
+def test_tgs_velocity_iterations_warm_start_from_the_mean_and_stop_the_landing():
+    """With velocity iterations TGS warm-starts them from the sub-steps' mean
+    multipliers (DESIGN.md §2 "TGS conditioning"): the box of the landing
+    above is still stopped at the ground over the step, and the bias-free
+    sweeps (targets over h from the final separation, about 0) remove the
+    approach velocity the mean carries."""
+    z0, r = _push_out(4, solver=1, depth=-0.001, vz=-1.0)
+    assert abs((r[2] - z0) + 0.001) < 2e-4, r[2] - z0
+    assert abs(r[9]) < 0.02, r[9]

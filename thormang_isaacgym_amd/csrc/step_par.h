@@ -1893,7 +1893,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 // separations and displacements)
                 // PGS: every lane holds every row's target (tg), as before TGS;
                 // TGS: the owner lane holds its rows' moving targets (tgo)
-                float wr[JL][K], rv[JL], tgo[JT], tg[T ? 1 : K], phio[JT], dsp[JT], wd[K], lam[K], lbar[KT];
+                float wr[JL][K], rv[JL], tgo[JT], tg[T ? 1 : K], phio[JT], dsp[JT], rvs[JT], wd[K], lam[K], lbar[KT];
                 bool nrm[JT];
                 const float hs = T ? h / (float)a.iters : h;   // (TGS sub-step)
 #pragma unroll
@@ -1907,6 +1907,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                         nrm[jj] = k < K && row_normal<M>(k);
                         phio[jj] = t6;
                         dsp[jj] = 0.f;
+                        rvs[jj] = 0.f;
                         tgo[jj] = nrm[jj] ? contact_target(a, t6, hs) : t6;
                     }
                 }
@@ -1998,6 +1999,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                         // separation; the multipliers accumulate for their mean
 #pragma unroll
                         for (int jj = 0; jj < JL; ++jj) {
+                            rvs[jj] += rv[jj];   // (the row velocity of the mean multipliers, rv being affine in them)
                             dsp[jj] += hs * rv[jj];
                             tgo[jj] = nrm[jj] ? contact_target(a, phio[jj] + dsp[jj], hs) : tgo[jj];
                         }
@@ -2023,12 +2025,21 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     if constexpr (T) {
                         // TGS: a normal row's bias-free target is re-formed from its
                         // final separation over the whole substep h, not the sub-step
-                        // hs: the velocity stored here is the one the next substep
-                        // starts from, and a speculative bound over hs gave it a gain
-                        // of N/h on the residual gap (DESIGN.md §2 "TGS conditioning")
+                        // hs, and the velocity iterations start from the sub-steps'
+                        // mean multipliers, not the last sub-step's: the velocity
+                        // stored here is the one the next substep starts from, and
+                        // either sub-step form gave it a gain of N/h on a contact's
+                        // residual gap (DESIGN.md §2 "TGS conditioning")
+                        // (no velocity iterations: the last sub-step's velocity is stored)
+                        const float inv = 1.0f / (float)a.iters;
+                        const bool mean = a.viters > 0;
 #pragma unroll
-                        for (int jj = 0; jj < JL; ++jj)
+                        for (int jj = 0; jj < JL; ++jj) {
                             tgo[jj] = nrm[jj] ? fminf(-(phio[jj] + dsp[jj] - a.rest) / h, 0.f) : fminf(tgo[jj], 0.f);
+                            rv[jj] = mean ? rvs[jj] * inv : rv[jj];
+                        }
+#pragma unroll
+                        for (int i = 0; i < K; ++i) lam[i] = mean ? lbar[i] * inv : lam[i];
                     } else {
 #pragma unroll
                         for (int i = 0; i < K; ++i) tg[i] = fminf(tg[i], 0.f);
@@ -2150,9 +2161,11 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                         for (int i = 0; i < K; ++i) s(PL::W + i) = tgs ? lbar[i] * inv : lam[i];
                     }
 #pragma unroll
-                    for (int i = 0; i < K; ++i)   // (TGS: over h, as the 16-lane sweeps)
+                    for (int i = 0; i < K; ++i) {   // (TGS: over h, from the mean multipliers, as the 16-lane sweeps)
                         tg[i] = (tgs && row_normal<M>(i)) ? fminf(-(phi[i] + dsp[i] - a.rest) / h, 0.f)
                                                           : fminf(tg[i], 0.f);
+                        if (tgs && a.viters > 0) set_lam(i, lbar[i] * (1.0f / (float)a.iters));
+                    }
                     if (a.viters > 0) sweeps(a.viters, false);
                 }
                 if (lead) {
