@@ -281,6 +281,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--solver-type", type=int, choices=(0, 1), default=None,
                     help="override the task cfg's sim.physx.solver_type (0 PGS, 1 TGS) for an A/B line")
+    ap.add_argument("--whole-body", action="store_true",
+                    help="walk tasks: env.asset.wholeBodyCollision (feet, shins and hands collide; model thormang_wb)")
     ap.add_argument("--terrain", action="store_true",
                     help="Gogoro only: the reference's USE_TERAIN Perlin terrain (gogoro_new.py:26)")
     args = ap.parse_args()
@@ -311,6 +313,10 @@ def main():
     cfg = load_task_cfg(args.task, num_envs=args.num_envs, sim_device=dev)
     if args.solver_type is not None:
         cfg["sim"]["physx"]["solver_type"] = args.solver_type
+    if args.whole_body:
+        if not args.task.startswith("ThormangWalk"):
+            ap.error("--whole-body applies to the ThormangWalk tasks")
+        cfg["env"]["asset"] = dict(cfg["env"].get("asset", {}), wholeBodyCollision=True)
     if args.terrain:
         from thormang_isaacgym_amd.tasks import gogoro as gogoro_task
         gogoro_task.USE_TERAIN = True
@@ -381,7 +387,9 @@ def main():
                                f"dt {sim_cfg['dt']} s x "
                                f"{sim_cfg.get('substeps', 2)} substeps ({1.0 / sim_cfg['dt']:.1f} Hz control)",
                    "num_envs_per_gpu": N, "parallelism": f"env-dp{world}",
-                   "contact_solver": solver_desc(env)},
+                   "contact_solver": solver_desc(env),
+                   "contact_shapes": f"{len(env.model.shapes)} ({', '.join(sorted(set(sh.kind for sh in env.model.shapes)))})"
+                   if hasattr(env, "model") else None},
         "dist": {"backend": ("nccl (RCCL)" if backend == "nccl" else
                              f"{backend} (rehearsal{', ranks share cuda:0' if os.environ.get('TG_BENCH_SHARE_GPU') else ''})")
                  if rccl_world else None, "world_size": rccl_world or 1,

@@ -1,3 +1,5 @@
+# Developer A/B (GPU): the 8192-env teacher-forced walk with the fp32 control, the
+# default library under TGS and PGS, then the TG_PGS_REFRESH build under TGS
 set -u
 mkdir -p gpurun_out/s4
 export PYTHONUNBUFFERED=1

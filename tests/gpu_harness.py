@@ -346,9 +346,10 @@ class OracleWalk:
         self.L = L = lib(precision)
         self.dr = {}
         from thormang_isaacgym_amd.sim import load_model
-        from thormang_isaacgym_amd.tasks.thormang_walk import walk_asset_options, walk_dof_props, walk_params
+        from thormang_isaacgym_amd.tasks.thormang_walk import walk_asset_options, walk_dof_props, walk_model_name, \
+            walk_params
         self.cfg, self.src, self.threads = cfg, draws, threads
-        self.model = m = load_model("thormang")
+        self.model = m = load_model(walk_model_name(cfg))
         env = cfg["env"]
         self.n = n = env["numEnvs"]
         self.D = D = m.num_dof
@@ -422,6 +423,40 @@ def walk_cfg(num_envs, task="ThormangWalk", dr=False, fix_base=False, spawn_heig
     if spawn_height is not None:
         cfg["env"]["spawnHeight"] = float(spawn_height)
     return cfg
+
+
+def walk_kneel_cfg(num_envs, whole_body=True, spawn_height=0.6):
+    """A kneel-and-fall scenario for whole-body contact: the PD targets fold
+    the knees to 1.6 rad with the hips straight, the humanoid spawns 0.6 m
+    up in that pose and drops onto its shins, then tips onto its hands; the
+    terminations are off so it stays down.  With the foot boxes alone
+    (whole_body=False) the pelvis sinks through the floor."""
+    cfg = walk_cfg(num_envs, spawn_height=spawn_height)
+    cfg["env"]["asset"] = dict(cfg["env"].get("asset", {}), wholeBodyCollision=bool(whole_body))
+    cfg["env"]["defaultJointAngles"] = {"l_leg_hip_p": 0.0, "l_leg_kn_p": 1.6, "l_leg_an_p": 0.0,
+                                        "r_leg_hip_p": 0.0, "r_leg_kn_p": -1.6, "r_leg_an_p": 0.0}
+    cfg["env"]["learn"]["terminationHeight"] = -10.0
+    cfg["env"]["learn"]["terminationUp"] = -2.0
+    return cfg
+
+
+def walk_kneel_forced(num_envs=32, steps=200, seed=0, amp=0.2):
+    """Teacher-forced whole-body kneel (walk_kneel_cfg) GPU vs oracle; also
+    the lowest pelvis height the GPU env reached."""
+    import torch
+    env = make_gpu_walk(walk_kneel_cfg(num_envs), NumpyDraws(seed))
+    orc = OracleWalk(walk_kneel_cfg(num_envs), NumpyDraws(seed))
+    rs = np.random.default_rng(seed + 100)
+    zmin = [float("inf")]
+
+    def act_fn(obs):
+        zmin[0] = min(zmin[0], float(env.root_tensor[:, 2].min()))
+        return rs.uniform(-amp, amp, (num_envs, orc.D)).astype(np.float32)
+    err = forced_step_errors(env, orc, act_fn, steps)
+    torch.cuda.synchronize()
+    err["pelvis_zmin"] = min(zmin[0], float(env.root_tensor[:, 2].min()))
+    err["shapes"] = len(env.model.shapes)
+    return err
 
 
 def make_gpu_walk(cfg, draws):

@@ -135,3 +135,20 @@ def test_gpu_walk_fused_step_equals_separate_calls():
             n_reset += int(f.reset_buf.sum())
         print(task, "max |fused - separate|", worst, "resets", n_reset)
         assert n_reset > 0, task   # the comparison covered resets
+
+
+def test_gpu_wholebody_kneel_matches_oracle():
+    """Whole-body contact (model thormang_wb: feet, shins and hands collide):
+    the kneel-and-fall scenario (tests.gpu_harness.walk_kneel_cfg) teacher-
+    forced for 200 steps against the oracle env -- the drop onto the shins,
+    the tip onto the hands, resting on them.  The GPU env's pelvis never
+    drops below 0.15 m (with the foot boxes alone it sinks through the floor,
+    tests/test_walk_wholebody.py)."""
+    _cuda()
+    from tests.gpu_harness import walk_kneel_forced
+    err = walk_kneel_forced(num_envs=32, steps=200, seed=0)
+    print(err)
+    assert err["shapes"] == 6
+    assert within(err) and within(err, "rew"), err
+    assert err["reset_equal"] and err["timeout_equal"], err
+    assert err["pelvis_zmin"] > 0.15, err

@@ -23,6 +23,13 @@ product path needs the URDF files.
   scooter_V13.urdf holds for the same links and the foot boxes of
   ``thormang3/thormang3.structure.leg.xacro:242-250`` (0.22 x 0.15 x 0.015 m,
   offset (0, +-0.014, -0.02) in the foot link).
+* ``thormang_wb`` -- the same humanoid with whole-body contact for the limbs
+  that reach the ground in a kneel or a fall: besides the foot boxes, the shin
+  boxes (``thormang3.structure.leg.xacro:135-138``, 0.11 x 0.16 x 0.33 m at
+  (0.01, -+0.065, -0.145) in the knee-pitch link) and the hand boxes
+  (``thormang3.structure.arm.xacro:252-254``, 0.07 x 0.1 x 0.06 m at
+  (0.07, +-0.045, 0) in the wrist-pitch link).  Selected by the walk cfg's
+  ``env.asset.wholeBodyCollision`` (tasks/thormang_walk.py).
 """
 from __future__ import annotations
 
@@ -54,18 +61,23 @@ def build_gogoro(urdf="scooter_V13.urdf", name="gogoro"):
     return m
 
 
-def build_thormang():
+def build_thormang(whole_body=False):
     v13 = ET.parse(f"{ASSETS}/urdf/scooter_V13.urdf").getroot()
     override = {}
     for l in v13.findall("link"):
         el = l.find("inertial")
         if el is not None:
             override[l.get("name")] = _parse_inertial(el)[2]
-    feet = [Shape("box", "l_leg_foot_link", [0.0, 0.014, -0.02], [[1, 0, 0], [0, 1, 0], [0, 0, 1]],
-                  [0.11, 0.075, 0.0075], 1.0),
-            Shape("box", "r_leg_foot_link", [0.0, -0.014, -0.02], [[1, 0, 0], [0, 1, 0], [0, 0, 1]],
-                  [0.11, 0.075, 0.0075], 1.0)]
-    m = load_urdf(f"{ASSETS}/urdf/thormang3.urdf", "thormang", inertia_override=override, extra_shapes=feet)
+    eye = [[1, 0, 0], [0, 1, 0], [0, 0, 1]]
+    shapes = [Shape("box", "l_leg_foot_link", [0.0, 0.014, -0.02], eye, [0.11, 0.075, 0.0075], 1.0),
+              Shape("box", "r_leg_foot_link", [0.0, -0.014, -0.02], eye, [0.11, 0.075, 0.0075], 1.0)]
+    if whole_body:   # shins (leg xacro :135-138, :410-413) and hands (arm xacro :252-254, :604-606), half sizes
+        shapes += [Shape("box", "l_leg_kn_p_link", [0.01, -0.065, -0.145], eye, [0.055, 0.08, 0.165], 1.0),
+                   Shape("box", "r_leg_kn_p_link", [0.01, 0.065, -0.145], eye, [0.055, 0.08, 0.165], 1.0),
+                   Shape("box", "l_arm_wr_p_link", [0.07, 0.045, 0.0], eye, [0.035, 0.05, 0.03], 1.0),
+                   Shape("box", "r_arm_wr_p_link", [0.07, -0.045, 0.0], eye, [0.035, 0.05, 0.03], 1.0)]
+    m = load_urdf(f"{ASSETS}/urdf/thormang3.urdf", "thormang_wb" if whole_body else "thormang",
+                  inertia_override=override, extra_shapes=shapes)
     m.build_groups([])
     return m
 
@@ -76,7 +88,8 @@ def main():
     from thormang_isaacgym_amd.model.kat_models import all_models
     # gogoro_v12: the asset of the "paper" variant (tasks/gogoro_realistic_turning_sim_paper.py:203;
     # same tree as V13, different link inertias), same locks (cfg/task/Gogoro_paper.yaml joints_pos)
-    for m in [build_gogoro(), build_gogoro("scooter_V12.urdf", "gogoro_v12"), build_thormang()] + all_models():
+    for m in [build_gogoro(), build_gogoro("scooter_V12.urdf", "gogoro_v12"), build_thormang(),
+              build_thormang(whole_body=True)] + all_models():
         with open(os.path.join(out, f"{m.name}.json"), "w") as f:
             f.write(m.to_json())
         print(m.name, "links", m.num_bodies, "dofs", m.num_dof, "groups", m.num_groups, "active", len(m.active_dofs),

@@ -139,6 +139,31 @@ def translating_locks(m: Model, a: dict) -> dict:
                 link_tl=link_tl, ag=ag, ashape=ashape, KX=(kx + 3) & ~3)
 
 
+LDS_BYTES = 160 * 1024
+
+
+def envs_per_block(G, K, NSA, NCG, MAXD, MAXC, NSTEP, LPE, fused):
+    """Envs per workgroup of the step kernel: 16 (every model so far: 4096
+    envs = one workgroup per CU), or the largest of 12, 8, 4, 2, 1 whose LDS
+    fits when 16 do not (models with many contact rows, e.g. thormang_wb).
+    Mirrors csrc/step_par.h ParLayout (the kernel static_asserts the budget)."""
+    W = G * 60
+    FLG = W + K * K + 8 * K + K + K + 2 * NSA + 12 * NCG + 6 * NCG
+    NPW = (NSTEP + 1) // 2
+    for epb in (16, 12, 8, 4, 2, 1):
+        t_desc = (G * (4 + MAXC) + NCG * MAXD + 3) & ~3
+        t_total = t_desc + 4 * NSTEP * LPE + NPW * LPE + 32 + (epb if fused & 4 else 0)
+        cb = (FLG + 1 + 3) & ~3
+        sepc = (epb * (cb + 32 * G) + t_total) * 4 <= LDS_BYTES
+        total = cb + 32 * G if sepc else FLG + 1
+        if G <= 8 and G - 1 <= LPE:   # Woodbury slots (ParLayout WOOD; counted whenever it may be on)
+            total = ((total + 3) & ~3) + 2 * 8 + 2 * 6 + 2 * 6 * NCG + 2 * max(K, 1) + 4
+        es = ((total + 3) & ~3) + (2 if G >= 16 else 0)
+        if (epb * es + t_total) * 4 <= LDS_BYTES:
+            return epb
+    raise ValueError("model does not fit the LDS with one env per workgroup")
+
+
 def emit(m: Model, cname: str) -> str:
     d = ModelDesc(m)
     a = d.arrays
@@ -166,19 +191,23 @@ def emit(m: Model, cname: str) -> str:
         p = [g for g in range(1, G) if anc[c][g]]
         cpaths.append(p + [0] * (maxd - len(p)))
     shape_cg = [cgroups.index(g) for g in sgroup]
-    # 8 schedule lanes x 16 envs per workgroup for every model: Thormang fills a
-    # CU's LDS with 16 envs; for the scooter 8 lanes also beat 2/4 (more
-    # Delassus columns in parallel) and 16 envs beat 8 (measured).
+    # 8 schedule lanes x 16 envs per workgroup for every model that fits
+    # (envs_per_block): Thormang fills a CU's LDS with 16 envs; for the scooter
+    # 8 lanes also beat 2/4 (more Delassus columns in parallel) and 16 envs
+    # beat 8 (measured).
     # Every tree with a joint group (PAIR) runs each schedule slot on a lane
     # pair (sub, sub + 8) that splits each group's update: 16 lanes per env, 4
     # wavefronts per workgroup, so 4096 envs put one wavefront on every SIMD
     # (the scooters too since round 3: Gogoro +4 %, GogoroPaper +6 % over 8
     # lanes per env, which left half the SIMDs idle; single-body models keep 8).
-    SL, EPB = LANES_PER_ENV, 16
+    SL = LANES_PER_ENV
     PAIR = 1 if G >= PAIR_MIN_GROUPS else 0
     LPE = SL * (1 + PAIR)
     sched = lane_schedule(gpar, SL)
     children = [[c for c in range(G) if gpar[c] == g] for g in range(G)]
+    maxc = max(1, max(len(c) for c in children))
+    K = sum(n + (2 if n == 1 else 3) for n in nrows_n)
+    EPB = envs_per_block(G, K, max(S, 1), max(len(cgroups), 1), maxd, maxc, len(sched), LPE, fused_tasks(m))
     # compose: link level below its group root (FK level by level), links per group
     lpar = [int(x) for x in a["link_parent"]]
     lgrp = [int(x) for x in a["link_group"]]
@@ -200,7 +229,6 @@ def emit(m: Model, cname: str) -> str:
     # in-place seat moves do not maintain them (and its task applies no
     # per-link forces), the paper's do (rb_force_env shifts them)
     lcom = 0 if tlc["NTL"] and not fused_tasks(m) & 4 else (3 * L + 3) & ~3
-    maxc = max(1, max(len(c) for c in children))
     lines = [
         f"// AUTO-GENERATED by thormang_isaacgym_amd/model/codegen.py from model '{m.name}'. Do not edit.",
         "#pragma once",

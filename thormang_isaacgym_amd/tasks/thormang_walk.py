@@ -12,7 +12,8 @@ are checked against their CPU restatement (oracle/walk_task.c).
 
 Model: thormang3.urdf (44 links, 33 revolute DOFs) with the mesh-derived link
 inertias scooter_V13.urdf carries and the xacro's foot boxes
-(model/build_models.py).  Actions [N,33] in [-1,1] -> joint targets
+(model/build_models.py); ``env.asset.wholeBodyCollision: true`` adds the
+xacro's shin and hand boxes (model ``thormang_wb``).  Actions [N,33] in [-1,1] -> joint targets
 default + actionScale * a; observation [N,112] (tg_walk.h).
 """
 from __future__ import annotations
@@ -39,7 +40,7 @@ class ThormangWalk(VecTask):
 
     def __init__(self, cfg, rl_device, sim_device, graphics_device_id, headless, virtual_screen_capture, force_render):
         self.cfg = cfg
-        self.model = load_model("thormang")
+        self.model = load_model(walk_model_name(cfg))
         D = self.model.num_dof
         cfg["env"]["numObservations"] = abi_num_obs = 13 + 3 * D
         cfg["env"]["numActions"] = D
@@ -168,6 +169,13 @@ class ThormangWalk(VecTask):
         check(lib().tg_walk_reset_idx(self.sim.handle, C.byref(self.params), C.byref(self._bufs), _p(ids32), n,
                                       _p(rd), self._counter()), "tg_walk_reset_idx")
         self._keep_reset = (ids32, rd)
+
+
+def walk_model_name(cfg) -> str:
+    """The compiled model the cfg asks for: ``thormang`` (foot boxes), or with
+    ``env.asset.wholeBodyCollision`` ``thormang_wb`` (feet, shins and hands
+    collide; model/build_models.py)."""
+    return "thormang_wb" if cfg["env"].get("asset", {}).get("wholeBodyCollision", False) else "thormang"
 
 
 def walk_asset_options(cfg) -> dict:
