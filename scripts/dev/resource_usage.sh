@@ -6,7 +6,7 @@ set -eu
 REPO=$(cd "$(dirname "$0")/../.." && pwd)
 OUT=${TMPDIR:-/tmp}/tg_ru
 mkdir -p $OUT
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -std=c++17 -O3 -ffast-math -ffp-contract=fast-honor-pragmas -munsafe-fp-atomics -fno-slp-vectorize "$@" \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -std=c++17 -O3 -ffast-math -fno-associative-math -ffp-contract=fast-honor-pragmas -munsafe-fp-atomics -fno-slp-vectorize "$@" \
   -Rpass-analysis=kernel-resource-usage -c $REPO/thormang_isaacgym_amd/csrc/articulation.hip -o $OUT/a.o 2> $OUT/ru.txt
 python3 - $OUT/ru.txt <<'PY'
 import re, subprocess, sys

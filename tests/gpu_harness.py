@@ -487,7 +487,9 @@ def walk_env_vs_oracle(num_envs=32, steps=30, seed=0, task="ThormangWalk", dr=Fa
     rs = np.random.default_rng(seed + 100)
     err = {"obs": 0.0, "rew": 0.0, "reset_equal": True, "timeout_equal": True, "root": 0.0, "steps": steps}
     if ctl is not None:
-        err["obs_f32"] = err["rew_f32"] = 0.0
+        # the control's own departure from fp64: its reset flags, the first
+        # step it leaves 1e-3; and the GPU's distance to the control itself
+        err.update(obs_f32=0.0, rew_f32=0.0, ctl_reset_equal=True, gpu_vs_f32=0.0)
     err["obs0"] = float(np.abs(env.obs_buf.cpu().numpy() - orc.a["obs_buf"]).max())
     for t in range(steps):
         if dr:
@@ -497,11 +499,20 @@ def walk_env_vs_oracle(num_envs=32, steps=30, seed=0, task="ThormangWalk", dr=Fa
         act = rs.uniform(-amp, amp, (num_envs, orc.D)).astype(np.float32)
         obs_d, rew, reset, extras = env.step(torch.from_numpy(act).to("cuda:0"))
         o_obs, o_rew, o_reset, o_to = orc.step(act)
+        g_obs = obs_d["obs"].cpu().numpy()
         if ctl is not None:
-            c_obs, c_rew = ctl.step(act)[:2]
-            err["obs_f32"] = max(err["obs_f32"], float(np.abs(c_obs - o_obs).max()))
+            c_obs, c_rew, c_reset = ctl.step(act)[:3]
+            ce = float(np.abs(c_obs - o_obs).max())
+            err["obs_f32"] = max(err["obs_f32"], ce)
             err["rew_f32"] = max(err["rew_f32"], float(np.abs(c_rew - o_rew).max()))
-        err["obs"] = max(err["obs"], float(np.abs(obs_d["obs"].cpu().numpy() - o_obs).max()))
+            err["ctl_reset_equal"] &= bool(np.array_equal(c_reset, o_reset))
+            err["gpu_vs_f32"] = max(err["gpu_vs_f32"], float(np.abs(g_obs - c_obs).max()))
+            if (ce > 1e-3 or not err["ctl_reset_equal"]) and "ctl_first_bad" not in err:
+                err["ctl_first_bad"] = t
+        e_obs = float(np.abs(g_obs - o_obs).max())
+        if e_obs > 1e-3 and "first_over_tol" not in err:
+            err["first_over_tol"] = t
+        err["obs"] = max(err["obs"], e_obs)
         err["rew"] = max(err["rew"], float(np.abs(rew.cpu().numpy() - o_rew).max()))
         err["root"] = max(err["root"], float(np.abs(env.root_tensor.cpu().numpy() - orc.a["root"]).max()))
         err["reset_equal"] &= bool(np.array_equal(reset.cpu().numpy(), o_reset))

@@ -31,8 +31,14 @@ UNITS = {
     # for the physics, but the fused task epilogues' `#pragma clang fp
     # contract(off)` blocks (the reference's fp32 operation order) are honoured
     # -- plain -ffast-math lets the backend fuse a*b+c there regardless
-    "articulation.hip": ["-O3", "-ffast-math", "-ffp-contract=fast-honor-pragmas", "-munsafe-fp-atomics",
-                         "-fno-slp-vectorize"],
+    # -fno-associative-math (round 4): reassociated sums rounded the GPU 2-6x
+    # further from the fp64 oracle than its fp32 build in the rounding-
+    # sensitive runs (GogoroPaper reward 2.0e-3 -> 7.1e-4, 8192-env walk
+    # reward 1.2e-3 -> 7.1e-4, teacher-forced) for +1.4 % step time; the
+    # other fast-math parts (reciprocals, approximate functions) measured
+    # no parity effect (DESIGN.md §2 "GPU rounding")
+    "articulation.hip": ["-O3", "-ffast-math", "-fno-associative-math", "-ffp-contract=fast-honor-pragmas",
+                         "-munsafe-fp-atomics", "-fno-slp-vectorize"],
     # task math must follow the reference's fp32 operation order
     "gogoro_task.hip": ["-O3", "-ffp-contract=off"],
     "walk_task.hip": ["-O3", "-ffp-contract=off"],

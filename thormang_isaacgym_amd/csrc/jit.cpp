@@ -105,7 +105,7 @@ std::string source_text(const char *struct_name, const char *model_source) {
 // the flags of the compiled-in articulation unit (build_ext.py UNITS); part of
 // the on-disk cache key (jit_compile), so a flag-only change never reuses a
 // code object built under other semantics
-const char *const JIT_OPTS[] = {"--offload-arch=gfx950", "-std=c++17", "-O3", "-ffast-math",
+const char *const JIT_OPTS[] = {"--offload-arch=gfx950", "-std=c++17", "-O3", "-ffast-math", "-fno-associative-math",
                                 "-ffp-contract=fast-honor-pragmas", "-munsafe-fp-atomics", "-fno-slp-vectorize",
                                 "-DTG_JIT=1"};
 constexpr int N_JIT_OPTS = (int)(sizeof JIT_OPTS / sizeof JIT_OPTS[0]);
