@@ -579,6 +579,17 @@ typedef struct {
     real mu, reff;
 } Patch;
 
+/* developer instrumentation (scripts/dev/contact_dump.py): the contact solve
+ * of env oracle_dump_env in the first substep of a call -- Delassus matrix
+ * [16 + i K + j], free row velocities [2000 + i], the stored-velocity
+ * multipliers [2500 + i] and the positions' [2600 + i] -- for a side-by-side
+ * with the kernel's dump (TG_DUMP_ENV builds).  Off (-1) by default. */
+int oracle_dump_env = -1;
+double oracle_dump_buf[4096];
+static __thread int t_env = -1, t_substep = -1;
+void oracle_dump_set(int e) { oracle_dump_env = e; }
+void oracle_dump_read(double *out, int n) { memcpy(out, oracle_dump_buf, sizeof(double) * (n > 4096 ? 4096 : n)); }
+
 /* a normal row's velocity lower bound over a step dt at separation phi: the
  * speculative approach bound -(phi - rest)/dt above the rest offset, the
  * Baumgarte push-out capped by max_depenetration_velocity below it */
@@ -867,6 +878,14 @@ static void solve_contacts(const Env *e, Work *w, real h, real *qds, V6 v0s, rea
         group_vels(m, w, dqd, dv0, dvg);
         for (int i = 0; i < K; ++i) W[i][col] = row_vel(w, &rows[i], dvg);
     }
+    const int dump = t_env >= 0 && t_env == oracle_dump_env && t_substep == 0;
+    if (dump) {
+        oracle_dump_buf[0] = K;
+        for (int i = 0; i < K; ++i) {
+            for (int j = 0; j < K; ++j) oracle_dump_buf[16 + i * K + j] = W[i][j];
+            oracle_dump_buf[2000 + i] = vfree[i];
+        }
+    }
     memset(lam, 0, sizeof(real) * K);
     for (int i = 0; i < K; ++i) target[i] = rows[i].target;
     const int tgs = e->sp->solver_type == 1 && e->sp->contact_iterations > 0;
@@ -919,6 +938,8 @@ static void solve_contacts(const Env *e, Work *w, real h, real *qds, V6 v0s, rea
         memcpy(lamv, e->sp->velocity_iterations > 0 ? lbar : lam, sizeof(real) * K);
         if (e->sp->velocity_iterations > 0)
             pgs_sweeps(K, npatch, patches, rows, target, W, vfree, lamv, e->sp->velocity_iterations);
+        if (dump)
+            for (int i = 0; i < K; ++i) { oracle_dump_buf[2500 + i] = lamv[i]; oracle_dump_buf[2600 + i] = lbar[i]; }
         apply_impulses(e, w, rows, K, lamv, qdv, v0v);
         apply_impulses(e, w, rows, K, lbar, qds, v0s);
         return;
@@ -974,6 +995,7 @@ void oracle_physics_step_env(const tg_model_desc *m, const tg_sim_params *sp, fl
     if (sp->fix_base) memset(v0, 0, sizeof v0);
 
     for (int s = 0; s < sp->substeps; ++s) {
+        t_substep = s;
         memcpy(w.Rw[0], R, sizeof(M3));
         memcpy(w.pw[0], pos, sizeof(V3));
         V6 a0;
@@ -982,6 +1004,10 @@ void oracle_physics_step_env(const tg_model_desc *m, const tg_sim_params *sp, fl
             real qdd0[MAXD];
             memcpy(qdd0, qdd, sizeof(real) * D);
             aba(&e, &w, h, q, qd, v0, qdd, a0, 1, qdd0);
+        }
+        if (t_env >= 0 && t_env == oracle_dump_env && s == 0) {   /* developer dump (contact_dump.py) */
+            for (int k = 0; k < 6; ++k) { oracle_dump_buf[2700 + k] = a0[k]; oracle_dump_buf[2710 + k] = v0[k]; }
+            for (int d = 0; d < D; ++d) oracle_dump_buf[2800 + d] = qdd[d];
         }
         real qds[MAXD];
         V6 v0s;
@@ -1070,6 +1096,7 @@ void oracle_physics_step(const tg_model_desc *m, const tg_sim_params *sp, int n,
     long stride = (long)n * D;   /* props are [F][N][D] */
 #pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1)
     for (int e = 0; e < n; ++e) {
+        t_env = e;
         oracle_physics_step_env(m, sp, root + 13 * (long)e, dof + 2 * (long)e * D, props + (long)e * D, stride,
                                 pos_tgt + (long)e * D, vel_tgt + (long)e * D, act ? act + (long)e * D : NULL,
                                 force ? force + 6L * e * m->num_groups : NULL,

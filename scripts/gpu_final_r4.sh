@@ -12,7 +12,7 @@ mkdir -p $OUT
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 if [ -n "${ONLY_PROF:-}" ]; then SKIP_TESTS=1; SKIP_BENCH=1; fi
 if [ -z "${SKIP_TESTS:-}" ]; then
-  timeout -k 10 700 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+  timeout -k 10 700 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
   rc=$?; tail -2 $OUT/gpu_tests.log; [ $rc -le 1 ] || exit $rc
 fi
 if [ -z "${SKIP_BENCH:-}" ]; then

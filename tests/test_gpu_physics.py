@@ -97,6 +97,7 @@ def test_gpu_matches_oracle_on_kat_models(name):
             props[TG_PROP_EFFORT, :, 0] = 1e9
             pt[:, 0] = rs.uniform(-0.5, 0.5, pt.shape[0])
     worst, *_ = side_by_side(m, 100, setup=setup, **kw)
+    print({"model": name, "worst_state_err": worst})
     assert worst < 2e-3, worst
 
 
@@ -114,6 +115,7 @@ def test_gpu_contact_matches_oracle_and_rests(shape, solver):
     worst, g, root, dof = side_by_side(m, 200, setup=setup, dt=0.01, substeps=2, solver_type=solver)
     z_rest = 0.1 if shape == "sphere" else 0.05
     gr = g.root_state.cpu().numpy()
+    print({"shape": shape, "solver": solver, "worst_state_err": worst, "rest_err": float(np.abs(gr[:, 2] - z_rest).max())})
     assert np.abs(gr[:, 2] - z_rest).max() < 3e-3
     assert worst < 5e-3, worst
 

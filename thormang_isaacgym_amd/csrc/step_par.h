@@ -79,6 +79,14 @@ template <int I, int N, class F> __device__ __forceinline__ void static_for(F &&
     }
 }
 
+#ifdef TG_DUMP_ENV
+// developer build (scripts/dev/contact_dump.py): the contact solve of one env
+// in the first substep of a launch -- Delassus matrix, free row velocities,
+// rows, multipliers -- for a side-by-side with the oracle's (oracle_dump_*)
+__device__ int tg_dump_env = -1;
+__device__ float tg_dump_buf[4096];
+#endif
+
 // one env's LDS state
 struct LE {
     float *b;
@@ -1871,6 +1879,19 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 }
             }
             TG_PROF(5)
+#ifdef TG_DUMP_ENV
+            if (e == tg_dump_env && owner && lead && sub_i == 0) {
+                tg_dump_buf[0] = (float)K;
+                for (int i = 0; i < K * K; ++i) tg_dump_buf[16 + i] = s(PL::W + i);
+                for (int i = 0; i < K; ++i) tg_dump_buf[2000 + i] = s(PL::VFREE + i);
+                for (int i = 0; i < K * 8; ++i) tg_dump_buf[2100 + i] = s(PL::ROW + i);
+                for (int k = 0; k < 6; ++k) tg_dump_buf[2700 + k] = k < 3 ? (&a0.w.x)[k] : (&a0.v.x)[k - 3];
+                for (int g = 1; g < M::NG; ++g) tg_dump_buf[2800 + M::gdof[g]] = s(g * GF + F_UU);   // (no rerun: qdd)
+                tg_dump_buf[2790] = s(PL::FLG);
+                for (int k = 0; k < 6; ++k) tg_dump_buf[2710 + k] = k < 3 ? (&v0.w.x)[k] : (&v0.v.x)[k - 3];
+            }
+            TG_SYNC();
+#endif
             if constexpr (!SUPER) {   // impulse accumulators (F_PA slots) cleared by all lanes
                 for (int g = sub; g < M::NG; g += LPE) stsv(s, g * GF + F_PA, sv0());
                 TG_SYNC();
@@ -2175,6 +2196,15 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             }
             }
             TG_SYNC();
+#ifdef TG_DUMP_ENV
+            if (e == tg_dump_env && owner && lead && sub_i == 0) {
+                for (int i = 0; i < K; ++i) {
+                    tg_dump_buf[2500 + i] = s(PL::LAM + i);                 // stored-velocity multipliers
+                    tg_dump_buf[2600 + i] = vit ? s(PL::W + i) : s(PL::LAM + i);   // the positions'
+                }
+            }
+            TG_SYNC();
+#endif
             SV da0 = sv0(), da0v = sv0();
             if constexpr (SUPER) {
                 TG_PROF(6)
