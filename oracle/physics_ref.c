@@ -580,14 +580,14 @@ typedef struct {
 } Patch;
 
 /* developer instrumentation (scripts/dev/contact_dump.py): the contact solve
- * of env oracle_dump_env in the first substep of a call -- Delassus matrix
+ * of env oracle_dump_env in substep oracle_dump_sub of a call -- Delassus matrix
  * [16 + i K + j], free row velocities [2000 + i], the stored-velocity
  * multipliers [2500 + i] and the positions' [2600 + i] -- for a side-by-side
  * with the kernel's dump (TG_DUMP_ENV builds).  Off (-1) by default. */
-int oracle_dump_env = -1;
+int oracle_dump_env = -1, oracle_dump_sub = 0;
 double oracle_dump_buf[4096];
 static __thread int t_env = -1, t_substep = -1;
-void oracle_dump_set(int e) { oracle_dump_env = e; }
+void oracle_dump_set(int e, int substep) { oracle_dump_env = e; oracle_dump_sub = substep; }
 void oracle_dump_read(double *out, int n) { memcpy(out, oracle_dump_buf, sizeof(double) * (n > 4096 ? 4096 : n)); }
 
 /* a normal row's velocity lower bound over a step dt at separation phi: the
@@ -878,12 +878,13 @@ static void solve_contacts(const Env *e, Work *w, real h, real *qds, V6 v0s, rea
         group_vels(m, w, dqd, dv0, dvg);
         for (int i = 0; i < K; ++i) W[i][col] = row_vel(w, &rows[i], dvg);
     }
-    const int dump = t_env >= 0 && t_env == oracle_dump_env && t_substep == 0;
+    const int dump = t_env >= 0 && t_env == oracle_dump_env && t_substep == oracle_dump_sub;
     if (dump) {
         oracle_dump_buf[0] = K;
         for (int i = 0; i < K; ++i) {
             for (int j = 0; j < K; ++j) oracle_dump_buf[16 + i * K + j] = W[i][j];
             oracle_dump_buf[2000 + i] = vfree[i];
+            oracle_dump_buf[2100 + i * 8 + 6] = rows[i].type == ROW_NORMAL ? rows[i].phi : 0;
         }
     }
     memset(lam, 0, sizeof(real) * K);
@@ -1005,7 +1006,7 @@ void oracle_physics_step_env(const tg_model_desc *m, const tg_sim_params *sp, fl
             memcpy(qdd0, qdd, sizeof(real) * D);
             aba(&e, &w, h, q, qd, v0, qdd, a0, 1, qdd0);
         }
-        if (t_env >= 0 && t_env == oracle_dump_env && s == 0) {   /* developer dump (contact_dump.py) */
+        if (t_env >= 0 && t_env == oracle_dump_env && s == oracle_dump_sub) {   /* developer dump (contact_dump.py) */
             for (int k = 0; k < 6; ++k) { oracle_dump_buf[2700 + k] = a0[k]; oracle_dump_buf[2710 + k] = v0[k]; }
             for (int d = 0; d < D; ++d) oracle_dump_buf[2800 + d] = qdd[d];
         }

@@ -84,17 +84,11 @@ def test_gpu_walk_dr_16384_envs():
     err = walk_forced(num_envs=16384, steps=100, seed=12, task="ThormangWalkDR")
     print(err)
     assert err["reset_equal"], err
-    assert within(err), err
-    # The reward's largest one-step error over these 1.6M env-steps sits at
-    # the bar (round 4: 1.08e-3; the fp32 oracle build 5.8e-4 on the same
-    # inputs, the 8192-env run 7.1e-4): the tail of the base yaw-rate error
-    # of flailing humanoids (scripts/dev/forced_outliers.py), which the
-    # velocity-tracking reward amplifies.  A miss of the 1e-3 bar is reported
-    # as an expected failure, not hidden behind a wider tolerance; twice the
-    # bar is a hard failure
-    assert err["rew"] < 2e-3, err
-    if not within(err, "rew"):
-        pytest.xfail(f"reward tail {err['rew']:.2e} > 1e-3 over 16384 x 100 env-steps (DESIGN.md §2)")
+    # (round 4: reward 1.6e-4 with the contact geometry formed about the root
+    # origin; 1.08e-3 while it was formed in world coordinates, whose fp32
+    # rounding ~158 m from the world origin perturbed the lever arms,
+    # DESIGN.md §2)
+    assert within(err) and within(err, "rew"), err
     import thormang_isaacgym_amd as tia
     n = 16384
     env = tia.make(seed=2, task="ThormangWalkDR", num_envs=n, sim_device="cuda:0", rl_device="cuda:0")

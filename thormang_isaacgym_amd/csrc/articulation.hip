@@ -225,7 +225,8 @@ int model_kc(uint64_t hash) {
 #ifdef TG_DUMP_ENV
 // developer build only: select the env whose first-substep contact solve the
 // step kernel dumps, and read the dump back (scripts/dev/contact_dump.py)
-extern "C" int tg_debug_dump_env(int e) {
+extern "C" int tg_debug_dump_env(int e, int substep) {
+    if (hipMemcpyToSymbol(HIP_SYMBOL(tg::tg_dump_sub), &substep, sizeof(int)) != hipSuccess) return -2;
     return hipMemcpyToSymbol(HIP_SYMBOL(tg::tg_dump_env), &e, sizeof(int)) == hipSuccess ? 0 : -2;
 }
 extern "C" int tg_debug_dump_read(float *out, int n) {

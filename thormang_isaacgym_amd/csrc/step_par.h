@@ -83,7 +83,7 @@ template <int I, int N, class F> __device__ __forceinline__ void static_for(F &&
 // developer build (scripts/dev/contact_dump.py): the contact solve of one env
 // in the first substep of a launch -- Delassus matrix, free row velocities,
 // rows, multipliers -- for a side-by-side with the oracle's (oracle_dump_*)
-__device__ int tg_dump_env = -1;
+__device__ int tg_dump_env = -1, tg_dump_sub = 0;
 __device__ float tg_dump_buf[4096];
 #endif
 
@@ -150,7 +150,7 @@ template <class M> struct ParLayout {
     static constexpr int VFREE = ROW + K * 8;
     static constexpr int LAM = VFREE + K;
     static constexpr int SHP = LAM + K;              // per shape: mu, reff
-    static constexpr int CGP = SHP + 2 * M::NSA;     // per contact group: world R (9), p (3)
+    static constexpr int CGP = SHP + 2 * M::NSA;     // per contact group: world R (9), p - root origin (3)
     static constexpr int CGV = CGP + 12 * M::NCG;    // per contact group: free velocity (6)
     static constexpr int FLG = CGV + 6 * M::NCG;     // a drive exceeded its effort limit
     // the Gogoro pre-physics values computed in the step kernel (models with
@@ -1640,7 +1640,12 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     }
                 }
                 stm3(s, PL::CGP + 12 * c, mul(R, ldR(s, cg)));
-                stv3(s, PL::CGP + 12 * c + 9, pos + mul(R, ldv3(s, cg * GF + F_P)));
+                // (the position relative to the root origin, world-oriented: the
+                // contact points and lever arms below never form world
+                // coordinates, whose fp32 rounding at env origins ~100 m from
+                // the world origin was 1.5e-5 m -- a lever-arm error that the
+                // speculative contact bound amplified)
+                stv3(s, PL::CGP + 12 * c + 9, mul(R, ldv3(s, cg * GF + F_P)));
                 SV v = v0s;   // root frame: the root velocity plus the path's joint terms
                 float qv[M::MAXD];
                 SV sv[M::MAXD];
@@ -1711,9 +1716,9 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 };
                 if constexpr (HF) {
                     bool th;
-                    ground_at(a, cw.x, cw.y, n, th);
+                    ground_at(a, pos.x + cw.x, pos.y + cw.y, n, th);
                     support(n);
-                    ground_at(a, pts[0].x, pts[0].y, n, th);
+                    ground_at(a, pos.x + pts[0].x, pos.y + pts[0].y, n, th);
                     if (th) gmu = a.hf_mu;
                 }
                 support(n);
@@ -1726,15 +1731,16 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 for (int k = 0; k < 4; ++k) {
                     if (k >= nr) break;
                     const int ro = PL::ROW + (rb + k) * 8;
-                    float phi = pts[k].z;
+                    // (pts: relative to the root origin, world-oriented)
+                    float phi = pos.z + pts[k].z;
                     if constexpr (HF) {   // separation along the normal of the point's own triangle
                         V3 nk;
                         bool th;
-                        const float gz = ground_at(a, pts[k].x, pts[k].y, nk, th);
-                        phi = (pts[k].z - gz) * nk.z;
+                        const float gz = ground_at(a, pos.x + pts[k].x, pos.y + pts[k].y, nk, th);
+                        phi = (pos.z + pts[k].z - gz) * nk.z;
                     }
                     // row Jacobian in the root frame: (r x d, d), r = the point about the root origin
-                    stsv(s, ro, SV{cross(mulT(R, pts[k] - pos), dl), dl});
+                    stsv(s, ro, SV{cross(mulT(R, pts[k]), dl), dl});
                     // (TGS: the separation itself, the PGS forms the sub-step targets)
                     s(ro + 6) = a.tgs ? phi : contact_target(a, phi, h);
                     s(ro + 7) = 1.f;
@@ -1763,7 +1769,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     if (nx > 1e-6f) t1 = (1.f / nx) * x;
                 }
                 const V3 t2 = cross(n, t1);
-                const V3 rl = mulT(R, cen - pos);
+                const V3 rl = mulT(R, cen);
                 const float fon = 1.f;
                 const int nf = nr == 1 ? 2 : 3;   // (shape_nfric: no torsion row for a one-point patch)
                 for (int t = 0; t < nf; ++t) {
@@ -1880,7 +1886,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             }
             TG_PROF(5)
 #ifdef TG_DUMP_ENV
-            if (e == tg_dump_env && owner && lead && sub_i == 0) {
+            if (e == tg_dump_env && owner && lead && sub_i == tg_dump_sub) {
                 tg_dump_buf[0] = (float)K;
                 for (int i = 0; i < K * K; ++i) tg_dump_buf[16 + i] = s(PL::W + i);
                 for (int i = 0; i < K; ++i) tg_dump_buf[2000 + i] = s(PL::VFREE + i);
@@ -2197,7 +2203,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             }
             TG_SYNC();
 #ifdef TG_DUMP_ENV
-            if (e == tg_dump_env && owner && lead && sub_i == 0) {
+            if (e == tg_dump_env && owner && lead && sub_i == tg_dump_sub) {
                 for (int i = 0; i < K; ++i) {
                     tg_dump_buf[2500 + i] = s(PL::LAM + i);                 // stored-velocity multipliers
                     tg_dump_buf[2600 + i] = vit ? s(PL::W + i) : s(PL::LAM + i);   // the positions'
