@@ -205,7 +205,8 @@ typedef struct {
     /* per substep */
     Xform X[MAXG];
     M3 Rw[MAXG];
-    V3 pw[MAXG];
+    V3 pw[MAXG];            /* group origins relative to the root origin (world-oriented) */
+    V3 org;                 /* the root origin in the world */
     V6 v[MAXG], c[MAXG], pA[MAXG], U[MAXG], S[MAXG];
     M6 IA[MAXG];
     real D[MAXG], u[MAXG];
@@ -727,9 +728,9 @@ static int collect_rows(const Env *e, Work *w, real h, Row *rows, Patch *patches
         real gmu = e->sp->ground_friction;
         if (g_hf.h) {
             int th;
-            ground_at(c[0], c[1], n, &th);
+            ground_at(w->org[0] + c[0], w->org[1] + c[1], n, &th);
             support_points(m, s, R, c, n, pts);
-            ground_at(pts[0][0], pts[0][1], n, &th);
+            ground_at(w->org[0] + pts[0][0], w->org[1] + pts[0][1], n, &th);
             if (th) gmu = g_hf.mu;
         }
         int np = support_points(m, s, R, c, n, pts);
@@ -746,12 +747,12 @@ static int collect_rows(const Env *e, Work *w, real h, Row *rows, Patch *patches
         real wk[8], wsum = 0;
         const real margin = e->sp->contact_margin;
         for (int k = 0; k < np; ++k) {
-            real phi = pts[k][2];
+            real phi = w->org[2] + pts[k][2];
             if (g_hf.h) {   /* separation along the normal of the point's own triangle */
                 V3 nk;
                 int th;
-                real gz = ground_at(pts[k][0], pts[k][1], nk, &th);
-                phi = (pts[k][2] - gz) * nk[2];
+                real gz = ground_at(w->org[0] + pts[k][0], w->org[1] + pts[k][1], nk, &th);
+                phi = (w->org[2] + pts[k][2] - gz) * nk[2];
             }
             Row *r = &rows[nr++];
             r->g = g; r->type = ROW_NORMAL; r->angular = 0; r->patch = np_;
@@ -998,7 +999,10 @@ void oracle_physics_step_env(const tg_model_desc *m, const tg_sim_params *sp, fl
     for (int s = 0; s < sp->substeps; ++s) {
         t_substep = s;
         memcpy(w.Rw[0], R, sizeof(M3));
-        memcpy(w.pw[0], pos, sizeof(V3));
+        /* (positions about the root origin: the contact geometry never forms
+         * world coordinates, as the kernel's, step_par.h PL::CGP) */
+        memset(w.pw[0], 0, sizeof(V3));
+        memcpy(w.org, pos, sizeof(V3));
         V6 a0;
         aba(&e, &w, h, q, qd, v0, qdd, a0, 1, NULL);
         if (drives_saturated(&e, &w, h, q, qd, qdd)) {

@@ -37,8 +37,17 @@ UNITS = {
     # reward 1.2e-3 -> 7.1e-4, teacher-forced) for +1.4 % step time; the
     # other fast-math parts (reciprocals, approximate functions) measured
     # no parity effect (DESIGN.md §2 "GPU rounding")
+    # The step kernels are split over two units by tree size (launch.h
+    # in_unit) so that each gets the machine scheduler that measured fastest
+    # for it (round 4, scripts/dev/ab_libs.sh): the scooters
+    # and the known-answer models the max-ILP strategy, the humanoid trees
+    # the iterative ILP one.  Scheduling reorders instructions only; the
+    # arithmetic, and with it every result, is the same
     "articulation.hip": ["-O3", "-ffast-math", "-fno-associative-math", "-ffp-contract=fast-honor-pragmas",
-                         "-munsafe-fp-atomics", "-fno-slp-vectorize"],
+                         "-munsafe-fp-atomics", "-fno-slp-vectorize", "-mllvm", "--amdgpu-sched-strategy=max-ilp"],
+    "articulation_tree.hip": ["-O3", "-ffast-math", "-fno-associative-math", "-ffp-contract=fast-honor-pragmas",
+                              "-munsafe-fp-atomics", "-fno-slp-vectorize", "-mllvm",
+                              "--amdgpu-sched-strategy=iterative-ilp"],
     # task math must follow the reference's fp32 operation order
     "gogoro_task.hip": ["-O3", "-ffp-contract=off"],
     "walk_task.hip": ["-O3", "-ffp-contract=off"],

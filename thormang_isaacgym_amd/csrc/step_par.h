@@ -83,8 +83,8 @@ template <int I, int N, class F> __device__ __forceinline__ void static_for(F &&
 // developer build (scripts/dev/contact_dump.py): the contact solve of one env
 // in the first substep of a launch -- Delassus matrix, free row velocities,
 // rows, multipliers -- for a side-by-side with the oracle's (oracle_dump_*)
-__device__ int tg_dump_env = -1, tg_dump_sub = 0;
-__device__ float tg_dump_buf[4096];
+static __device__ int tg_dump_env = -1, tg_dump_sub = 0;
+static __device__ float tg_dump_buf[4096];
 #endif
 
 // one env's LDS state
