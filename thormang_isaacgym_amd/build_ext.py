@@ -21,6 +21,25 @@ EXTRA = os.environ.get("TG_EXTRA_FLAGS", "").split()
 if EXTRA:
     BUILD = BUILD + "_" + "_".join(f.strip("-").replace("=", "_") for f in EXTRA)
 ARCH = os.environ.get("TG_OFFLOAD_ARCH", "gfx950")
+
+
+def _sched(env, dflt):
+    """-mllvm scheduler flags of a unit (developer override: TG_SCHED_MAIN /
+    TG_SCHED_TREE = a strategy name, 'default', or raw -mllvm options after
+    'raw:' separated by commas)"""
+    v = os.environ.get(env, dflt)
+    if v == "default":
+        return []
+    if v.startswith("raw:"):
+        return [x for o in v[4:].split(",") if o for x in ("-mllvm", o)]
+    return ["-mllvm", f"--amdgpu-sched-strategy={v}"]
+
+
+SCHED_MAIN = _sched("TG_SCHED_MAIN", "max-ilp")
+SCHED_TREE = _sched("TG_SCHED_TREE", "iterative-ilp")
+for _k in ("TG_SCHED_MAIN", "TG_SCHED_TREE"):   # developer variants get their own objects
+    if _k in os.environ:
+        BUILD = BUILD + "_" + _k[-4:].lower() + "_" + "".join(c if c.isalnum() else "_" for c in os.environ[_k])
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 UNITS = {
@@ -44,10 +63,9 @@ UNITS = {
     # the iterative ILP one.  Scheduling reorders instructions only; the
     # arithmetic, and with it every result, is the same
     "articulation.hip": ["-O3", "-ffast-math", "-fno-associative-math", "-ffp-contract=fast-honor-pragmas",
-                         "-munsafe-fp-atomics", "-fno-slp-vectorize", "-mllvm", "--amdgpu-sched-strategy=max-ilp"],
+                         "-munsafe-fp-atomics", "-fno-slp-vectorize", *SCHED_MAIN],
     "articulation_tree.hip": ["-O3", "-ffast-math", "-fno-associative-math", "-ffp-contract=fast-honor-pragmas",
-                              "-munsafe-fp-atomics", "-fno-slp-vectorize", "-mllvm",
-                              "--amdgpu-sched-strategy=iterative-ilp"],
+                              "-munsafe-fp-atomics", "-fno-slp-vectorize", *SCHED_TREE],
     # task math must follow the reference's fp32 operation order
     "gogoro_task.hip": ["-O3", "-ffp-contract=off"],
     "walk_task.hip": ["-O3", "-ffp-contract=off"],
