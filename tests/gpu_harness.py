@@ -515,7 +515,21 @@ def walk_env_vs_oracle(num_envs=32, steps=30, seed=0, task="ThormangWalk", dr=Fa
         err["obs"] = max(err["obs"], e_obs)
         err["rew"] = max(err["rew"], float(np.abs(rew.cpu().numpy() - o_rew).max()))
         err["root"] = max(err["root"], float(np.abs(env.root_tensor.cpu().numpy() - orc.a["root"]).max()))
-        err["reset_equal"] &= bool(np.array_equal(reset.cpu().numpy(), o_reset))
+        r_g = reset.cpu().numpy()
+        if err["reset_equal"] and not np.array_equal(r_g, o_reset):
+            # the first reset-mask disagreement: the envs' termination margins
+            # in the oracle (pelvis height and uprightness against the cfg's
+            # thresholds, oracle/walk_task.c observe) -- a threshold tie when
+            # each disagreeing env sits within 1e-3 of a threshold, i.e. the
+            # comparison's own tolerance
+            bad = np.nonzero(r_g != o_reset)[0]
+            margin = np.minimum(np.abs(o_obs[bad, 0] - orc.p.termination_height),
+                                np.abs(-o_obs[bad, 9] - orc.p.termination_up))
+            err.update(reset_diff_step=t, reset_diff_envs=bad.tolist(),
+                       reset_diff_margin=[float(x) for x in margin],
+                       reset_diff_obs_err=float(np.abs(g_obs[bad] - o_obs[bad]).max()),
+                       reset_diff_tie=bool(np.all(margin < 1e-3)))
+        err["reset_equal"] &= bool(np.array_equal(r_g, o_reset))
         err["timeout_equal"] &= bool(np.array_equal(extras["time_outs"].cpu().numpy().astype(np.uint8), o_to))
         if not within(err) and "first_bad_step" not in err:
             err["first_bad_step"] = t
