@@ -13,7 +13,7 @@ import sys
 import numpy as np
 
 sys.path.insert(0, ".")
-from tests.gpu_harness import NumpyDraws, OracleWalk, walk_cfg  # noqa: E402
+from tests.gpu_harness import NumpyDraws, OracleWalk, perturbed_walk_oracle, walk_cfg  # noqa: E402
 
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 6
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 32
@@ -23,11 +23,7 @@ eps = float(sys.argv[5]) if len(sys.argv) > 5 else 1e-7
 ref = OracleWalk(walk_cfg(n), NumpyDraws(seed))
 runs = {}
 for k in range(K):
-    p = OracleWalk(walk_cfg(n), NumpyDraws(seed))
-    rs = np.random.default_rng(1000 + k)
-    p.a["root"][:, 2] += (eps * rs.choice([-1.0, 1.0], n)).astype(np.float32)
-    p.a["dof_state"][:, 0] += (eps * rs.choice([-1.0, 1.0], p.a["dof_state"].shape[0])).astype(np.float32)
-    runs[f"fp64+{eps:g}#{k}"] = p
+    runs[f"fp64+{eps:g}#{k}"] = perturbed_walk_oracle(walk_cfg(n), seed, k, eps)
 runs["fp32"] = OracleWalk(walk_cfg(n), NumpyDraws(seed), precision="f32")
 res = {k: {"horizon": None, "reset_diff": None} for k in runs}
 act = np.zeros((n, ref.D), np.float32)

@@ -126,6 +126,11 @@ def balance_policy(obs):
     return np.clip(4.0 * roll + 0.8 * droll, -1.0, 1.0)[:, None].astype(np.float32)
 
 
+def brief(err):
+    """The error dict without its per-step traces (keys starting with _)."""
+    return {k: v for k, v in err.items() if not k.startswith("_")}
+
+
 def within(err, key="obs", tol=1e-3, factor=2.0):
     """The parity bar, north_star's: the GPU-vs-fp64-oracle error under
     ``tol`` = 1e-3.  The one exception is a run that carries the rounding
@@ -472,20 +477,38 @@ def n_resets(orc):
     return getattr(orc, "reset_count", 0)
 
 
+def perturbed_walk_oracle(cfg, seed, k, eps=1e-7):
+    """The fp64 oracle env with its initial pelvis height and every joint
+    position moved by +-eps (random signs, stream k): a rounding-level
+    perturbation of the reference itself (scripts/dev/standing_chaos_cpu.py)."""
+    p = OracleWalk(cfg, NumpyDraws(seed))
+    rs = np.random.default_rng(1000 + k)
+    p.a["root"][:, 2] += (eps * rs.choice([-1.0, 1.0], p.n)).astype(np.float32)
+    p.a["dof_state"][:, 0] += (eps * rs.choice([-1.0, 1.0], p.a["dof_state"].shape[0])).astype(np.float32)
+    return p
+
+
 def walk_env_vs_oracle(num_envs=32, steps=30, seed=0, task="ThormangWalk", dr=False, fix_base=False,
-                       spawn_height=None, amp=0.3, control=False, solver_type=None):
+                       spawn_height=None, amp=0.3, control=False, solver_type=None, perturbed=0):
     """Free-running GPU walk env vs the oracle env on the same draws and
     actions U(-amp, amp) (amp 0: the PD-held default pose); with ``control``
     the fp32 oracle build runs the same episode beside the fp64 one
-    (``within``)."""
+    (``within``); with ``perturbed`` = K also K fp64 runs from initial states
+    perturbed by 1e-7 (``perturbed_walk_oracle``): ``pert_first_bad`` is the
+    first step any of them leaves 1e-3 of the unperturbed reference -- the
+    reference's own predictability horizon at that precision.  Per-step
+    maxima of the GPU's errors are kept in ``_obs_t`` / ``_rew_t``
+    (``brief`` drops them for printing)."""
     import torch
     mk = lambda: walk_cfg(num_envs, task, dr=dr, fix_base=fix_base, spawn_height=spawn_height,
                           solver_type=solver_type)
     env = make_gpu_walk(mk(), NumpyDraws(seed))
     orc = OracleWalk(mk(), NumpyDraws(seed))
     ctl = OracleWalk(mk(), NumpyDraws(seed), precision="f32") if control else None
+    perts = [perturbed_walk_oracle(mk(), seed, k) for k in range(perturbed)]
     rs = np.random.default_rng(seed + 100)
-    err = {"obs": 0.0, "rew": 0.0, "reset_equal": True, "timeout_equal": True, "root": 0.0, "steps": steps}
+    err = {"obs": 0.0, "rew": 0.0, "reset_equal": True, "timeout_equal": True, "root": 0.0, "steps": steps,
+           "_obs_t": [], "_rew_t": []}
     if ctl is not None:
         # the control's own departure from fp64: its reset flags, the first
         # step it leaves 1e-3; and the GPU's distance to the control itself
@@ -509,11 +532,19 @@ def walk_env_vs_oracle(num_envs=32, steps=30, seed=0, task="ThormangWalk", dr=Fa
             err["gpu_vs_f32"] = max(err["gpu_vs_f32"], float(np.abs(g_obs - c_obs).max()))
             if (ce > 1e-3 or not err["ctl_reset_equal"]) and "ctl_first_bad" not in err:
                 err["ctl_first_bad"] = t
+        for pk in perts:
+            p_obs, _, p_reset = pk.step(act)[:3]
+            if "pert_first_bad" not in err and (float(np.abs(p_obs - o_obs).max()) > 1e-3 or
+                                                not np.array_equal(p_reset, o_reset)):
+                err["pert_first_bad"] = t
         e_obs = float(np.abs(g_obs - o_obs).max())
         if e_obs > 1e-3 and "first_over_tol" not in err:
             err["first_over_tol"] = t
+        e_rew = float(np.abs(rew.cpu().numpy() - o_rew).max())
+        err["_obs_t"].append(e_obs)
+        err["_rew_t"].append(e_rew)
         err["obs"] = max(err["obs"], e_obs)
-        err["rew"] = max(err["rew"], float(np.abs(rew.cpu().numpy() - o_rew).max()))
+        err["rew"] = max(err["rew"], e_rew)
         err["root"] = max(err["root"], float(np.abs(env.root_tensor.cpu().numpy() - orc.a["root"]).max()))
         r_g = reset.cpu().numpy()
         if err["reset_equal"] and not np.array_equal(r_g, o_reset):

@@ -20,7 +20,7 @@ scripts/parity_drift.py measures, for the chaotic configurations, how far a
 from it (profiles/r2/drift_*.txt)."""
 import pytest
 import torch
-from tests.gpu_harness import within
+from tests.gpu_harness import brief, within
 
 pytestmark = pytest.mark.gpu
 
@@ -34,7 +34,7 @@ def test_gpu_gogoro_fixed_base_free_running_1000_steps():
     _cuda()
     from tests.gpu_harness import balance_policy, gogoro_env_vs_oracle
     err = gogoro_env_vs_oracle(num_envs=64, steps=1000, seed=31, policy=balance_policy, fix_base=True)
-    print(err)
+    print(brief(err))
     assert within(err) and within(err, "rew"), err
     assert err["reset_equal"] and err["timeout_equal"], err
     assert err["resets"] >= 64          # every env times out at step 999 and re-spawns
@@ -44,35 +44,50 @@ def test_gpu_walk_fixed_base_free_running_1000_steps():
     _cuda()
     from tests.gpu_harness import walk_env_vs_oracle
     err = walk_env_vs_oracle(num_envs=32, steps=1000, seed=32, fix_base=True, spawn_height=1.3, amp=0.3)
-    print(err)
+    print(brief(err))
     assert within(err) and within(err, "rew"), err
     assert err["reset_equal"] and err["timeout_equal"], err
 
 
 def test_gpu_walk_standing_free_running_1000_steps():
+    """ThormangWalk standing (zero actions: the PD-held default pose), 32 envs,
+    1000 free-running steps; some spawn poses topple (20 falls with seed 21).
+
+    A toppling humanoid amplifies rounding: the fp64 reference itself, started
+    from states perturbed by 1e-7, leaves the 1e-3 band between steps 580 and
+    853, and by 1e-6 between 131 and 165 with a reset a step apart in 3 of
+    10 runs (profiles/r4/standing_chaos_cpu.txt).  So the run carries its own
+    yardstick: the fp32 oracle build and three 1e-7-perturbed fp64 runs beside
+    the reference; the earliest step any of them leaves 1e-3 (or changes a
+    reset flag) is the trajectory's predictability horizon at fp32-level
+    precision.  Up to 10 steps before it the GPU is held to north_star's bar
+    outright -- obs and reward within 1e-3 every step, identical reset flags
+    -- and it must not leave the band before it.  After it the comparison
+    reports but does not assert (the reference no longer determines the
+    trajectory to 1e-3); time-out flags must agree throughout."""
     _cuda()
+    import numpy as np
     from tests.gpu_harness import walk_env_vs_oracle
-    err = walk_env_vs_oracle(num_envs=32, steps=1000, seed=21, amp=0.0, control=True)
-    print(err)
-    # most stand the whole 1000 steps; some spawn poses (random yaw, joint
-    # noise) topple (fewer than one reset per env).  A toppling humanoid
-    # amplifies rounding, so the fp32 control rides beside: under TGS one env
-    # (seed 21) topples a step apart in fp32 and fp64 (round 4: step ~580, the
-    # control's reset flags differ) -- the GPU then follows the fp32 build
-    # (gpu_vs_f32), and the reset flags must agree with fp64 unless the
-    # control's do not either
-    assert err["resets"] < 32, err
-    assert within(err) and within(err, "rew"), err
-    assert err["timeout_equal"], err
-    assert err["reset_equal"] or not err["ctl_reset_equal"], err
-    assert err.get("first_over_tol", 1000) >= err.get("ctl_first_bad", 1000) - 10, err
+    err = walk_env_vs_oracle(num_envs=32, steps=1000, seed=21, amp=0.0, control=True, perturbed=3)
+    hz = min(err.get("ctl_first_bad", 1000), err.get("pert_first_bad", 1000))
+    pre = max(hz - 10, 0)
+    err["horizon"] = hz
+    err["obs_pre_horizon"] = float(np.max(err["_obs_t"][:pre])) if pre else 0.0
+    err["rew_pre_horizon"] = float(np.max(err["_rew_t"][:pre])) if pre else 0.0
+    print(brief(err))
+    assert err["resets"] < 32, brief(err)
+    assert hz >= 100, brief(err)                      # the yardstick itself is sane
+    assert err["obs_pre_horizon"] < 1e-3 and err["rew_pre_horizon"] < 1e-3, brief(err)
+    assert err.get("first_over_tol", 1000) >= pre, brief(err)
+    assert err["reset_equal"] or err["reset_diff_step"] >= pre, brief(err)
+    assert err["timeout_equal"], brief(err)
 
 
 def test_gpu_gogoro_free_base_free_running_1000_steps():
     _cuda()
     from tests.gpu_harness import balance_policy, gogoro_env_vs_oracle
     err = gogoro_env_vs_oracle(num_envs=32, steps=1000, seed=21, policy=balance_policy)
-    print(err)
+    print(brief(err))
     assert err["resets"] > 32           # falls and re-spawns happen along the way
     assert within(err) and within(err, "rew"), err
     assert err["reset_equal"] and err["timeout_equal"], err
@@ -85,13 +100,13 @@ def test_gpu_gogoro_domain_randomisation_matches_oracle():
     _cuda()
     from tests.gpu_harness import balance_policy, gogoro_env_vs_oracle, gogoro_forced
     err = gogoro_env_vs_oracle(num_envs=64, steps=150, seed=41, policy=balance_policy, dr=True)
-    print(err)
+    print(brief(err))
     lo, hi = err["mass_scale_range"]
     assert 0.95 <= lo < 0.96 and 1.04 < hi <= 1.05, err      # masses really randomised
     assert within(err) and within(err, "rew"), err
     assert err["reset_equal"] and err["timeout_equal"], err
     err = gogoro_forced(num_envs=64, steps=1000, seed=42, dr=True)
-    print(err)
+    print(brief(err))
     assert err["gravity"] != [0.0, 0.0, -9.81], err            # resampled at frame 600
     assert within(err) and within(err, "rew"), err
     assert err["reset_equal"] and err["timeout_equal"], err
@@ -115,7 +130,7 @@ def test_gpu_gogoro_free_base_random_actions_free_running():
     rs = np.random.default_rng(77)
     err = gogoro_env_vs_oracle(num_envs=64, steps=100, seed=22,
                                policy=lambda o: rs.uniform(-1, 1, (o.shape[0], 1)).astype(np.float32))
-    print(err)
+    print(brief(err))
     assert err["resets"] >= 64
     assert within(err) and within(err, "rew"), err
     assert err["reset_equal"] and err["timeout_equal"], err
@@ -135,7 +150,7 @@ def test_gpu_walk_random_actions_free_running_600_steps():
     _cuda()
     from tests.gpu_harness import walk_env_vs_oracle
     err = walk_env_vs_oracle(num_envs=64, steps=600, seed=21, amp=0.3, control=True)
-    print(err)
+    print(brief(err))
     assert err["resets"] > 0, err            # envs fall and re-spawn along the way
     assert within(err) and within(err, "rew"), err
     assert err["reset_equal"] and err["timeout_equal"], err

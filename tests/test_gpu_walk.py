@@ -3,7 +3,7 @@ step) against its CPU oracle env on identical draws, and a 4096-env run."""
 import numpy as np
 import pytest
 import torch
-from tests.gpu_harness import within
+from tests.gpu_harness import brief, within
 
 pytestmark = pytest.mark.gpu
 
@@ -17,7 +17,7 @@ def test_gpu_walk_matches_oracle_env():
     _cuda()
     from tests.gpu_harness import walk_env_vs_oracle
     err = walk_env_vs_oracle(num_envs=32, steps=200, seed=5)
-    print(err)
+    print(brief(err))
     assert err["obs0"] < 1e-5, err
     assert within(err) and within(err, "rew"), err
     assert err["reset_equal"] and err["timeout_equal"], err
@@ -27,7 +27,7 @@ def test_gpu_walk_dr_pushes_match_oracle_env():
     _cuda()
     from tests.gpu_harness import walk_env_vs_oracle
     err = walk_env_vs_oracle(num_envs=32, steps=200, seed=7, task="ThormangWalkDR")
-    print(err)
+    print(brief(err))
     assert within(err) and within(err, "rew"), err
     assert err["reset_equal"], err
 
@@ -56,7 +56,7 @@ def test_gpu_walk_step_matches_oracle_along_1000_steps():
     _cuda()
     from tests.gpu_harness import walk_forced
     err = walk_forced(num_envs=32, steps=1000, seed=8)
-    print(err)
+    print(brief(err))
     assert within(err) and within(err, "rew"), err
     assert err["reset_equal"] and err["timeout_equal"], err
 
@@ -68,7 +68,7 @@ def test_gpu_walk_8192_envs_step_matches_oracle():
     _cuda()
     from tests.gpu_harness import walk_forced
     err = walk_forced(num_envs=8192, steps=100, seed=11)
-    print(err)
+    print(brief(err))
     assert within(err) and within(err, "rew"), err
     assert err["reset_equal"] and err["timeout_equal"], err
 
@@ -82,7 +82,7 @@ def test_gpu_walk_dr_16384_envs():
     _cuda()
     from tests.gpu_harness import walk_forced
     err = walk_forced(num_envs=16384, steps=100, seed=12, task="ThormangWalkDR")
-    print(err)
+    print(brief(err))
     assert err["reset_equal"], err
     # (round 4: reward 1.6e-4 with the contact geometry formed about the root
     # origin; 1.08e-3 while it was formed in world coordinates, whose fp32
@@ -153,7 +153,7 @@ def test_gpu_wholebody_kneel_matches_oracle():
     _cuda()
     from tests.gpu_harness import walk_kneel_forced
     err = walk_kneel_forced(num_envs=32, steps=200, seed=0)
-    print(err)
+    print(brief(err))
     assert err["shapes"] == 6
     assert within(err) and within(err, "rew"), err
     assert err["reset_equal"] and err["timeout_equal"], err
