@@ -1,13 +1,18 @@
 #!/bin/bash
 # Register / scratch / LDS use of every step_par_kernel instantiation
 # (hipcc -Rpass-analysis=kernel-resource-usage on articulation.hip).
-# usage: scripts/dev/resource_usage.sh [extra hipcc flags]
+# usage: EXTRA="extra hipcc flags" scripts/dev/resource_usage.sh
 set -eu
 REPO=$(cd "$(dirname "$0")/../.." && pwd)
 OUT=${TMPDIR:-/tmp}/tg_ru
 mkdir -p $OUT
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -std=c++17 -O3 -ffast-math -fno-associative-math -ffp-contract=fast-honor-pragmas -munsafe-fp-atomics -fno-slp-vectorize "$@" \
-  -Rpass-analysis=kernel-resource-usage -c $REPO/thormang_isaacgym_amd/csrc/articulation.hip -o $OUT/a.o 2> $OUT/ru.txt
+# the two units, each with its machine scheduler (build_ext.py)
+: > $OUT/ru.txt
+for u in "articulation.hip max-ilp" "articulation_tree.hip iterative-ilp"; do
+  set -- $u
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -std=c++17 -O3 -ffast-math -fno-associative-math -ffp-contract=fast-honor-pragmas -munsafe-fp-atomics -fno-slp-vectorize -mllvm --amdgpu-sched-strategy=$2 ${EXTRA:-} \
+    -Rpass-analysis=kernel-resource-usage -c $REPO/thormang_isaacgym_amd/csrc/$1 -o $OUT/a.o 2>> $OUT/ru.txt
+done
 python3 - $OUT/ru.txt <<'PY'
 import re, subprocess, sys
 txt = open(sys.argv[1]).read()

@@ -1076,6 +1076,22 @@ template <class M> __device__ __forceinline__ int row_cg(int i) {
     }
     return r;
 }
+// the most contact points (normal rows) of any shape of the model
+template <class M> __device__ __forceinline__ constexpr int max_shape_rows() {
+    int m = 0;
+    for (int s = 0; s < M::NS; ++s) m = M::shape_nrows[s] > m ? M::shape_nrows[s] : m;
+    return m;
+}
+// the shape of row i (lane-dependent i): compares and selects, no table load
+template <class M> __device__ __forceinline__ int row_shape_sel(int i) {
+    int r = 0, base = 0;
+#pragma unroll
+    for (int sh = 0; sh < M::NS; ++sh) {
+        r = i >= base ? sh : r;
+        base += M::shape_nrows[sh] + shape_nfric<M>(sh);
+    }
+    return r;
+}
 template <class M> __device__ __forceinline__ constexpr int row_base(int s) {
     int base = 0;
     for (int k = 0; k < s; ++k) base += M::shape_nrows[k] + shape_nfric<M>(k);

@@ -921,10 +921,21 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
 #ifndef TG_SHAPE_ONCE
 #define TG_SHAPE_ONCE 1   // developer switch: 0 = loads inside the contact setup (A/B)
 #endif
-    constexpr bool SHP1 = TG_SHAPE_ONCE && M::NS > 0 && M::NS <= LPE;
+    // one lane per contact ROW when every row has a lane (ROWPAR, round 4;
+    // the contact setup below), else one lane per shape; either way the
+    // lane's shape is loaded here
+#ifndef TG_ROW_PAR
+#define TG_ROW_PAR 1   // developer switch: 0 = one lane per shape builds its rows (A/B)
+#endif
+    // (multi-point patches only -- the box faces' 7 rows per shape: on the
+    // scooters' one-point tori, 3 rows per shape, every lane redoing the
+    // shape geometry measured +0.35 % (Gogoro), where Thormang gains 1.0 %,
+    // profiles/r4/rowpar_ab.txt)
+    constexpr bool ROWPAR = TG_ROW_PAR && M::NS > 0 && PL::K <= LPE && max_shape_rows<M>() > 1;
+    constexpr bool SHP1 = TG_SHAPE_ONCE && M::NS > 0 && (ROWPAR || M::NS <= LPE);
     float shp1[SHP1 ? 12 : 1], smu1 = 0.f;
     if constexpr (SHP1) {
-        const int sh = sub < M::NS ? sub : 0;
+        const int sh = ROWPAR ? row_shape_sel<M>(sub < PL::K ? sub : 0) : (sub < M::NS ? sub : 0);
 #pragma unroll
         for (int k = 0; k < 12; ++k) shp1[k] = CP(CL::shape(sh) + k);
         smu1 = a.shape_mu[(size_t)e * M::NS + sh];
@@ -1659,6 +1670,136 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 stsv(s, PL::CGV + 6 * c, v);
             }
             TG_SYNC();
+            if constexpr (ROWPAR) {
+            // contact rows, one lane per ROW (K <= LPE): the lane forms its
+            // row's shape geometry itself -- support points, separations,
+            // patch centroid: the operations of the one-lane-per-shape form
+            // below, in the same order, so every row is bit-identical -- and
+            // stores only its own row.  The rows' Jacobians and stores then
+            // spread over the env's lanes instead of running serially on one
+            // lane per shape (a wave instruction costs its full width however
+            // few lanes are active)
+            if (sub < K) {
+                const int i = sub;
+                const int sh = row_shape_sel<M>(i);
+                int cgi = M::shape_cg[0];   // (selected from the constant table, no load)
+#pragma unroll
+                for (int k = 1; k < M::NS; ++k) cgi = sh == k ? M::shape_cg[k] : cgi;
+                const int kr = i - row_base<M>(sh);   // the row within its shape
+                const M3 Rwg = ldm3(s, PL::CGP + 12 * cgi);
+                const V3 pwg = ldv3(s, PL::CGP + 12 * cgi + 9);
+                M3 Rsl;
+                V3 cl;
+                if constexpr (SHP1) {   // (the row's shape: loaded at kernel start)
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) Rsl.a[k] = shp1[k];
+                    cl = v3(shp1[9], shp1[10], shp1[11]);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) Rsl.a[k] = CP(CL::shape(sh) + k);
+                    cl = v3(CP(CL::shape(sh) + 9), CP(CL::shape(sh) + 10), CP(CL::shape(sh) + 11));
+                }
+                const M3 Rs = mul(Rwg, Rsl);
+                const V3 cw = pwg + mul(Rwg, cl);
+                V3 pts[4];
+                const int nr = M::shape_nrows[sh];
+                const int kind = M::shape_kind[sh];
+                V3 n = v3(0, 0, 1);
+                float gmu = a.ground_mu;
+                auto support = [&](V3 nn) __attribute__((always_inline)) {
+                    if (kind == TG_SHAPE_TORUS) {
+                        const V3 ax = v3(Rs.a[2], Rs.a[5], Rs.a[8]);
+                        V3 dd = nn - dot(ax, nn) * ax;
+                        float nd = sqrtf(dot(dd, dd));
+                        if (nd < 1e-6f) { dd = v3(1, 0, 0); nd = 1.f; }
+                        pts[0] = cw - (M::shape_params[sh][0] / nd) * dd - M::shape_params[sh][1] * nn;
+                    } else if (kind == TG_SHAPE_SPHERE) {
+                        pts[0] = cw - M::shape_params[sh][0] * nn;
+                    } else {
+                        const float hx = M::shape_params[sh][0], hy = M::shape_params[sh][1], hz = M::shape_params[sh][2];
+                        const V3 ex = v3(Rs.a[0], Rs.a[3], Rs.a[6]), ey = v3(Rs.a[1], Rs.a[4], Rs.a[7]),
+                                 ez = v3(Rs.a[2], Rs.a[5], Rs.a[8]);
+                        const float zx = dot(ex, nn), zy = dot(ey, nn), zz = dot(ez, nn);
+                        const float ax_ = fabsf(zx), ay_ = fabsf(zy), az_ = fabsf(zz);
+                        V3 fn, u1, u2;
+                        if (az_ >= ax_ && az_ >= ay_) { fn = (zz > 0 ? -hz : hz) * ez; u1 = hx * ex; u2 = hy * ey; }
+                        else if (ay_ >= ax_) { fn = (zy > 0 ? -hy : hy) * ey; u1 = hx * ex; u2 = hz * ez; }
+                        else { fn = (zx > 0 ? -hx : hx) * ex; u1 = hy * ey; u2 = hz * ez; }
+                        pts[0] = cw + fn - u1 - u2;
+                        pts[1] = cw + fn + u1 - u2;
+                        pts[2] = cw + fn - u1 + u2;
+                        pts[3] = cw + fn + u1 + u2;
+                    }
+                };
+                if constexpr (HF) {
+                    bool th;
+                    ground_at(a, pos.x + cw.x, pos.y + cw.y, n, th);
+                    support(n);
+                    ground_at(a, pos.x + pts[0].x, pos.y + pts[0].y, n, th);
+                    if (th) gmu = a.hf_mu;
+                }
+                support(n);
+                const V3 dl = mulT(R, n);   // root frame
+                V3 cen = v3(0, 0, 0), cen0 = v3(0, 0, 0), pk = pts[0];
+                float wk[4], wsum = 0.f, phk = 0.f;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (k >= nr) continue;
+                    // (pts: relative to the root origin, world-oriented)
+                    float phi = pos.z + pts[k].z;
+                    if constexpr (HF) {
+                        V3 nk;
+                        bool th;
+                        const float gz = ground_at(a, pos.x + pts[k].x, pos.y + pts[k].y, nk, th);
+                        phi = (pos.z + pts[k].z - gz) * nk.z;
+                    }
+                    phk = k == kr ? phi : phk;
+                    // (component-wise: a select of whole V3s becomes a pointer
+                    // select over the array, which then stays in scratch)
+                    pk.x = k == kr ? pts[k].x : pk.x;
+                    pk.y = k == kr ? pts[k].y : pk.y;
+                    pk.z = k == kr ? pts[k].z : pk.z;
+                    wk[k] = fminf(fmaxf((a.margin - phi) / a.margin, 0.f), 1.f);
+                    wsum += wk[k];
+                    cen = cen + wk[k] * pts[k];
+                    cen0 = cen0 + pts[k];
+                }
+                const int ro = PL::ROW + i * 8;
+                if (kr < nr) {   // normal row kr: Jacobian about the root origin, separation
+                    stsv(s, ro, SV{cross(mulT(R, pk), dl), dl});
+                    s(ro + 6) = a.tgs ? phk : contact_target(a, phk, h);
+                    s(ro + 7) = 1.f;
+                } else {         // friction row t of the patch
+                    const int t = kr - nr;
+                    cen = wsum > 0.f ? (1.f / wsum) * cen : (1.f / nr) * cen0;
+                    if (t == 0) {
+                        float re = 0.f;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            if (k >= nr) continue;
+                            const V3 d = pts[k] - cen;
+                            const V3 dt = d - dot(d, n) * n;   // in the contact plane
+                            re += (wsum > 0.f ? wk[k] / wsum : 1.f / nr) * sqrtf(dot(dt, dt));
+                        }
+                        s(PL::SHP + 2 * sh) = 0.5f * ((SHP1 ? smu1 : a.shape_mu[(size_t)e * M::NS + sh]) + gmu);
+                        s(PL::SHP + 2 * sh + 1) = re;
+                    }
+                    V3 t1 = v3(1, 0, 0);
+                    {
+                        const V3 x = kind == TG_SHAPE_TORUS ? cross(v3(Rs.a[2], Rs.a[5], Rs.a[8]), n)
+                                                            : v3(1, 0, 0) - n.x * n;
+                        const float nx = sqrtf(dot(x, x));
+                        if (nx > 1e-6f) t1 = (1.f / nx) * x;
+                    }
+                    const V3 t2 = cross(n, t1);
+                    const V3 rl = mulT(R, cen);
+                    const V3 dt = mulT(R, t == 0 ? t1 : (t == 1 ? t2 : n));
+                    stsv(s, ro, t == 2 ? SV{dt, v3(0, 0, 0)} : SV{cross(rl, dt), dt});   // torsion row: angular
+                    s(ro + 6) = 0.f;
+                    s(ro + 7) = 1.f;
+                }
+            }
+            } else {
             // contact rows (one lane per shape)
             for (int sh = sub; sh < M::NS; sh += LPE) {
                 int cgi = M::shape_cg[0];   // (selected from the constant table, no load)
@@ -1780,6 +1921,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     s(ro + 7) = fon;
                 }
             }
+            }   // ROWPAR
             TG_SYNC();
             // row i: root-frame Jacobian J_i (6) -> velocity J_i . v, impulse lam J_i
             auto rvel = [&](int i, const SV &vg) { return dot(ldsv(s, PL::ROW + i * 8), vg); };
