@@ -538,6 +538,27 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
     // issued before the first LDS store: one memory round trip instead of one
     // per table (the stores would otherwise pin each table's loads behind the
     // previous one's)
+    // the env's state (root, joint positions and velocities), loaded early
+    // for one-round trees (EARLY) or, for the larger trees with an affine
+    // group -> dof map, inside the table fill (OVL, round 4: its round trip
+    // overlaps the table's; ThormangWalk -0.3 us, three A/B rounds,
+    // profiles/r4/state_overlap_ab.txt)
+#ifndef TG_STATE_OVERLAP
+#define TG_STATE_OVERLAP 1   // developer switch: 0 = the state loads after the table barrier (A/B)
+#endif
+#ifndef TG_EARLY_STATE
+#define TG_EARLY_STATE 0   // developer switch: 1 = every tree with an affine group -> dof map
+#endif
+    constexpr int NGR = (M::NG - 1 + LPE - 1) / LPE;
+    // one-round trees: the env's state issued before the barrier (group ->
+    // dof from the model's constants, not the LDS table) so its latency
+    // overlaps the table fill's (larger trees: measured no gain, more live
+    // registers across the barrier)
+    constexpr bool EARLY = NGR == 1 || (TG_EARLY_STATE && group_dof_offset<M>() != -1000);
+    constexpr bool OVL = TG_STATE_OVERLAP && !EARLY && group_dof_offset<M>() != -1000;
+    float q0[NGR > 0 ? NGR : 1], qd0[NGR > 0 ? NGR : 1], rt0[13];
+    const float *st_root = a.root + (size_t)e * 13;
+    const float *st_dofs = a.dof + (size_t)e * a.D * 2;
     constexpr int NT = EPB * M::LPE;
     constexpr bool ONE = M::NG <= NT && M::NSTEP * LPE <= NT && PackTab<M>::NPW * LPE <= NT &&
                          M::NCG * M::MAXD <= NT && 32 <= NT;
@@ -554,6 +575,20 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
         const I4 dv = DescTab<M>::tab.d[idd];
         const int pv = PackTab<M>::tab.v[ipk];
         const int cv = M::cpath[icp / M::MAXD][icp % M::MAXD];
+        if constexpr (OVL) {
+            // the env's state issued here, between the table loads and their
+            // stores: its memory round trip overlaps the table's instead of
+            // following the barrier (the group -> dof map from the model's
+            // constants)
+#pragma unroll
+            for (int r = 0; r < NGR; ++r) {
+                const int d = group_dof<M>(min(1 + sub + r * LPE, M::NG - 1));
+                q0[r] = st_dofs[2 * d];
+                qd0[r] = st_dofs[2 * d + 1];
+            }
+#pragma unroll
+            for (int k = 0; k < 13; ++k) rt0[k] = st_root[k];
+        }
         if (tid < M::NG) {
 #pragma unroll
             for (int k = 0; k < GIW; ++k) tab[PL::T_GI + tid * GIW + k] = gv[k];
@@ -671,16 +706,6 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
     }
     float *root = a.root + (size_t)e * 13;
     float *dofs = a.dof + (size_t)e * D * 2;
-    // one-round trees: the env's state issued before the barrier (group ->
-    // dof from the model's constants, not the LDS table) so its latency
-    // overlaps the table fill's (larger trees: measured no gain, more live
-    // registers across the barrier)
-    constexpr int NGR = (M::NG - 1 + LPE - 1) / LPE;
-#ifndef TG_EARLY_STATE
-#define TG_EARLY_STATE 0   // developer switch: 1 = every tree with an affine group -> dof map
-#endif
-    constexpr bool EARLY = NGR == 1 || (TG_EARLY_STATE && group_dof_offset<M>() != -1000);
-    float q0[NGR > 0 ? NGR : 1], qd0[NGR > 0 ? NGR : 1], rt0[13];
     if constexpr (EARLY) {
 #pragma unroll
         for (int r = 0; r < NGR; ++r) {
@@ -727,7 +752,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
     if constexpr ((M::FUSED & 4) != 0) {
         if (a.pp_in_step && a.pp.t7 && tid == 0) paper_t7_block(a.pp, reinterpret_cast<const float *>(tab + PL::T_T7), chunk);
     }
-    if constexpr (!EARLY) {
+    if constexpr (!EARLY && !OVL) {
 #pragma unroll
         for (int k = 0; k < 13; ++k) rt0[k] = root[k];
     }
@@ -740,7 +765,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             }
         }
     }
-    if constexpr (EARLY) {
+    if constexpr (EARLY || OVL) {
 #pragma unroll
         for (int r = 0; r < NGR; ++r) {
             const int g = 1 + sub + r * LPE;
