@@ -555,13 +555,15 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
     // overlaps the table fill's (larger trees: measured no gain, more live
     // registers across the barrier)
     constexpr bool EARLY = NGR == 1 || (TG_EARLY_STATE && group_dof_offset<M>() != -1000);
-    constexpr bool OVL = TG_STATE_OVERLAP && !EARLY && group_dof_offset<M>() != -1000;
     float q0[NGR > 0 ? NGR : 1], qd0[NGR > 0 ? NGR : 1], rt0[13];
     const float *st_root = a.root + (size_t)e * 13;
     const float *st_dofs = a.dof + (size_t)e * a.D * 2;
     constexpr int NT = EPB * M::LPE;
     constexpr bool ONE = M::NG <= NT && M::NSTEP * LPE <= NT && PackTab<M>::NPW * LPE <= NT &&
                          M::NCG * M::MAXD <= NT && 32 <= NT;
+    // (inside the one-pass table fill only: the whole-body model's 8-env
+    // workgroups fill the table in loops and load the state after the barrier)
+    constexpr bool OVL = TG_STATE_OVERLAP && ONE && !EARLY && group_dof_offset<M>() != -1000;
     if constexpr (ONE) {
         const int ig = tid < M::NG ? tid : 0, idd = tid < M::NSTEP * LPE ? tid : 0,
                   ipk = tid < PackTab<M>::NPW * LPE ? tid : 0, icp = tid < M::NCG * M::MAXD ? tid : 0;
