@@ -858,6 +858,11 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
     };
     // pass 1b: groups sub, sub + LPE, ... of the env (all lanes, no schedule)
     constexpr int NR1 = (M::NG + LPE - 1) / LPE;
+#ifdef TG_DEV_R2   // developer timing probe (results wrong): the all-groups passes stop after two rounds
+    constexpr int NRX = NR1 < 2 ? NR1 : 2;
+#else
+    constexpr int NRX = NR1;
+#endif
     auto load_inertia = [&](float (*x)[12]) {   // mass, com, inertia (10 + 2 pad) of the lane's groups
 #pragma unroll
         for (int r = 0; r < NR1; ++r) {
@@ -1272,7 +1277,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
 #endif
         TG_PROF(16)
 #pragma unroll
-        for (int r = 0; r < NR1; ++r) {
+        for (int r = 0; r < NRX; ++r) {
             const int g = sub + r * LPE;
             if (g < M::NG) body_bias(g, ldsv(s, g * GF + F_V), ldR(s, g), ldv3(s, g * GF + F_P), gr, cin[r]);
         }
@@ -1298,7 +1303,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             load_drv(bounded(gi[gc * GIW + GI_DOF], 0, 1 << 16), cdr[r]);
         }
 #pragma unroll
-        for (int r = 0; r < NR1; ++r) {
+        for (int r = 0; r < NRX; ++r) {
             const int g0 = sub + r * LPE;
             const bool valid = g0 > 0 && g0 < M::NG;
             const int g = min(max(g0, 1), M::NG - 1);
@@ -2591,7 +2596,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
         // (F_QD, v0v) when velocity iterations ran
         const bool vst = M::NS > 0 && (a.viters > 0 || a.tgs);
 #pragma unroll
-        for (int r = 0; r < (M::NG + LPE - 1) / LPE; ++r) {
+        for (int r = 0; r < NRX; ++r) {
             const int g = 1 + sub + r * LPE;
             if (g >= M::NG) break;
             const int o = g * GF;
