@@ -1134,7 +1134,25 @@ struct WalkPost {
     static constexpr bool on = true;
     static constexpr int NPRE = 0;
     static constexpr bool PM_OUT = true;   // stores the pre-physics' actions / targets (pm_in_step) below
+    static constexpr bool TOUCH = true;
     using Args = WalkPostArgs;
+    // the line of the epilogue's inputs lane `sub` touches in the last
+    // substep (step_par.h EPI_TOUCH): progress, reset flag, last actions (two
+    // lines), commands, the reset root state; the other lanes the first
+    template <class M, int LPE>
+    static __device__ __forceinline__ const float *touch_addr(const Args &pa, const StepArgs &, int e, int sub) {
+        const tg_walk_buffers &b = pa.b;
+        constexpr int D = M::ND;
+        const float *la = b.last_actions + (size_t)e * D;
+        switch (sub) {
+        case 1: return reinterpret_cast<const float *>(b.reset_buf + e);
+        case 2: return la;
+        case 3: return la + (D - 1);
+        case 4: return b.commands + 3 * (size_t)e;
+        case 5: return b.root_reset + 13 * (size_t)e;
+        default: return reinterpret_cast<const float *>(b.progress_buf + e);
+        }
+    }
     static __device__ __forceinline__ float clampw(float x, float lo, float hi) {
         return x < lo ? lo : (x > hi ? hi : x);
     }
@@ -1446,6 +1464,7 @@ template <class M> __device__ __forceinline__ void tl_update(float *c, const flo
 struct GogoroPost {
     static constexpr bool on = true;
     static constexpr bool PM_OUT = false;
+    static constexpr bool TOUCH = false;
     using Args = GogoroPostArgs;
     // the translating-lock extension of an env the previous step reset (its
     // reset happens in this epilogue), LPE lanes x NPRE floats, loaded at
