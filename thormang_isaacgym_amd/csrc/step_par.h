@@ -1118,7 +1118,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
         }
     };
 #ifndef TG_EPI_TOUCH
-X
+#define TG_EPI_TOUCH 0   // developer switch: 1 = touch the epilogue's inputs in the last substep (round 4 A/B: +0.6 us, AGPRs 54 -> 65; profiles/r4/epilogue_touch_ab.txt)
 #endif
     constexpr bool EPI_TOUCH = TG_EPI_TOUCH && P::TOUCH;
     float epi_touch = 0.f;
