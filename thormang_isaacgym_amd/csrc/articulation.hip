@@ -53,6 +53,24 @@ int launch_step_walk(uint64_t hash, const StepArgs &a, const WalkPostArgs &pa, h
     return jit_has(hash) ? 1 : TG_ERR_MODEL;
 }
 
+#ifdef TG_SECTION_PROF
+// developer builds: the section counters, summed over both units' step kernels
+int tree_cprof_read(unsigned long long *out, int n);
+int tree_prof_read(unsigned long long *out, int n);
+extern "C" int tg_cprof_read(unsigned long long *out, int n) {
+    unsigned long long a[8] = {}, b[8] = {};
+    if (hipMemcpyFromSymbol(a, HIP_SYMBOL(tg_cprof_acc), sizeof a) != hipSuccess || tree_cprof_read(b, 8)) return -1;
+    for (int k = 0; k < n && k < 8; ++k) out[k] = a[k] + b[k];
+    return 0;
+}
+extern "C" int tg_prof_read(unsigned long long *out, int n) {
+    unsigned long long a[24] = {}, b[24] = {};
+    if (hipMemcpyFromSymbol(a, HIP_SYMBOL(tg_prof_acc), sizeof a) != hipSuccess || tree_prof_read(b, 24)) return -1;
+    for (int k = 0; k < n && k < 24; ++k) out[k] = a[k] + b[k];
+    return 0;
+}
+#endif
+
 #define TG_HASH(MODEL) if (n < cap) out[n] = MODEL::hash; ++n;
 #define TG_KC(MODEL) if (hash == MODEL::hash) return MODEL::KC;
 

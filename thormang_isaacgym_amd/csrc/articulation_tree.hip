@@ -28,16 +28,15 @@ int tree_launch_step_walk(uint64_t hash, const StepArgs &a, const WalkPostArgs &
 }
 
 // developer builds: the section counters of this unit's step kernels
+// (articulation.hip's tg_prof_read / tg_cprof_read add them to its own)
 #ifdef TG_SECTION_PROF
-extern "C" int tg_cprof_read(unsigned long long *out, int n) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tg_cprof_acc), sizeof(unsigned long long) * (n < 8 ? n : 8)) != hipSuccess)
-        return -1;
-    return 0;
+int tree_cprof_read(unsigned long long *out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(tg_cprof_acc), sizeof(unsigned long long) * (n < 8 ? n : 8)) ==
+                   hipSuccess ? 0 : -1;
 }
-extern "C" int tg_prof_read(unsigned long long *out, int n) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tg_prof_acc), sizeof(unsigned long long) * (n < 24 ? n : 24)) != hipSuccess)
-        return -1;
-    return 0;
+int tree_prof_read(unsigned long long *out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(tg_prof_acc), sizeof(unsigned long long) * (n < 24 ? n : 24)) ==
+                   hipSuccess ? 0 : -1;
 }
 #endif
 
