@@ -131,19 +131,41 @@ def brief(err):
     return {k: v for k, v in err.items() if not k.startswith("_")}
 
 
-def within(err, key="obs", tol=1e-3, factor=2.0):
+def within(err, key="obs", tol=1e-3):
     """The parity bar, north_star's: the GPU-vs-fp64-oracle error under
-    ``tol`` = 1e-3.  The one exception is a run that carries the rounding
-    control (``err[key + "_f32"]``: the fp32 build of the same oracle on the
-    same inputs) whose control *itself* leaves the 1e-3 band -- a trajectory
-    on which fp32 rounding alone is amplified past the bar (a falling
-    humanoid).  Only then the bar is ``factor`` (2) times the control's own
-    departure, the GPU-vs-fp32-build ratio measured at the 99.9th percentile
-    (DESIGN.md §2).  A control under 1e-3 leaves the bar at 1e-3."""
-    c = err.get(key + "_f32")
-    if c is None or c <= tol:
+    ``tol`` = 1e-3 at every compared step.
+
+    The one qualification is a FREE-RUNNING run that carries the rounding
+    control (the fp32 build of the same oracle, stepped beside the fp64 one
+    on the same inputs) and whose control itself leaves the band: its first
+    departure, ``err["ctl_first_bad"]`` (obs or reward over ``tol`` or a
+    reset flag changed), is the step from which fp32 rounding alone no longer
+    determines the trajectory to 1e-3 (a falling humanoid).  The GPU is then
+    held to ``tol`` at every step BEFORE that step (the per-step trace
+    ``err["_<key>_t"]``) and nothing is asserted after it -- the control
+    never raises the bar (the round-4 form, 2x the control's
+    whole-run maximum, let a diverged control loosen it to 10).  Without a
+    departure, or without a control, the whole run is held to ``tol``;
+    teacher-forced runs never set a departure step."""
+    h = err.get("ctl_first_bad")
+    trace = err.get("_" + key + "_t")
+    if h is None or trace is None:
         return err[key] < tol
-    return err[key] < factor * c
+    return (max(trace[:h]) if h > 0 else 0.0) < tol
+
+
+def note_control(err, t, c_obs, c_rew, c_reset, o_obs, o_rew, o_reset, tol=1e-3):
+    """The fp32 rounding control's step-t errors against the fp64 oracle
+    (maxima in ``obs_f32`` / ``rew_f32``) and its first departure from the
+    band, ``ctl_first_bad`` (``within``)."""
+    ce = float(np.abs(c_obs - o_obs).max())
+    cr = float(np.abs(c_rew - o_rew).max())
+    err["obs_f32"] = max(err.get("obs_f32", 0.0), ce)
+    err["rew_f32"] = max(err.get("rew_f32", 0.0), cr)
+    same = bool(np.array_equal(c_reset, o_reset))
+    err["ctl_reset_equal"] = err.get("ctl_reset_equal", True) and same
+    if (ce > tol or cr > tol or not same) and "ctl_first_bad" not in err:
+        err["ctl_first_bad"] = t
 
 
 def tgs_configured(cfg):
@@ -169,7 +191,7 @@ def gogoro_env_vs_oracle(num_envs=64, steps=20, seed=0, policy=None, max_steps=1
     ctl = OracleGogoro(parity_cfg(num_envs, max_steps=max_steps, dr=dr), NumpyDraws(seed), fix_base=fix_base,
                        precision="f32") if control else None
     err = {"obs": 0.0, "rew": 0.0, "reset_equal": True, "timeout_equal": True, "root": 0.0, "steps": steps,
-           "resets": 0}
+           "resets": 0, "_obs_t": [], "_rew_t": []}
     if ctl is not None:
         err["obs_f32"] = err["rew_f32"] = 0.0
     obs_np = orc.a["obs_buf"].copy()
@@ -182,17 +204,20 @@ def gogoro_env_vs_oracle(num_envs=64, steps=20, seed=0, policy=None, max_steps=1
         obs_d, rew, reset, extras = env.step(torch.from_numpy(act).to("cuda:0"))
         o_obs, o_rew, o_reset, o_to = orc.step(act[:, 0])
         if ctl is not None:
-            c_obs, c_rew = ctl.step(act[:, 0])[:2]
-            err["obs_f32"] = max(err["obs_f32"], float(np.abs(c_obs - o_obs).max()))
-            err["rew_f32"] = max(err["rew_f32"], float(np.abs(c_rew - o_rew).max()))
+            c_obs, c_rew, c_reset = ctl.step(act[:, 0])[:3]
+            note_control(err, t, c_obs, c_rew, c_reset, o_obs, o_rew, o_reset)
         g_obs = obs_d["obs"].cpu().numpy()
-        err["obs"] = max(err["obs"], float(np.abs(g_obs - o_obs).max()))
-        err["rew"] = max(err["rew"], float(np.abs(rew.cpu().numpy() - o_rew).max()))
+        e_obs = float(np.abs(g_obs - o_obs).max())
+        e_rew = float(np.abs(rew.cpu().numpy() - o_rew).max())
+        err["_obs_t"].append(e_obs)
+        err["_rew_t"].append(e_rew)
+        err["obs"] = max(err["obs"], e_obs)
+        err["rew"] = max(err["rew"], e_rew)
         err["root"] = max(err["root"], float(np.abs(env.root_tensor.cpu().numpy() - orc.a["root"]).max()))
         err["reset_equal"] &= bool(np.array_equal(reset.cpu().numpy(), o_reset))
         err["timeout_equal"] &= bool(np.array_equal(extras["time_outs"].cpu().numpy().astype(np.uint8), o_to))
         err["resets"] += int(o_reset.sum())
-        if not within(err) and "first_bad_step" not in err:
+        if (e_obs >= 1e-3 or e_rew >= 1e-3) and "first_bad_step" not in err:
             err["first_bad_step"] = t
         obs_np = o_obs.copy()
     err["resets_seen"] = int(orc.a["progress_buf"].min())
@@ -259,13 +284,15 @@ def forced_step_errors(env, orc, act_fn, steps, act_to_orc=lambda a: a, ctl=None
     return err
 
 
-def gogoro_forced(num_envs=64, steps=1000, seed=0, max_steps=300, dr=False):
+def gogoro_forced(num_envs=64, steps=1000, seed=0, max_steps=300, dr=False, policy=None, threads=8):
+    """Teacher-forced Gogoro (the oracle re-synced from the GPU env before
+    every step) under ``policy`` (default: the balance controller)."""
     cfg = parity_cfg(num_envs, max_steps=max_steps, dr=dr)
     env = make_gpu_gogoro(cfg, NumpyDraws(seed))
-    orc = OracleGogoro(parity_cfg(num_envs, max_steps=max_steps, dr=dr), NumpyDraws(seed))
-    ctl = OracleGogoro(parity_cfg(num_envs, max_steps=max_steps, dr=dr), NumpyDraws(seed),
+    orc = OracleGogoro(parity_cfg(num_envs, max_steps=max_steps, dr=dr), NumpyDraws(seed), threads=threads)
+    ctl = OracleGogoro(parity_cfg(num_envs, max_steps=max_steps, dr=dr), NumpyDraws(seed), threads=threads,
                        precision="f32") if tgs_configured(cfg) else None
-    err = forced_step_errors(env, orc, balance_policy, steps, act_to_orc=lambda a: a[:, 0], ctl=ctl)
+    err = forced_step_errors(env, orc, policy or balance_policy, steps, act_to_orc=lambda a: a[:, 0], ctl=ctl)
     if dr:
         err["gravity"] = list(env.sim.gravity)
         err["mass_scale_range"] = [float(env.sim.body_mass_scale.min()), float(env.sim.body_mass_scale.max())]
@@ -525,18 +552,15 @@ def walk_env_vs_oracle(num_envs=32, steps=30, seed=0, task="ThormangWalk", dr=Fa
         g_obs = obs_d["obs"].cpu().numpy()
         if ctl is not None:
             c_obs, c_rew, c_reset = ctl.step(act)[:3]
-            ce = float(np.abs(c_obs - o_obs).max())
-            err["obs_f32"] = max(err["obs_f32"], ce)
-            err["rew_f32"] = max(err["rew_f32"], float(np.abs(c_rew - o_rew).max()))
-            err["ctl_reset_equal"] &= bool(np.array_equal(c_reset, o_reset))
+            note_control(err, t, c_obs, c_rew, c_reset, o_obs, o_rew, o_reset)
             err["gpu_vs_f32"] = max(err["gpu_vs_f32"], float(np.abs(g_obs - c_obs).max()))
-            if (ce > 1e-3 or not err["ctl_reset_equal"]) and "ctl_first_bad" not in err:
-                err["ctl_first_bad"] = t
-        for pk in perts:
+        for k, pk in enumerate(perts):
             p_obs, _, p_reset = pk.step(act)[:3]
-            if "pert_first_bad" not in err and (float(np.abs(p_obs - o_obs).max()) > 1e-3 or
-                                                not np.array_equal(p_reset, o_reset)):
-                err["pert_first_bad"] = t
+            dep = err.setdefault("pert_departures", [None] * len(perts))
+            if dep[k] is None and (float(np.abs(p_obs - o_obs).max()) > 1e-3 or
+                                   not np.array_equal(p_reset, o_reset)):
+                dep[k] = t
+                err.setdefault("pert_first_bad", t)
         e_obs = float(np.abs(g_obs - o_obs).max())
         if e_obs > 1e-3 and "first_over_tol" not in err:
             err["first_over_tol"] = t
@@ -562,7 +586,7 @@ def walk_env_vs_oracle(num_envs=32, steps=30, seed=0, task="ThormangWalk", dr=Fa
                        reset_diff_tie=bool(np.all(margin < 1e-3)))
         err["reset_equal"] &= bool(np.array_equal(r_g, o_reset))
         err["timeout_equal"] &= bool(np.array_equal(extras["time_outs"].cpu().numpy().astype(np.uint8), o_to))
-        if not within(err) and "first_bad_step" not in err:
+        if (e_obs >= 1e-3 or e_rew >= 1e-3) and "first_bad_step" not in err:
             err["first_bad_step"] = t
     err["resets"] = int(n_resets(orc))
     err["min_height"] = float(orc.a["root"][:, 2].min())

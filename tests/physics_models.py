@@ -59,3 +59,54 @@ def system_com(m, root, q):
         acc += l.mass * (p + R @ np.asarray(l.com))
         tot += l.mass
     return acc / tot
+
+
+def drop_box(solver_type, iters=4, viters=1, rest_offset=0.0, z0=0.25, steps=90, dt=1.0 / 60.0, substeps=2,
+             step_fn=None):
+    """A 0.1 m box (kat_models.box_body, half height 0.05) released at rest
+    ``z0`` above the ground under gravity, with the walk cfg's solver
+    (cfg/task/ThormangWalk.yaml: dt 1/60 x 2 substeps, TGS 4 position + 1
+    velocity iterations).  Returns the per-step root height and vertical
+    velocity.  ``step_fn(desc, sp, root, dof, props, pt, vt)`` steps one env
+    (default: the CPU oracle)."""
+    from tests.oracle_lib import physics_step
+    m = box_body(mu=0.8)
+    sp = sim_params_from_cfg({"dt": dt, "substeps": substeps, "gravity": [0, 0, -9.81],
+                              "physx": {"num_position_iterations": iters, "num_velocity_iterations": viters,
+                                        "rest_offset": rest_offset, "max_depenetration_velocity": 1.0,
+                                        "solver_type": solver_type}},
+                             dict(angular_damping=0.0, linear_damping=0.0, ground_friction=0.8), 1, warn=False)
+    desc = ModelDesc(m)
+    props = default_dof_props(m, 1)
+    root = np.zeros((1, 13), np.float32)
+    root[0, 2] = z0
+    root[0, 6] = 1.0
+    dof = np.zeros((0, 2), np.float32)
+    z = np.zeros((1, 0), np.float32)
+    step = step_fn or physics_step
+    zs, vs = [], []
+    for _ in range(steps):
+        step(desc, sp, root, dof, props, z, z)
+        zs.append(float(root[0, 2]))
+        vs.append(float(root[0, 9]))
+    return np.array(zs), np.array(vs)
+
+
+def landing_checks(zs, vs, rest_offset=0.0, half=0.05):
+    """What the physics itself requires of a restitution-0 landing, whatever
+    the solver's internals: once the box has reached the ground
+    it never moves up again by more than 0.5 mm nor leaves with an upward
+    velocity over 2 cm/s (no rebound), it never sinks more than 2 mm below
+    its rest height, and it comes to rest at half height + rest offset
+    within 0.5 mm, at rest within 1 mm/s.  Returns a dict of the measured
+    quantities and ``ok``."""
+    rest = half + rest_offset
+    hit = int(np.argmax(zs < rest + 0.002))
+    after = zs[hit:]
+    out = {"hit_step": hit, "rise_after_hit": float(after.max() - after[0]) if len(after) else 0.0,
+           "max_up_velocity": float(vs[hit:].max()), "min_height": float(zs.min()) - rest,
+           "final_height": float(zs[-1]) - rest, "final_vz": float(vs[-1])}
+    out["ok"] = bool(hit > 0 and zs[hit - 1] > rest + 0.002 and out["rise_after_hit"] < 5e-4 and
+                     out["max_up_velocity"] < 0.02 and out["min_height"] > -0.002 and
+                     abs(out["final_height"]) < 5e-4 and abs(out["final_vz"]) < 1e-3)
+    return out

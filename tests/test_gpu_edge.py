@@ -123,7 +123,33 @@ def test_gpu_rb_forces_survive_a_declined_fused_walk_step():
     assert float((r0[:, 7] - r2[:, 7]).abs().min()) > 1e-2   # the push acted
 
 
-@pytest.mark.parametrize("task", ["Gogoro", "GogoroPaper", "ThormangWalk", "ThormangWalkDR"])
+def _probe_env(case, n):
+    """The env of one stale-LDS probe case: a task, or a task on a model /
+    kernel variant -- ``+wb`` the whole-body walk model (thormang_wb: 8-env
+    workgroups, the looped table fill), ``+hf`` the heightfield instantiation
+    of the step kernel (the walk on a heightfield below the plane; Gogoro
+    with USE_TERAIN, its Perlin trimesh)."""
+    import thormang_isaacgym_amd as tia
+    from thormang_isaacgym_amd.cfg import load_task_cfg
+    task, _, var = case.partition("+")
+    cfg = load_task_cfg(task, num_envs=n)
+    if var == "wb":
+        cfg["env"]["asset"] = dict(cfg["env"].get("asset", {}), wholeBodyCollision=True)
+    if var == "hf" and task == "Gogoro":
+        from thormang_isaacgym_amd.tasks import gogoro as gmod
+        saved, gmod.USE_TERAIN = gmod.USE_TERAIN, True
+        try:
+            return tia.make(seed=11, task=task, num_envs=n, sim_device="cuda:0", rl_device="cuda:0", cfg=cfg)
+        finally:
+            gmod.USE_TERAIN = saved
+    env = tia.make(seed=11, task=task, num_envs=n, sim_device="cuda:0", rl_device="cuda:0", cfg=cfg)
+    if var == "hf":
+        env.sim.set_heightfield(np.full((16, 16), 0.01, np.float32), 1.0, 1.0, -8.0, -8.0, friction=1.0)
+    return env
+
+
+@pytest.mark.parametrize("task", ["Gogoro", "GogoroPaper", "ThormangWalk", "ThormangWalkDR", "ThormangWalk+wb",
+                                  "ThormangWalk+hf", "Gogoro+hf"])
 def test_gpu_steps_read_no_stale_lds(task):
     """No kernel of a step reads LDS it has not written this launch (round 3:
     the Woodbury update once multiplied an unwritten slot by zero, and a NaN
@@ -131,15 +157,17 @@ def test_gpu_steps_read_no_stale_lds(task):
     random actions; a second env from the same seed (tia.make re-seeds torch,
     so the DR draws repeat) steps them again with every CU's LDS filled with
     a NaN or FLT_MAX pattern (tg_debug_fill_lds) before every step, and the
-    results must be bit-identical.  48 envs: a partial last workgroup."""
+    results must be bit-identical.  48 envs: a partial last workgroup.
+    Round 5: also the whole-body model (whose looped
+    table fill once left the env state unloaded, caught only by its kneel
+    test) and the heightfield instantiations."""
     _cuda()
-    import thormang_isaacgym_amd as tia
     n, steps = 48, 40
     g = torch.Generator(device="cuda:0").manual_seed(4)
     acts = [torch.rand(n, 64, device="cuda:0", generator=g) * 2 - 1 for _ in range(steps)]
     runs = []
     for fill in (False, True):
-        env = tia.make(seed=11, task=task, num_envs=n, sim_device="cuda:0", rl_device="cuda:0")
+        env = _probe_env(task, n)
         out = []
         for t in range(steps):
             if fill:

@@ -226,6 +226,24 @@ def test_gpu_env_step_matches_oracle_along_1000_steps():
     assert err["reset_equal"] and err["timeout_equal"], err
 
 
+def test_gpu_gogoro_4096_envs_step_matches_oracle():
+    """BASELINE config 2's batch (Gogoro, 4096 envs, cfg/task/Gogoro.yaml:6)
+    against the oracle env: 100 teacher-forced steps of every env under the
+    bench's own action distribution (U(-1,1) steering increments: the
+    scooters swerve and fall, so resets, re-spawns and the in-place seat
+    composites run at the headline batch), the reference's 1000-step episode
+    length."""
+    _cuda()
+    from tests.gpu_harness import gogoro_forced
+    rs = np.random.default_rng(4096)
+    err = gogoro_forced(num_envs=4096, steps=100, seed=23, max_steps=1000, threads=16,
+                        policy=lambda o: rs.uniform(-1, 1, (o.shape[0], 1)).astype(np.float32))
+    print(err)
+    assert err["resets"] > 2048, err      # the scooters fall and re-spawn along the way
+    assert within(err) and within(err, "rew"), err
+    assert err["reset_equal"] and err["timeout_equal"], err
+
+
 def test_gpu_gogoro_inplace_seat_composites_equal_a_full_compose():
     """The fused epilogue's resets move only the seat locks (base_x/y/z), so it
     updates the rider group's composite and the placements below the seat in

@@ -120,6 +120,28 @@ def test_gpu_contact_matches_oracle_and_rests(shape, solver):
     assert worst < 5e-3, worst
 
 
+@pytest.mark.parametrize("solver,viters,rest", [(1, 1, 0.0), (1, 4, 0.002), (0, 1, 0.0)])
+def test_gpu_landing_known_answer_no_rebound_and_rest_height(solver, viters, rest):
+    """The landing known answer of tests/test_solver_cfg.py on the GPU kernel
+    itself (behaviour the physics requires, not agreement with the
+    oracle): the box dropped 0.2 m with the walk cfg's step lands without
+    rebound and rests at half height + rest offset."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs the MI355X")
+    sims = {}
+
+    def gpu_step(desc, sp, root, dof, props, pt, vt):
+        if "g" not in sims:
+            sims["g"] = gpu_sim(pm.box_body(mu=0.8), sp, 1, root, dof, props, pt, vt)
+        g = sims["g"]
+        g.simulate()
+        root[...] = g.root_state.cpu().numpy()
+    zs, vs = pm.drop_box(solver, viters=viters, rest_offset=rest, step_fn=gpu_step)
+    r = pm.landing_checks(zs, vs, rest_offset=rest)
+    print(r)
+    assert r["ok"], r
+
+
 def test_gpu_free_fall_exact():
     if not torch.cuda.is_available():
         pytest.skip("needs the MI355X")

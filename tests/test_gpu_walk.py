@@ -25,15 +25,16 @@ def test_gpu_walk_matches_oracle_env():
 
 def test_gpu_walk_dr_pushes_match_oracle_env():
     """ThormangWalkDR (pushes), 32 envs, 200 free-running steps, with the fp32
-    rounding control beside it: on this seed the control's own reward error
-    reaches 1.45e-3 (round 4), i.e. the trajectory is rounding-sensitive past
-    the bar; the GPU's (8.6e-4) is held to 1e-3 unless the control leaves it
-    (tests/gpu_harness.within: then 2x the control)."""
+    rounding control beside it, recorded only: on this seed the control's own
+    reward error reaches 1.45e-3 (round 4), i.e. the trajectory is
+    rounding-sensitive past the bar, but the GPU meets it (8.6e-4), so the
+    GPU is held to 1e-3 over all 200 steps -- the control does not shorten
+    the asserted span here."""
     _cuda()
     from tests.gpu_harness import walk_env_vs_oracle
     err = walk_env_vs_oracle(num_envs=32, steps=200, seed=7, task="ThormangWalkDR", control=True)
     print(brief(err))
-    assert within(err) and within(err, "rew"), err
+    assert err["obs"] < 1e-3 and err["rew"] < 1e-3, brief(err)
     assert err["reset_equal"], err
 
 

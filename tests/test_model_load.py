@@ -174,6 +174,40 @@ def test_native_loader_number_parsing_ignores_the_host_locale(tmp_path):
     assert abs(a["link_inertia"][0] - 0.5) < 1e-7, a["link_inertia"][:10]
 
 
+def test_native_loader_parses_numbers_as_python_float(tmp_path):
+    """a number attribute reads as the Python host's float() reads
+    it (model/urdf.py) -- blanks around it, underscores between digits, an
+    exponent, inf / nan in any case -- and what float() rejects (hex floats,
+    misplaced underscores, trailing text) is an error."""
+    ok = '<joint name="bc" type="fixed"><parent link="B"/><child link="C"/></joint>'
+    for text, want in ((" 1_0.5 ", 10.5), ("1E1", 10.0), ("+2.5e-1", 0.25)):
+        p = tmp_path / "m.urdf"
+        p.write_text(MINI.format(m=text, extra=ok))
+        a, _ = native(str(p))
+        assert abs(a["link_inertia"][0] - want) < 1e-12 * max(1.0, want), (text, a["link_inertia"][0])
+    for text in ("inf", "-Infinity", "NaN", "1e999"):   # accepted by float(); the parse itself must not fail
+        rc, msg = _parse_text(tmp_path, MINI.format(m=text, extra=ok))
+        assert "malformed number" not in msg, (text, msg)
+    for text in ("0x1p3", "1__0", "_1", "1_", "1.5 2", "nan1"):
+        rc, msg = _parse_text(tmp_path, MINI.format(m=text, extra=ok))
+        assert rc == TG_ERR_MODEL and "malformed number" in msg, (text, msg)
+
+
+def test_native_loader_bounds_the_link_chain_depth(tmp_path):
+    """the depth-first walk over the joint tree is recursive, so a
+    hostile 2000-link chain is refused with a message (no stack exhaustion);
+    a 200-link chain still loads."""
+    def chain(n):
+        links = "".join(f'<link name="L{i}"/>' for i in range(n))
+        joints = "".join(f'<joint name="j{i}" type="fixed"><parent link="L{i}"/><child link="L{i + 1}"/></joint>'
+                         for i in range(n - 1))
+        return f'<robot name="c">{links}{joints}</robot>'
+    rc, msg = _parse_text(tmp_path, chain(2000))
+    assert rc == TG_ERR_MODEL and "deeper than" in msg, msg
+    rc, msg = _parse_text(tmp_path, chain(200))
+    assert rc == 0, msg
+
+
 @pytest.mark.skipif(not os.path.exists(REF), reason="reference assets not present (build container only)")
 def test_native_loader_on_the_reference_assets():
     """The registered task's scooter with the reference's locked joints and the

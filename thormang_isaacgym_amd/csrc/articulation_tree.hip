@@ -43,14 +43,19 @@ int tree_prof_read(unsigned long long *out, int n) {
 }  // namespace tg
 
 #ifdef TG_DUMP_ENV
-// developer build only: select the env whose first-substep contact solve the
-// step kernel dumps, and read the dump back (scripts/dev/contact_dump.py)
-extern "C" int tg_debug_dump_env(int e, int substep) {
-    if (hipMemcpyToSymbol(HIP_SYMBOL(tg::tg_dump_sub), &substep, sizeof(int)) != hipSuccess) return -2;
-    return hipMemcpyToSymbol(HIP_SYMBOL(tg::tg_dump_env), &e, sizeof(int)) == hipSuccess ? 0 : -2;
+// developer build only (scripts/dev/contact_dump.py): this unit's copies of
+// the dump symbols (tg_dump_* are static __device__, so each unit's step
+// kernels have their own); articulation.hip's tg_debug_dump_env /
+// tg_debug_dump_read arm and read both units
+namespace tg {
+int tree_dump_arm(int e, int substep) {
+    static float zero[4096];
+    if (hipMemcpyToSymbol(HIP_SYMBOL(tg_dump_buf), zero, sizeof zero) != hipSuccess) return -2;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(tg_dump_sub), &substep, sizeof(int)) != hipSuccess) return -2;
+    return hipMemcpyToSymbol(HIP_SYMBOL(tg_dump_env), &e, sizeof(int)) == hipSuccess ? 0 : -2;
 }
-extern "C" int tg_debug_dump_read(float *out, int n) {
-    if (n > 4096) n = 4096;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(tg::tg_dump_buf), (size_t)n * 4) == hipSuccess ? 0 : -2;
+int tree_dump_read(float *out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(tg_dump_buf), (size_t)n * 4) == hipSuccess ? 0 : -2;
 }
+}  // namespace tg
 #endif

@@ -22,6 +22,8 @@
 
 #include <algorithm>
 #include <cctype>
+#include <cerrno>
+#include <clocale>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -199,38 +201,59 @@ struct Shape {
     double friction = 1.0;
 };
 
+// one number token as the Python host's float() reads it (model/urdf.py):
+// surrounding blanks allowed, decimal point '.' whatever LC_NUMERIC the host
+// set (strtod_l in the "C" locale), "inf" / "infinity" / "nan" in any case
+// with an optional sign, overflow to +-inf, underscores only between digits,
+// and the WHOLE token consumed -- no hex floats (strtod's, not float()'s)
+bool parse_float(const std::string &tok, double &out) {
+    size_t b = tok.find_first_not_of(" \t\r\n"), e = tok.find_last_not_of(" \t\r\n");
+    if (b == std::string::npos) return false;
+    std::string t;
+    for (size_t k = b; k <= e; ++k) {
+        const char c = tok[k];
+        if (c == 'x' || c == 'X') return false;
+        if (c == '_') {   // float("1_000.5") == 1000.5; "1__0", "_1", "1_" are errors
+            if (k == b || k == e || !std::isdigit((unsigned char)tok[k - 1]) || !std::isdigit((unsigned char)tok[k + 1]))
+                return false;
+            continue;
+        }
+        t += c;
+    }
+    static const locale_t c_loc = newlocale(LC_ALL_MASK, "C", (locale_t)0);
+    char *end = nullptr;
+    errno = 0;
+    const double v = strtod_l(t.c_str(), &end, c_loc);
+    if (end == t.c_str() || *end != '\0') return false;
+    out = v;   // (ERANGE overflow: +-HUGE_VAL = +-inf, as float("1e999"); underflow: 0 or a denormal, as float())
+    return true;
+}
+
 bool vec_attr(const XNode *el, const char *key, int n, double dflt, double *out, std::string &err) {
     for (int i = 0; i < n; ++i) out[i] = dflt;
     if (!el) return true;
     const std::string *v = el->attr(key);
     if (!v) return true;
     std::istringstream is(*v);
-    is.imbue(std::locale::classic());   // '.' decimals whatever LC_NUMERIC the host set
-    for (int i = 0; i < n; ++i)
-        if (!(is >> out[i])) {
-            err = std::string("expected ") + std::to_string(n) + " numbers in " + key + "=\"" + *v + "\"";
-            return false;
-        }
-    std::string extra;
-    if (is >> extra) {
+    std::string tok;
+    int i = 0;
+    for (; is >> tok; ++i)
+        if (i >= n || !parse_float(tok, out[i])) break;
+    if (i != n || (is >> tok)) {
         err = std::string("expected ") + std::to_string(n) + " numbers in " + key + "=\"" + *v + "\"";
         return false;
     }
     return true;
 }
 
-// one number attribute (absent: dflt).  Parsed in the classic locale and
-// required to consume the whole value (surrounding blanks aside), as the
-// Python host's float() does: a malformed value is an error, not a silent 0
+// one number attribute (absent: dflt), parsed as float() parses it
+// (parse_float): a malformed value is an error, not a silent 0
 bool num_attr(const XNode *el, const char *key, double dflt, double &out, std::string &err) {
     out = dflt;
     if (!el) return true;
     const std::string *v = el->attr(key);
     if (!v) return true;
-    std::istringstream is(*v);
-    is.imbue(std::locale::classic());
-    std::string extra;
-    if (!(is >> out) || (is >> extra)) {
+    if (!parse_float(*v, out)) {
         err = std::string("malformed number in ") + el->tag + " " + key + "=\"" + *v + "\"";
         return false;
     }
@@ -436,7 +459,21 @@ bool build_model(const std::string &path, const std::string &name, const std::ve
     std::function<int(const std::string &, int, int)> dfs;
     std::set<std::string> visited;
     bool ok = true;
+    // the joint-tree depth is bounded like the XML nesting: a hostile chain of
+    // links must not exhaust the stack through this recursion
+    static constexpr int kMaxTreeDepth = 1024;
+    int tdepth = 0;
     dfs = [&](const std::string &lname, int parent, int joint) -> int {
+        if (tdepth >= kMaxTreeDepth) {
+            err = "URDF: link chain deeper than " + std::to_string(kMaxTreeDepth);
+            ok = false;
+            return -1;
+        }
+        struct Depth {
+            int &d;
+            explicit Depth(int &x) : d(++x) {}
+            ~Depth() { --d; }
+        } depth_guard(tdepth);
         auto it = link_el.find(lname);
         if (it == link_el.end()) {
             err = "URDF: joint child link " + lname + " not declared";
