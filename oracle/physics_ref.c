@@ -712,7 +712,19 @@ static int support_points(const tg_model_desc *m, int s, const M3 R, const V3 c,
     return 0;
 }
 
-static int collect_rows(const Env *e, Work *w, real h, Row *rows, Patch *patches, int *npatch) {
+/* physx.contact_offset (round 5): a point whose separation above the rest
+ * offset is not below the contact offset plus its free approach over the
+ * substep, max(0, -vn) h, has no normal row this substep -- its separation
+ * becomes NO_ROW, whose target -NO_ROW/h no row velocity reaches, so its
+ * multiplier stays 0 (the kernel's contact_row_phi, articulation_kernels.h).
+ * contact_offset <= 0: every point speculative (rounds 1-4). */
+#define NO_ROW ((real)1e30f)
+static real contact_row_phi(const tg_sim_params *sp, real phi, real vn, real h) {
+    const real off = sp->contact_offset, ap = vn < 0 ? -vn : 0;
+    return (off > 0 && !(phi - sp->rest_offset < off + ap * h)) ? NO_ROW : phi;
+}
+
+static int collect_rows(const Env *e, Work *w, real h, const V6 *vg, Row *rows, Patch *patches, int *npatch) {
     const tg_model_desc *m = e->m;
     int nr = 0, np_ = 0;
     for (int s = 0; s < m->num_shapes; ++s) {
@@ -760,8 +772,8 @@ static int collect_rows(const Env *e, Work *w, real h, Row *rows, Patch *patches
             for (int j = 0; j < 3; ++j) rel[j] = pts[k][j] - w->pw[g][j];
             m3T_v(w->Rw[g], rel, r->r);
             memcpy(r->d, n, sizeof(V3));
-            r->phi = phi;
-            r->target = row_target(e->sp, phi, h);
+            r->phi = contact_row_phi(e->sp, phi, row_vel(w, r, vg), h);
+            r->target = row_target(e->sp, r->phi, h);
             real wv = (margin - phi) / margin;
             wk[k] = wv < 0 ? 0 : (wv > 1 ? 1 : wv);
             wsum += wk[k];
@@ -862,12 +874,12 @@ static void solve_contacts(const Env *e, Work *w, real h, real *qds, V6 v0s, rea
     Row rows[3 * MAXC];
     Patch patches[MAXC];
     int npatch = 0;
-    int K = collect_rows(e, w, h, rows, patches, &npatch);
+    V6 vg[MAXG];
+    group_vels(m, w, qds, v0s, vg);
+    int K = collect_rows(e, w, h, vg, rows, patches, &npatch);
     if (K == 0) return;
     static __thread real W[3 * MAXC][3 * MAXC];
     real vfree[3 * MAXC], lam[3 * MAXC], target[3 * MAXC];
-    V6 vg[MAXG];
-    group_vels(m, w, qds, v0s, vg);
     for (int i = 0; i < K; ++i) vfree[i] = row_vel(w, &rows[i], vg);
     for (int col = 0; col < K; ++col) {
         V6 fi[MAXG];

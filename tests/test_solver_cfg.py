@@ -25,17 +25,19 @@ def _cfg_sim():
         return yaml.safe_load(f)["sim"]
 
 
-def test_gogoro_cfg_warns_on_each_unhonoured_key():
-    with pytest.warns(SolverCfgWarning) as rec:
-        sp = sim_params_from_cfg(_cfg_sim())
-    msg = " ".join(str(w.message) for w in rec)
-    assert "contact_offset" in msg
-    # resource knobs, honoured keys (solver_type 1 = TGS since round 3) and the
-    # inert bounce threshold (restitution 0 everywhere) are not reported
-    for k in ("num_threads", "num_subscenes", "max_gpu_contact_pairs", "num_position_iterations",
-              "num_velocity_iterations", "rest_offset", "max_depenetration_velocity", "solver_type",
-              "bounce_threshold_velocity"):
-        assert f"{k}:" not in msg, k
+@pytest.mark.parametrize("task", ["Gogoro", "GogoroPaper", "ThormangWalk", "ThormangWalkDR"])
+def test_task_cfgs_raise_no_solver_warning(task):
+    """Every sim.physx key of the shipped task cfgs is honoured or inert since
+    round 5 (contact_offset was the last one): building
+    the sim params from them raises no SolverCfgWarning."""
+    import os
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(here, "thormang_isaacgym_amd", "cfg", "task", task + ".yaml")) as f:
+        sim = yaml.safe_load(f)["sim"]
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", SolverCfgWarning)
+        sp = sim_params_from_cfg(sim)
+    assert abs(sp.contact_offset - float(sim["physx"]["contact_offset"])) < 1e-9
     assert sp.solver_type == 1
 
 

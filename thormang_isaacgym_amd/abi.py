@@ -46,6 +46,7 @@ class tg_sim_params(C.Structure):
         ("limit_damping", C.c_float), ("contact_iterations", C.c_int32),
         ("velocity_iterations", C.c_int32), ("fix_base", C.c_int32),
         ("env_spacing", C.c_float), ("envs_per_row", C.c_int32), ("solver_type", C.c_int32),
+        ("contact_offset", C.c_float),
     ]
 
 
@@ -226,7 +227,7 @@ PHYSX_RESOURCE_KEYS = frozenset({
 #: physx keys honoured by the solver (DESIGN.md §4 "Solver cfg"); solver_type
 #: 0 (PGS) and 1 (TGS) are both implemented, other values warn
 PHYSX_HONOURED_KEYS = frozenset({"num_position_iterations", "num_velocity_iterations", "rest_offset",
-                                 "max_depenetration_velocity"})
+                                 "max_depenetration_velocity", "contact_offset"})
 #: physx keys that cannot change a result of these tasks in PhysX either:
 #: bounce_threshold_velocity only gates restitution, and every material here
 #: (and in the reference, which sets none) has restitution 0
@@ -242,8 +243,9 @@ def unhonoured_physx_keys(physx: dict, asset_opts: dict | None = None) -> Dict[s
     params) that would change a PhysX result but not this solver's, each with
     the reason.  ``solver_type`` 0 (PGS) and 1 (TGS, the position iterations
     as sub-steps with re-formed contact targets, DESIGN.md §4 "Solver cfg")
-    are honoured, any other value is reported; ``contact_offset``: contacts
-    are speculative within the asset option ``contact_margin`` instead;
+    are honoured, any other value is reported; ``contact_offset`` is honoured
+    since round 5 (a point's normal row exists only within the offset plus
+    its free approach over the substep, ``tg_sim_params.contact_offset``);
     ``bounce_threshold_velocity`` is inert (``PHYSX_INERT_KEYS``).  Unknown
     keys are reported too."""
     ao = asset_opts or {}
@@ -254,9 +256,6 @@ def unhonoured_physx_keys(physx: dict, asset_opts: dict | None = None) -> Dict[s
         if k == "solver_type":
             if int(v) not in (0, 1):
                 out[k] = f"{v} is neither PGS (0) nor TGS (1); TGS is used"
-        elif k == "contact_offset":
-            out[k] = (f"{v} ignored; contacts are speculative within contact_margin "
-                      f"{float(ao.get('contact_margin', 0.05))}")
         else:
             out[k] = "unknown physx key, ignored"
     return out
@@ -289,6 +288,9 @@ def sim_params_from_cfg(cfg_sim: dict, asset_opts: dict | None = None, num_envs:
     sp.max_depenetration_velocity = float(physx.get("max_depenetration_velocity", 100.0))
     sp.rest_offset = float(physx.get("rest_offset", 0.001))
     sp.contact_margin = float(ao.get("contact_margin", 0.05))
+    # IsaacGym's default contact_offset is 0.02 (an asset option overrides it;
+    # <= 0 keeps every point speculative, the rounds 1-4 behaviour)
+    sp.contact_offset = float(ao.get("contact_offset", physx.get("contact_offset", 0.02)))
     sp.ground_friction = float(ao.get("ground_friction", 1.0))
     sp.baumgarte = float(ao.get("baumgarte", 0.2))
     sp.limit_stiffness = float(ao.get("limit_stiffness", 1.0))

@@ -1114,6 +1114,18 @@ template <class M> __device__ __forceinline__ bool row_normal(int k) {
 __device__ __forceinline__ float contact_target(const StepArgs &a, float phi, float dt) {
     return phi > a.rest ? -(phi - a.rest) / dt : fminf(a.baumgarte * (a.rest - phi) / dt, a.max_depen);
 }
+// physx.contact_offset (round 5): a point whose separation
+// above the rest offset is not below the contact offset plus its free
+// approach over the substep, max(0, -vn) h, has no normal row this substep --
+// its separation becomes TG_NO_ROW, whose target (-TG_NO_ROW / h) no row
+// velocity reaches, so its multiplier stays 0 in every sweep (PGS and TGS
+// sub-steps alike) and its patch's friction limit counts nothing from it.
+// vn: the point's free normal velocity (row Jacobian . contact group's free
+// velocity).  oracle/physics_ref.c collect_rows applies the same rule.
+#define TG_NO_ROW 1e30f
+__device__ __forceinline__ float contact_row_phi(const StepArgs &a, float phi, float vn, float h) {
+    return (a.coff > 0.f && !(phi - a.rest < a.coff + fmaxf(-vn, 0.f) * h)) ? TG_NO_ROW : phi;
+}
 
 }  // namespace tg
 

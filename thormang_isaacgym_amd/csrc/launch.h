@@ -62,7 +62,12 @@ int launch_par(const StepArgs &a, hipStream_t stream, const typename P::Args &pa
             return TG_ERR_HIP;
         attr_set.fetch_or(bit, std::memory_order_acq_rel);
     }
-    hipLaunchKernelGGL((step_par_kernel<M, EPBX, HF, P>), dim3((a.N + EPBX - 1) / EPBX), dim3(EPBX * M::LPE),
+#ifdef TG_GHOST_DEV   // (two real envs per wave: half the envs per workgroup)
+    constexpr int EPRX = (M::PAIR && M::LPE == 16 && M::NG >= 16) ? EPBX / 2 : EPBX;
+#else
+    constexpr int EPRX = EPBX;
+#endif
+    hipLaunchKernelGGL((step_par_kernel<M, EPBX, HF, P>), dim3((a.N + EPRX - 1) / EPRX), dim3(EPBX * M::LPE),
                        bytes, stream, a, pa);
     return 0;
 }

@@ -483,9 +483,21 @@ template <class M> __device__ __forceinline__ int dof_group(int d) {
 // trees' envs share TG_ALIAS_DEV LDS slots and the kernel is compiled for two
 // waves per SIMD, so two workgroups fit a CU -- what a per-env LDS footprint
 // half the size would buy
-#ifdef TG_ALIAS_DEV
-template <class M> constexpr int alias_slots(int epb) { return M::PAIR ? TG_ALIAS_DEV : epb; }
+// TG_GHOST_DEV (developer timing prototype, VERDICT r4 item 1, results
+// exact): the lane-pair trees run two envs per wavefront instead of four --
+// lanes 0-31 two real envs, lanes 32-63 their "ghost" twins, which compute
+// the same env on the same LDS slot and never store -- so 4096 envs are 2048
+// waves, and with half the LDS slots per workgroup and the kernel compiled
+// for two waves per SIMD two workgroups share a CU: two waves per SIMD, each
+// carrying the whole per-env chain for half the envs.  What a second wave
+// per SIMD buys when the env's work is NOT split across more lanes (the
+// 32-lane design's lower end)
+#if defined(TG_ALIAS_DEV)
+template <class M> constexpr int alias_slots(int epb) { return M::PAIR && TG_ALIAS_DEV < epb ? TG_ALIAS_DEV : epb; }
 #define TG_STEP_BOUNDS(M, EPB) __launch_bounds__(EPB * M::LPE, M::PAIR ? 2 : 1)
+#elif defined(TG_GHOST_DEV)
+template <class M> constexpr int alias_slots(int epb) { return (M::PAIR && M::NG >= 16) ? epb / 2 : epb; }
+#define TG_STEP_BOUNDS(M, EPB) __launch_bounds__(EPB * M::LPE, (M::PAIR && M::NG >= 16) ? 2 : 1)
 #else
 template <class M> constexpr int alias_slots(int epb) { return epb; }
 #define TG_STEP_BOUNDS(M, EPB) __launch_bounds__(EPB * M::LPE)
@@ -530,8 +542,18 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
     // of neighbouring chunks share 128-B lines)
     const int nb = gridDim.x;
     const int chunk = (nb % 8 == 0) ? (blockIdx.x % 8) * (nb / 8) + blockIdx.x / 8 : blockIdx.x;
+#ifdef TG_GHOST_DEV
+    // (lanes 32-63 of a wave: the ghost twins of lanes 0-31's envs)
+    constexpr bool GH = M::PAIR && LPE == 16 && M::NG >= 16;
+    constexpr int EPR = GH ? EPB / 2 : EPB;   // real envs per workgroup
+    const int lr = GH ? (le >> 2) * 2 + (le & 1) : le;
+    const int e = min(chunk * EPR + lr, a.N - 1);
+    const bool owner = (!GH || (le & 3) < 2) && chunk * EPR + lr < a.N;
+#else
+    const int lr = le;
     const int e = min(chunk * EPB + le, a.N - 1);   // tail lanes redo the last env, never store
     const bool owner = chunk * EPB + le < a.N;
+#endif
     TG_PROF_INIT
 
     // the per-block tables, copied from the model's constants.  When every
@@ -621,7 +643,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
     for (int i = tid; i < 32; i += EPB * LPE) tab[PL::T_ZERO + i] = 0;
     for (int i = tid; i < M::NCG * M::MAXD; i += EPB * LPE) tab[PL::T_CPATH + i] = M::cpath[i / M::MAXD][i % M::MAXD];
     }
-    const LE s{lds_raw + (le % alias_slots<M>(EPB)) * PL::ES};
+    const LE s{lds_raw + (lr % alias_slots<M>(EPB)) * PL::ES};
     const size_t N = a.N;
     const int D = a.D;
     const float h = a.h;
@@ -1810,8 +1832,11 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 }
                 const int ro = PL::ROW + i * 8;
                 if (kr < nr) {   // normal row kr: Jacobian about the root origin, separation
-                    stsv(s, ro, SV{cross(mulT(R, pk), dl), dl});
-                    s(ro + 6) = a.tgs ? phk : contact_target(a, phk, h);
+                    const SV J = SV{cross(mulT(R, pk), dl), dl};
+                    stsv(s, ro, J);
+                    // (contact_offset: no row beyond the offset plus the point's free approach)
+                    const float phr = contact_row_phi(a, phk, dot(J, ldsv(s, PL::CGV + 6 * cgi)), h);
+                    s(ro + 6) = a.tgs ? phr : contact_target(a, phr, h);
                     s(ro + 7) = 1.f;
                 } else {         // friction row t of the patch
                     const int t = kr - nr;
@@ -1925,9 +1950,12 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                         phi = (pos.z + pts[k].z - gz) * nk.z;
                     }
                     // row Jacobian in the root frame: (r x d, d), r = the point about the root origin
-                    stsv(s, ro, SV{cross(mulT(R, pts[k]), dl), dl});
-                    // (TGS: the separation itself, the PGS forms the sub-step targets)
-                    s(ro + 6) = a.tgs ? phi : contact_target(a, phi, h);
+                    const SV J = SV{cross(mulT(R, pts[k]), dl), dl};
+                    stsv(s, ro, J);
+                    // (TGS: the separation itself, the PGS forms the sub-step targets;
+                    // contact_offset: no row beyond the offset plus the point's free approach)
+                    const float phr = contact_row_phi(a, phi, dot(J, ldsv(s, PL::CGV + 6 * cgi)), h);
+                    s(ro + 6) = a.tgs ? phr : contact_target(a, phr, h);
                     s(ro + 7) = 1.f;
                     wk[k] = fminf(fmaxf((a.margin - phi) / a.margin, 0.f), 1.f);
                     wsum += wk[k];

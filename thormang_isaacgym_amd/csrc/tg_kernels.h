@@ -59,6 +59,7 @@ struct StepArgs {
     int substeps;
     float gx, gy, gz;
     float lin_damp, ang_damp, max_depen, rest, margin, ground_mu, baumgarte, lim_k, lim_c;
+    float coff;                    // physx.contact_offset (contact_row_phi); <= 0: every point speculative
     int iters, viters, fix_base;   // biased (position) and bias-free (velocity) PGS sweeps
     int tgs;                       // solver_type 1: position iterations as sub-steps (step_par.h PGS)
     float *root;              // [N,13]

@@ -161,6 +161,7 @@ tg::StepArgs step_args(tg_sim *s) {
     a.max_depen = p.max_depenetration_velocity;
     a.rest = p.rest_offset;
     a.margin = p.contact_margin;
+    a.coff = p.contact_offset;
     a.ground_mu = p.ground_friction;
     a.baumgarte = p.baumgarte;
     a.lim_k = p.limit_stiffness;
