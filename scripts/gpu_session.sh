@@ -1,19 +1,26 @@
 #!/bin/bash
-# Round-4 closing evidence: the full GPU test suite, the bench line of every
-# workload in DESIGN.md §5 (the default line with its cpu_baseline), the
-# driver's distributed launch form at one rank, rocprofv3 kernel statistics of
-# the three step paths, the HBM PMC passes and the SQ / LDS counter passes of
-# the two headline workloads.  Every GPU step has its own time limit; a
-# failure stops the script.
+# Closing evidence of a round on one MI355X (replaces the per-round
+# gpu_final_r2/r2b/r3/r4.sh and gpu_r2_prof/r3/r4.sh scripts): the full GPU
+# test suite, smoke(), the bench line of every workload in DESIGN.md §5 (the
+# default line with its cpu_baseline), the driver's short form and its
+# distributed launch at one rank, rocprofv3 kernel statistics of the three
+# step paths, the HBM PMC passes and the SQ / LDS counter passes of the two
+# headline workloads, and the register / scratch use of every step kernel.
+# Every GPU step has its own time limit; a failure stops the script.
+#   ROUND=5 bash scripts/gpu_session.sh            (everything, into gpurun_out/final$ROUND)
+#   SKIP_TESTS=1 SKIP_PROF=1 ... / ONLY_PROF=1     (parts; the GPU call's time limit is 20 min)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=${OUT_DIR:-gpurun_out/final4}
+ROUND=${ROUND:-5}
+OUT=${OUT_DIR:-gpurun_out/final$ROUND}
 mkdir -p $OUT
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 if [ -n "${ONLY_PROF:-}" ]; then SKIP_TESTS=1; SKIP_BENCH=1; fi
 if [ -z "${SKIP_TESTS:-}" ]; then
   timeout -k 10 700 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
   rc=$?; tail -2 $OUT/gpu_tests.log; [ $rc -le 1 ] || exit $rc
+  timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit $?
+  tail -1 $OUT/smoke.log
 fi
 if [ -z "${SKIP_BENCH:-}" ]; then
 timeout -k 10 400 python bench.py > $OUT/bench_default.log 2>&1 || exit $?

@@ -59,22 +59,20 @@ int launch_step_walk(uint64_t hash, const StepArgs &a, const WalkPostArgs &pa, h
 // the known-answer models run in this unit, the humanoid trees in
 // articulation_tree.hip -- and read back whichever unit's kernel fired (its
 // buffer's word 0 holds the row count; scripts/dev/contact_dump.py)
-namespace tg {
 int tree_dump_arm(int e, int substep);
 int tree_dump_read(float *out, int n);
-}
 extern "C" int tg_debug_dump_env(int e, int substep) {
     static float zero[4096];
-    if (hipMemcpyToSymbol(HIP_SYMBOL(tg::tg_dump_buf), zero, sizeof zero) != hipSuccess) return -2;
-    if (hipMemcpyToSymbol(HIP_SYMBOL(tg::tg_dump_sub), &substep, sizeof(int)) != hipSuccess) return -2;
-    if (hipMemcpyToSymbol(HIP_SYMBOL(tg::tg_dump_env), &e, sizeof(int)) != hipSuccess) return -2;
-    return tg::tree_dump_arm(e, substep);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(tg_dump_buf), zero, sizeof zero) != hipSuccess) return -2;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(tg_dump_sub), &substep, sizeof(int)) != hipSuccess) return -2;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(tg_dump_env), &e, sizeof(int)) != hipSuccess) return -2;
+    return tree_dump_arm(e, substep);
 }
 extern "C" int tg_debug_dump_read(float *out, int n) {
     if (n > 4096) n = 4096;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tg::tg_dump_buf), (size_t)n * 4) != hipSuccess) return -2;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tg_dump_buf), (size_t)n * 4) != hipSuccess) return -2;
     if (n > 0 && out[0] != 0.f) return 0;          // this unit's kernel dumped
-    return tg::tree_dump_read(out, n);              // else the humanoid unit's (or nothing: zeros)
+    return tree_dump_read(out, n);              // else the humanoid unit's (or nothing: zeros)
 }
 #endif
 

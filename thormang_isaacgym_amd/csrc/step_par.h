@@ -1196,13 +1196,25 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
         }
         if (lead) stsv(s, F_V, v0);
         TG_SYNC();
+#ifndef TG_PROBE
+#define TG_PROBE 0   // developer timing probes (results wrong): the tree passes' parent / child LDS traffic
+#endif               // replaced by the lane's own previous-step registers (1 pass 1a, 2 pass 2b, 4 pass 3, 8 impulse)
+        M3 pr_R = eye3();
+        V3 pr_P = v3(0, 0, 0);
+        SV pr_v = v0;
         auto body1 = [&](const I4 &dc, const float *ck) {
             const int g = dc.x;
             if (g > 0) {
                 const int o = g * GF, par = dc.y, jt = d_jt(dc);
+#if TG_PROBE & 1
+                const M3 Rp = pr_R;
+                const V3 Pp = pr_P;
+                const SV vp = pr_v;
+#else
                 const M3 Rp = ldR(s, par);
                 const V3 Pp = ldv3(s, par * GF + F_P);
                 const SV vp = ldsv(s, par * GF + F_V);
+#endif
                 const float qg = s(o + F_Q), qdg = s(o + F_QD);
                 M3 Rpc;   // child -> parent rotation at q, then the root-frame pose
 #pragma unroll
@@ -1227,6 +1239,11 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 const SV Sg = motion_Sm<M>(jt, v3(Rg.a[2], Rg.a[5], Rg.a[8]), Pg);
                 const SV vg = vp + qdg * Sg;
                 stsv(s, o + F_V, vg);
+#if TG_PROBE & 1
+                pr_R = Rg;
+                pr_P = Pg;
+                pr_v = vg;
+#endif
             }
             TG_SYNC();
         };
@@ -1466,6 +1483,9 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
         // the step index a compile-time constant (its gather width too)
         // (the children's descriptor read one step ahead, ahead of the step's own loads)
         I4 dnext = dsc(M::NSTEP - 1);
+        float p2X[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, p2B[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f},
+              p2p[3] = {0.f, 0.f, 0.f};
+        (void)p2X; (void)p2B; (void)p2p;
         static_for<0, M::NSTEP>([&](auto TT) {
             constexpr int t = M::NSTEP - 1 - decltype(TT)::value;
             const I4 dc = dnext;   // (children for the gather)
@@ -1514,7 +1534,17 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     }
                 };
                 constexpr int smax = step_smax<M>(t);
+#if TG_PROBE & 2
+                (void)gather2;
+#pragma unroll
+                for (int k = 0; k < 6; ++k) X[k] += p2X[k];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) Bm[k] += p2B[k];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) ph[k] += p2p[k];
+#else
                 if constexpr (smax >= 1) gather2(IntC<(smax < 3 ? smax : 3)>{});
+#endif
                 // the half's orientation of B
                 float Y[9];
                 Y[0] = Bm[0]; Y[4] = Bm[4]; Y[8] = Bm[8];
@@ -1553,6 +1583,13 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 s(o + F_DINV) = Dinv;
                 s(o + F_UU) = u;
                 // contribution to the parent (same frame: no transform)
+#if TG_PROBE & 2
+#pragma unroll
+                for (int k = 0; k < 6; ++k) p2X[k] = X[k];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) p2B[k] = Y[k];
+                p2p[0] = pav.x; p2p[1] = pav.y; p2p[2] = pav.z;
+#else
 #pragma unroll
                 for (int k = 0; k < 6; ++k) s(ia_c(g) + 15 * hh + k) = X[k];
                 if (!hb) {
@@ -1560,6 +1597,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     for (int k = 0; k < 9; ++k) s(ia_c(g) + 6 + k) = Y[k];
                 }
                 stv3(s, pa_c(g) + 3 * hh, pav);
+#endif
             }
             TG_SYNC();
         });
@@ -1641,6 +1679,8 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
         };
         I4 dr[2];
         Own ow[2];
+        SV pr3 = a0;
+        (void)pr3;
         dr[0] = pdsc3(0);
         ow[0] = ld_own(dr[0]);
 #pragma unroll
@@ -1648,7 +1688,11 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             const I4 dc = dr[t % 2];
             const Own &w = ow[t % 2];
             const int g = dc.x;
+#if TG_PROBE & 4
+            const SV apar = pr3;
+#else
             const SV apar = ldsv(s, ac_s(max(dc.y, 0)));
+#endif
             if (t + 1 < M::NSTEP) {
                 dr[(t + 1) % 2] = pdsc3(t + 1);
                 ow[(t + 1) % 2] = ld_own(dr[(t + 1) % 2]);
@@ -1657,7 +1701,11 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 const int o = g * GF;
                 const SV ap = apar + w.cb;   // cb: pass 2a
                 const float qdd = (w.uu - dot(w.U, ap)) * w.dinv;
+#if TG_PROBE & 4
+                pr3 = ap + qdd * w.S;
+#else
                 stsv(s, ac_s(g), ap + qdd * w.S);
+#endif
                 s(o + F_QDS) = w.qd + h * qdd;
                 if (cp == 0) {
                     s(o + F_UU) = qdd;
@@ -2490,6 +2538,8 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 };
                 I4 dr[2];
                 OwnI ow[2];
+                SV pri = da0, priv = da0v;
+                (void)pri; (void)priv;
                 dr[0] = pdsc4(0);
                 ow[0] = ld_own(dr[0]);
 #pragma unroll
@@ -2498,8 +2548,13 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     const OwnI &w = ow[t % 2];
                     const int g = dc.x;
                     const int op = max(dc.y, 0) * GF;
+#if TG_PROBE & 8
+                    const SV ap = pri, av = priv;
+                    (void)op;
+#else
                     const SV ap = ldsv(s, op + F_PA);
                     const SV av = vit ? ldsv(s, op + F_V) : sv0();
+#endif
                     if (t + 1 < M::NSTEP) {
                         dr[(t + 1) % 2] = pdsc4(t + 1);
                         ow[(t + 1) % 2] = ld_own(dr[(t + 1) % 2]);
@@ -2507,11 +2562,19 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     if (g > 0) {
                         const int o = g * GF;
                         const float x = (w.uu - dot(w.U, ap)) * w.dinv;
+#if TG_PROBE & 8
+                        pri = ap + x * w.S;
+#else
                         stsv(s, o + F_PA, ap + x * w.S);
+#endif
                         s(o + F_QDS) = w.qds + x;
                         if (vit) {
                             const float xv = (w.uv - dot(w.U, av)) * w.dinv;
+#if TG_PROBE & 8
+                            priv = av + xv * w.S;
+#else
                             stsv(s, o + F_V, av + xv * w.S);
+#endif
                             s(o + F_QD) = w.qds + xv;
                         }
                     }
