@@ -25,10 +25,16 @@ import torch  # noqa: E402
 sys.path.insert(0, ".")
 import thormang_isaacgym_amd as tia  # noqa: E402
 
+from thormang_isaacgym_amd.cfg import load_task_cfg  # noqa: E402
+
 out = {}
 for task, n, na in (("ThormangWalk", 1024, 33), ("ThormangWalkDR", 1024, 33), ("Gogoro", 1024, 1),
-                    ("GogoroPaper", 1024, 1)):
-    env = tia.make(seed=3, task=task, num_envs=n, sim_device="cuda:0", rl_device="cuda:0")
+                    ("GogoroPaper", 1024, 1), ("ThormangWalk+wb", 1024, 33)):
+    name, _, var = task.partition("+")
+    cfg = load_task_cfg(name, num_envs=n)
+    if var == "wb":   # the whole-body contact model (thormang_wb)
+        cfg["env"]["asset"] = dict(cfg["env"].get("asset", {}), wholeBodyCollision=True)
+    env = tia.make(seed=3, task=name, num_envs=n, sim_device="cuda:0", rl_device="cuda:0", cfg=cfg)
     g = torch.Generator(device="cuda:0").manual_seed(9)
     for _ in range(100):
         obs, rew, reset, extras = env.step(torch.rand(n, na, device="cuda:0", generator=g) * 2 - 1)

@@ -234,9 +234,82 @@ template <class M> __device__ __forceinline__ GInfo ginfo(const int *gi, int g) 
     return GInfo{p[GI_PARENT], p[GI_DOF], p[GI_JT]};
 }
 
+// Chain schedule (round 5; TG_CHAIN, the humanoid-size lane-pair trees): one
+// schedule slot per root-to-leaf chain of the group tree -- slot s runs, at
+// step t, the group at depth t + 1 on the path from the root to its leaf --
+// so in every tree pass a group's parent (forward passes) or first child
+// (pass 2b) was computed by the same lane one step earlier and its values
+// are still in that lane's registers: pass 1a, pass 3 and the impulse
+// top-down pass read no parent pose / velocity / acceleration from LDS and
+// store none of the last two, and pass 2b gathers from LDS only the children
+// after the first (the chains that branch off).  A group shared by several
+// chains (the chest, the wrists) is computed by each of their slots in the
+// forward passes (identical values) and stored by its OWNER, the slot of its
+// first-child chain; pass 2b runs each group on its owner only, which keeps
+// the children's summation order (own + child 0 + child 1 + ...), so every
+// result is bit-identical to the list schedule's.  Leaves are the slots
+// (Thormang: 7 of 8), in depth-first order, children in child-list order.
+#ifndef TG_CHAIN
+#define TG_CHAIN 1   // developer switch: 0 = the list schedule for every tree (A/B)
+#endif
+template <class M> struct Chain {
+    struct Tab {
+        int g[M::NSTEP][M::SL];             // group at (step, slot), -1 idle
+        unsigned char own[M::NSTEP][M::SL]; // the slot owns that group
+        unsigned char st[M::NG];            // pass 2b stores the group's contribution (its parent is another slot's or the root)
+        int nleaf, depth;
+    };
+    static constexpr Tab make() {
+        Tab x{};
+        int leaf[M::NG > 0 ? M::NG : 1] = {}, stack[M::NG > 0 ? M::NG : 1] = {};
+        int sp = 0, nl = 0;
+        stack[sp++] = 0;
+        while (sp > 0) {   // depth-first, children in child-list order
+            const int g = stack[--sp];
+            if (g != 0 && M::nchild[g] == 0) leaf[nl++] = g;
+            for (int c = M::nchild[g] - 1; c >= 0; --c) stack[sp++] = M::child[g][c];
+        }
+        x.nleaf = nl;
+        for (int t = 0; t < M::NSTEP; ++t)
+            for (int s = 0; s < M::SL; ++s) x.g[t][s] = -1;
+        if (nl > M::SL) return x;
+        int owner[M::NG > 0 ? M::NG : 1] = {};
+        for (int g = 0; g < M::NG; ++g) owner[g] = -1;
+        for (int s = 0; s < nl; ++s) owner[leaf[s]] = s;
+        for (int g = M::NG - 1; g >= 1; --g)   // parents precede children (topological numbering)
+            if (M::nchild[g] > 0) owner[g] = owner[M::child[g][0]];
+        for (int s = 0; s < nl; ++s) {
+            int path[M::NG > 0 ? M::NG : 1] = {}, n = 0;
+            for (int g = leaf[s]; g > 0; g = M::parent[g]) path[n++] = g;
+            if (n > x.depth) x.depth = n;
+            if (n > M::NSTEP) return x;
+            for (int t = 0; t < n; ++t) {
+                const int g = path[n - 1 - t];
+                x.g[t][s] = g;
+                x.own[t][s] = owner[g] == s ? 1 : 0;
+            }
+        }
+        for (int g = 1; g < M::NG; ++g) x.st[g] = (M::parent[g] == 0 || owner[M::parent[g]] != owner[g]) ? 1 : 0;
+        return x;
+    }
+    static constexpr Tab tab = make();
+    static constexpr bool ON = TG_CHAIN && M::PAIR && M::NG >= 16 && M::NG <= 128 && tab.nleaf <= M::SL &&
+                               tab.depth <= M::NSTEP;
+};
+// the group (step t, slot) runs (chain: only its owner counts, for the gather widths)
+template <class M> constexpr int sched_at(int t, int slot) {
+    if constexpr (Chain<M>::ON) return Chain<M>::tab.g[t][slot];
+    else return M::sched[t][slot];
+}
+template <class M> constexpr bool sched_own(int t, int slot) {
+    if constexpr (Chain<M>::ON) return Chain<M>::tab.own[t][slot] != 0;
+    else return M::sched[t][slot] > 0;
+}
+
 // Schedule descriptor of (step t, lane): everything a lane needs about the
 // group it handles, in one ds_read_b128 (prefetched a step ahead):
-//   x = group (0: idle), y = parent, z = dof | jt << 16,
+//   x = group (0: idle), y = parent, z = dof | jt << 16 | own << 24 | st << 25
+//   (chain schedule: the lane owns the group; pass 2b stores its contribution),
 //   w = nch | smax << 4 | child_c << (8 + 8c)  (smax: the step's max nch over lanes)
 struct alignas(16) I4 {
     int x, y, z, w;
@@ -244,21 +317,23 @@ struct alignas(16) I4 {
 template <class M> constexpr I4 step_desc(int t, int lane) {
     // lane pairs (M::PAIR): lanes sub and sub + SL run schedule slot sub
     const int slot = lane % M::SL;
-    const int g = (lane < M::SL || M::PAIR) ? M::sched[t][slot] : -1;
+    const int g = (lane < M::SL || M::PAIR) ? sched_at<M>(t, slot) : -1;
     if (g <= 0) return I4{0, 0, 0, 0};
     int smax = 0;
     for (int l = 0; l < M::SL; ++l)
-        if (M::sched[t][l] > 0 && M::nchild[M::sched[t][l]] > smax) smax = M::nchild[M::sched[t][l]];
+        if (sched_own<M>(t, l) && M::nchild[sched_at<M>(t, l)] > smax) smax = M::nchild[sched_at<M>(t, l)];
     int w = M::nchild[g] | smax << 4;
     for (int c = 0; c < M::nchild[g]; ++c) w |= M::child[g][c] << (8 + 8 * c);
-    return I4{g, M::parent[g], M::gdof[g] | M::jtype[g] << 16, w};
+    int z = M::gdof[g] | M::jtype[g] << 16;
+    if constexpr (Chain<M>::ON) z |= (sched_own<M>(t, slot) ? 1 : 0) << 24 | Chain<M>::tab.st[g] << 25;
+    return I4{g, M::parent[g], z, w};
 }
 // the largest child count among schedule step t's groups (the gather width
 // of pass 2b at that step, a compile-time constant)
 template <class M> constexpr int step_smax(int t) {
     int m = 0;
     for (int l = 0; l < M::SL; ++l)
-        if (M::sched[t][l] > 0 && M::nchild[M::sched[t][l]] > m) m = M::nchild[M::sched[t][l]];
+        if (sched_own<M>(t, l) && M::nchild[sched_at<M>(t, l)] > m) m = M::nchild[sched_at<M>(t, l)];
     return m;
 }
 template <class M> constexpr int max_nonroot_children() {
@@ -299,8 +374,10 @@ template <class M> struct PackTab {
                     const int t = 2 * w + k;
                     if (t >= M::NSTEP) break;
                     const I4 d = step_desc<M>(t, lane);
-                    const int jp = (d.z >> 16) == TG_JOINT_PRISMATIC ? 1 : 0;
-                    x |= ((d.x & 127) | jp << 7 | (d.y & 255) << 8) << (16 * k);
+                    const int jp = ((d.z >> 16) & 255) == TG_JOINT_PRISMATIC ? 1 : 0;
+                    // (chain schedule: bit 15 the owner flag, the parent in bits 8-14)
+                    const int py = Chain<M>::ON ? ((d.y & 127) | ((d.z >> 24) & 1) << 7) : (d.y & 255);
+                    x |= ((d.x & 127) | jp << 7 | py << 8) << (16 * k);
                 }
                 a.v[w * M::LPE + lane] = x;
             }
@@ -309,7 +386,9 @@ template <class M> struct PackTab {
     static constexpr Arr tab = make();
 };
 __device__ __forceinline__ int d_dof(const I4 &d) { return d.z & 0xFFFF; }
-__device__ __forceinline__ int d_jt(const I4 &d) { return d.z >> 16; }
+__device__ __forceinline__ int d_jt(const I4 &d) { return (d.z >> 16) & 255; }
+__device__ __forceinline__ bool d_own(const I4 &d) { return (d.z >> 24) & 1; }
+__device__ __forceinline__ bool d_store(const I4 &d) { return (d.z >> 25) & 1; }
 __device__ __forceinline__ int d_nch(const I4 &d) { return d.w & 15; }
 __device__ __forceinline__ int d_smax(const I4 &d) { return (d.w >> 4) & 15; }
 __device__ __forceinline__ int d_child(const I4 &d, int c) { return (d.w >> (8 + 8 * c)) & 255; }
@@ -764,8 +843,11 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             int wv = pkw[t / 2];
             __asm__ volatile("" : "+v"(wv));
             const int v = (wv >> (16 * (t % 2))) & 0xFFFF;
-            return I4{bounded(v & 127, 0, M::NG), bounded(v >> 8, 0, M::NG),
-                      ((v >> 7) & 1 ? TG_JOINT_PRISMATIC : TG_JOINT_REVOLUTE) << 16, 0};
+            const int jz = ((v >> 7) & 1 ? TG_JOINT_PRISMATIC : TG_JOINT_REVOLUTE) << 16;
+            if constexpr (Chain<M>::ON)   // (bit 15: the lane owns the group)
+                return I4{bounded(v & 127, 0, M::NG), bounded((v >> 8) & 127, 0, M::NG), jz | ((v >> 15) & 1) << 24, 0};
+            else
+                return I4{bounded(v & 127, 0, M::NG), bounded(v >> 8, 0, M::NG), jz, 0};
         } else {
             return dsc(t);
         }
@@ -1199,6 +1281,10 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
 #ifndef TG_PROBE
 #define TG_PROBE 0   // developer timing probes (results wrong): the tree passes' parent / child LDS traffic
 #endif               // replaced by the lane's own previous-step registers (1 pass 1a, 2 pass 2b, 4 pass 3, 8 impulse)
+        // (chain schedule: the parent's pose and velocity are the lane's own
+        // previous step's, the root's at step 0)
+        constexpr bool CH = Chain<M>::ON;
+        constexpr bool CH1 = CH || (TG_PROBE & 1);
         M3 pr_R = eye3();
         V3 pr_P = v3(0, 0, 0);
         SV pr_v = v0;
@@ -1206,15 +1292,18 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             const int g = dc.x;
             if (g > 0) {
                 const int o = g * GF, par = dc.y, jt = d_jt(dc);
-#if TG_PROBE & 1
-                const M3 Rp = pr_R;
-                const V3 Pp = pr_P;
-                const SV vp = pr_v;
-#else
-                const M3 Rp = ldR(s, par);
-                const V3 Pp = ldv3(s, par * GF + F_P);
-                const SV vp = ldsv(s, par * GF + F_V);
-#endif
+                M3 Rp;
+                V3 Pp;
+                SV vp;
+                if constexpr (CH1) {
+                    Rp = pr_R;
+                    Pp = pr_P;
+                    vp = pr_v;
+                } else {
+                    Rp = ldR(s, par);
+                    Pp = ldv3(s, par * GF + F_P);
+                    vp = ldsv(s, par * GF + F_V);
+                }
                 const float qg = s(o + F_Q), qdg = s(o + F_QD);
                 M3 Rpc;   // child -> parent rotation at q, then the root-frame pose
 #pragma unroll
@@ -1234,16 +1323,18 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 }
                 const M3 Rg = mul(Rp, Rpc);
                 const V3 Pg = Pp + mul(Rp, tr);
-                stR(s, g, Rg);
-                stv3(s, o + F_P, Pg);
                 const SV Sg = motion_Sm<M>(jt, v3(Rg.a[2], Rg.a[5], Rg.a[8]), Pg);
                 const SV vg = vp + qdg * Sg;
-                stsv(s, o + F_V, vg);
-#if TG_PROBE & 1
-                pr_R = Rg;
-                pr_P = Pg;
-                pr_v = vg;
-#endif
+                if (!CH || d_own(dc)) {   // (chain: the group's owner stores it)
+                    stR(s, g, Rg);
+                    stv3(s, o + F_P, Pg);
+                    stsv(s, o + F_V, vg);
+                }
+                if constexpr (CH1) {
+                    pr_R = Rg;
+                    pr_P = Pg;
+                    pr_v = vg;
+                }
             }
             TG_SYNC();
         };
@@ -1492,7 +1583,11 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             if constexpr (t > 0) dnext = dsc(t - 1);
             const I4 pc = pdsc2(t);  // own group from registers: its loads need not wait for dc
             const int g = pc.x;
-            if (g > 0) {
+            // (chain schedule: each group on its owner lane only; the first
+            // child's contribution is in this lane's registers from the step
+            // before, zeros for a leaf)
+            constexpr bool CH2 = Chain<M>::ON;
+            if (g > 0 && (!CH2 || d_own(pc))) {
                 const int o = g * GF;
                 float X[6], Bm[9], ph[3], cb1[3], cb2[3];
 #pragma unroll
@@ -1508,11 +1603,11 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 const SV Sg = ldSm<M>(s, g, d_jt(pc));
                 const float c0 = s(o + F_DINV), tau = s(o + F_UU), al = s(o + F_QDS), c1 = s(o + F_C1);
                 // children: every load issued before the first add (absent children read the zero block)
-                auto gather2 = [&](auto NCc) {
-                    constexpr int n = decltype(NCc)::value;
+                auto gather2 = [&](auto NCc, auto C0c) {
+                    constexpr int n = decltype(NCc)::value, c0 = decltype(C0c)::value;
                     float cx[n][6], cbm[n][9], cp[n][3];
 #pragma unroll
-                    for (int c = 0; c < n; ++c) {
+                    for (int c = c0; c < n; ++c) {
                         const bool has = c < d_nch(dc);
                         const int ch = d_child(dc, c);
                         const float *pi = has ? s.b + ia_c(ch) : zeros, *pp = has ? s.b + pa_c(ch) : zeros;
@@ -1524,7 +1619,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                         for (int k = 0; k < 3; ++k) cp[c][k] = pp[3 * hh + k];
                     }
 #pragma unroll
-                    for (int c = 0; c < n; ++c) {
+                    for (int c = c0; c < n; ++c) {
 #pragma unroll
                         for (int k = 0; k < 6; ++k) X[k] += cx[c][k];
 #pragma unroll
@@ -1534,17 +1629,19 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     }
                 };
                 constexpr int smax = step_smax<M>(t);
-#if TG_PROBE & 2
-                (void)gather2;
+                if constexpr (CH2 || (TG_PROBE & 2)) {
+                    // the first child from registers, then the children after it
+                    // (other chains' heads) from LDS -- the list schedule's order
 #pragma unroll
-                for (int k = 0; k < 6; ++k) X[k] += p2X[k];
+                    for (int k = 0; k < 6; ++k) X[k] += p2X[k];
 #pragma unroll
-                for (int k = 0; k < 9; ++k) Bm[k] += p2B[k];
+                    for (int k = 0; k < 9; ++k) Bm[k] += p2B[k];
 #pragma unroll
-                for (int k = 0; k < 3; ++k) ph[k] += p2p[k];
-#else
-                if constexpr (smax >= 1) gather2(IntC<(smax < 3 ? smax : 3)>{});
-#endif
+                    for (int k = 0; k < 3; ++k) ph[k] += p2p[k];
+                    if constexpr (CH2 && smax >= 2) gather2(IntC<(smax < 3 ? smax : 3)>{}, IntC<1>{});
+                } else {
+                    if constexpr (smax >= 1) gather2(IntC<(smax < 3 ? smax : 3)>{}, IntC<0>{});
+                }
                 // the half's orientation of B
                 float Y[9];
                 Y[0] = Bm[0]; Y[4] = Bm[4]; Y[8] = Bm[8];
@@ -1582,22 +1679,28 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 stv3(s, o + F_U + 3 * hh, Uv);
                 s(o + F_DINV) = Dinv;
                 s(o + F_UU) = u;
-                // contribution to the parent (same frame: no transform)
-#if TG_PROBE & 2
+                // contribution to the parent (same frame: no transform); chain
+                // schedule: into this lane's registers for the parent (B in its
+                // canonical orientation: half 1 holds its transpose, bitwise),
+                // and to LDS only when the parent is another lane's or the root
+                if constexpr (CH2 || (TG_PROBE & 2)) {
 #pragma unroll
-                for (int k = 0; k < 6; ++k) p2X[k] = X[k];
+                    for (int k = 0; k < 6; ++k) p2X[k] = X[k];
 #pragma unroll
-                for (int k = 0; k < 9; ++k) p2B[k] = Y[k];
-                p2p[0] = pav.x; p2p[1] = pav.y; p2p[2] = pav.z;
-#else
+                    for (int i = 0; i < 3; ++i)
 #pragma unroll
-                for (int k = 0; k < 6; ++k) s(ia_c(g) + 15 * hh + k) = X[k];
-                if (!hb) {
-#pragma unroll
-                    for (int k = 0; k < 9; ++k) s(ia_c(g) + 6 + k) = Y[k];
+                        for (int j = 0; j < 3; ++j) p2B[3 * i + j] = hb ? Y[3 * j + i] : Y[3 * i + j];
+                    p2p[0] = pav.x; p2p[1] = pav.y; p2p[2] = pav.z;
                 }
-                stv3(s, pa_c(g) + 3 * hh, pav);
-#endif
+                if (!(CH2 || (TG_PROBE & 2)) || (CH2 && d_store(dc))) {
+#pragma unroll
+                    for (int k = 0; k < 6; ++k) s(ia_c(g) + 15 * hh + k) = X[k];
+                    if (!hb) {
+#pragma unroll
+                        for (int k = 0; k < 9; ++k) s(ia_c(g) + 6 + k) = Y[k];
+                    }
+                    stv3(s, pa_c(g) + 3 * hh, pav);
+                }
             }
             TG_SYNC();
         });
@@ -1688,11 +1791,11 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             const I4 dc = dr[t % 2];
             const Own &w = ow[t % 2];
             const int g = dc.x;
-#if TG_PROBE & 4
-            const SV apar = pr3;
-#else
-            const SV apar = ldsv(s, ac_s(max(dc.y, 0)));
-#endif
+            // (chain schedule: the parent's acceleration is the lane's previous step's)
+            constexpr bool CH3 = Chain<M>::ON || (TG_PROBE & 4);
+            SV apar;
+            if constexpr (CH3) apar = pr3;
+            else apar = ldsv(s, ac_s(max(dc.y, 0)));
             if (t + 1 < M::NSTEP) {
                 dr[(t + 1) % 2] = pdsc3(t + 1);
                 ow[(t + 1) % 2] = ld_own(dr[(t + 1) % 2]);
@@ -1701,19 +1804,18 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 const int o = g * GF;
                 const SV ap = apar + w.cb;   // cb: pass 2a
                 const float qdd = (w.uu - dot(w.U, ap)) * w.dinv;
-#if TG_PROBE & 4
-                pr3 = ap + qdd * w.S;
-#else
-                stsv(s, ac_s(g), ap + qdd * w.S);
-#endif
-                s(o + F_QDS) = w.qd + h * qdd;
-                if (cp == 0) {
-                    s(o + F_UU) = qdd;
-                    const float ti = w.te - w.K * qdd;
-                    const bool sat = w.K >= 0.f && fabsf(ti) > w.eff;
-                    if (sat) s(PL::FLG) = 1.f;
-                    // (Woodbury: the drive's clamp side, F_C1 being dead after pass 2b)
-                    if constexpr (PL::WOOD) s(o + F_C1) = sat ? (ti > 0.f ? 1.f : -1.f) : 0.f;
+                if constexpr (CH3) pr3 = ap + qdd * w.S;
+                else stsv(s, ac_s(g), ap + qdd * w.S);
+                if (!Chain<M>::ON || d_own(dc)) {   // (chain: the group's owner stores it)
+                    s(o + F_QDS) = w.qd + h * qdd;
+                    if (cp == 0) {
+                        s(o + F_UU) = qdd;
+                        const float ti = w.te - w.K * qdd;
+                        const bool sat = w.K >= 0.f && fabsf(ti) > w.eff;
+                        if (sat) s(PL::FLG) = 1.f;
+                        // (Woodbury: the drive's clamp side, F_C1 being dead after pass 2b)
+                        if constexpr (PL::WOOD) s(o + F_C1) = sat ? (ti > 0.f ? 1.f : -1.f) : 0.f;
+                    }
                 }
             }
             TG_SYNC();
@@ -2548,13 +2650,17 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     const OwnI &w = ow[t % 2];
                     const int g = dc.x;
                     const int op = max(dc.y, 0) * GF;
-#if TG_PROBE & 8
-                    const SV ap = pri, av = priv;
-                    (void)op;
-#else
-                    const SV ap = ldsv(s, op + F_PA);
-                    const SV av = vit ? ldsv(s, op + F_V) : sv0();
-#endif
+                    // (chain schedule: the parent's responses are the lane's previous step's)
+                    constexpr bool CHI = Chain<M>::ON || (TG_PROBE & 8);
+                    SV ap, av;
+                    if constexpr (CHI) {
+                        ap = pri;
+                        av = priv;
+                        (void)op;
+                    } else {
+                        ap = ldsv(s, op + F_PA);
+                        av = vit ? ldsv(s, op + F_V) : sv0();
+                    }
                     if (t + 1 < M::NSTEP) {
                         dr[(t + 1) % 2] = pdsc4(t + 1);
                         ow[(t + 1) % 2] = ld_own(dr[(t + 1) % 2]);
@@ -2562,20 +2668,15 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     if (g > 0) {
                         const int o = g * GF;
                         const float x = (w.uu - dot(w.U, ap)) * w.dinv;
-#if TG_PROBE & 8
-                        pri = ap + x * w.S;
-#else
-                        stsv(s, o + F_PA, ap + x * w.S);
-#endif
-                        s(o + F_QDS) = w.qds + x;
+                        const bool ow = !Chain<M>::ON || d_own(dc);   // (chain: the group's owner stores it)
+                        if constexpr (CHI) pri = ap + x * w.S;
+                        else stsv(s, o + F_PA, ap + x * w.S);
+                        if (ow) s(o + F_QDS) = w.qds + x;
                         if (vit) {
                             const float xv = (w.uv - dot(w.U, av)) * w.dinv;
-#if TG_PROBE & 8
-                            priv = av + xv * w.S;
-#else
-                            stsv(s, o + F_V, av + xv * w.S);
-#endif
-                            s(o + F_QD) = w.qds + xv;
+                            if constexpr (CHI) priv = av + xv * w.S;
+                            else stsv(s, o + F_V, av + xv * w.S);
+                            if (ow) s(o + F_QD) = w.qds + xv;
                         }
                     }
                     TG_SYNC();
