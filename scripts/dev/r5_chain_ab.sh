@@ -11,9 +11,13 @@ L=thormang_isaacgym_amd
 timeout -k 10 300 python scripts/dev/bitcmp_libs.py run $OUT/chain.npz > $OUT/bit_chain.log 2>&1 || { tail -5 $OUT/bit_chain.log; exit 1; }
 TG_LIB_PATH=$L/libtgsim_list.so timeout -k 10 300 python scripts/dev/bitcmp_libs.py run $OUT/list.npz > $OUT/bit_list.log 2>&1 || { tail -5 $OUT/bit_list.log; exit 1; }
 python scripts/dev/bitcmp_libs.py cmp $OUT/chain.npz $OUT/list.npz | tee $OUT/bitcmp.txt
+if [ -f $L/libtgsim_nosync.so ]; then
+  TG_LIB_PATH=$L/libtgsim_nosync.so timeout -k 10 300 python scripts/dev/bitcmp_libs.py run $OUT/nosync.npz > $OUT/bit_nosync.log 2>&1 || { tail -5 $OUT/bit_nosync.log; exit 1; }
+  python scripts/dev/bitcmp_libs.py cmp $OUT/nosync.npz $OUT/list.npz | tee $OUT/bitcmp_nosync.txt
+fi
 for r in 1 2; do
   for t in ThormangWalk Gogoro; do
-    for v in chain:libtgsim.so list:libtgsim_list.so; do
+    for v in chain:libtgsim.so list:libtgsim_list.so nosync:libtgsim_nosync.so; do
       n=${v%%:*}; lib=${v#*:}
       TG_LIB_PATH=$L/$lib timeout -k 10 200 python bench.py --task $t --no-cpu-baseline > $OUT/${t}_${n}_r$r.log 2>&1 \
         || { echo "$t $n failed"; tail -5 $OUT/${t}_${n}_r$r.log; exit 1; }

@@ -252,6 +252,13 @@ template <class M> __device__ __forceinline__ GInfo ginfo(const int *gi, int g) 
 #ifndef TG_CHAIN
 #define TG_CHAIN 1   // developer switch: 0 = the list schedule for every tree (A/B)
 #endif
+// chain schedule: the forward passes have no LDS dependence between their
+// steps, pass 2b only where a group gathers another chain's head; 0 = a
+// wave-scope sync only there (and after each pass), 1 = after every step
+#ifndef TG_CHAIN_SYNC
+#define TG_CHAIN_SYNC 1
+#endif
+
 template <class M> struct Chain {
     struct Tab {
         int g[M::NSTEP][M::SL];             // group at (step, slot), -1 idle
@@ -336,6 +343,9 @@ template <class M> constexpr int step_smax(int t) {
         if (sched_own<M>(t, l) && M::nchild[sched_at<M>(t, l)] > m) m = M::nchild[sched_at<M>(t, l)];
     return m;
 }
+// pass 2b's step t gathers from LDS under the chain schedule (a group with
+// children after its first)
+template <class M> constexpr bool step_gathers(int t) { return step_smax<M>(t) >= 2; }
 template <class M> constexpr int max_nonroot_children() {
     int m = 0;
     for (int g = 1; g < M::NG; ++g) m = M::nchild[g] > m ? M::nchild[g] : m;
@@ -1336,7 +1346,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     pr_v = vg;
                 }
             }
-            TG_SYNC();
+            if constexpr (!CH || TG_CHAIN_SYNC) TG_SYNC();
         };
         // fully unrolled, inputs two steps ahead in a 3-deep ring (renamed
         // registers, no copies: the wait for step t's inputs leaves steps
@@ -1362,6 +1372,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             body1(dr[t % 3], kr[t % 3]);
         }
         }
+        if constexpr (CH && !TG_CHAIN_SYNC) TG_SYNC();   // (pass 1b reads every group's pose)
 #ifdef TG_DUMMY_STEPS
         // developer ablation: TG_DUMMY_STEPS dependent LDS round trips with no
         // arithmetic (kind 0: one float; kind 1: pass 1a's traffic, 18 floats
@@ -1702,7 +1713,10 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     stv3(s, pa_c(g) + 3 * hh, pav);
                 }
             }
-            TG_SYNC();
+            // (chain schedule: a sync where the next step gathers another chain's
+            // head, and after the last step -- the root gathers its children)
+            if constexpr (!CH2 || TG_CHAIN_SYNC || t == 0) TG_SYNC();
+            else if constexpr (step_gathers<M>(t - 1)) TG_SYNC();
         });
         } else {
         // unrolled (round 2: Gogoro 8.27e7 -> 8.36e7, GogoroPaper 8.55e7 -> 8.64e7, A/B twice)
@@ -1818,8 +1832,9 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     }
                 }
             }
-            TG_SYNC();
+            if constexpr (!Chain<M>::ON || TG_CHAIN_SYNC) TG_SYNC();
         }
+        if constexpr (Chain<M>::ON && !TG_CHAIN_SYNC) TG_SYNC();   // (the flag and F_QDS are read below)
         }
         if constexpr (PL::WOOD) {
             if (cp == 0 && s(PL::FLG) != 0.f && wood_update()) break;   // else the rerun below
@@ -2679,8 +2694,9 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                             if (ow) s(o + F_QD) = w.qds + xv;
                         }
                     }
-                    TG_SYNC();
+                    if constexpr (!Chain<M>::ON || TG_CHAIN_SYNC) TG_SYNC();
                 }
+                if constexpr (Chain<M>::ON && !TG_CHAIN_SYNC) TG_SYNC();
             } else {
                 // bottom-up gather, root solve, top-down -- once per multiplier
                 // set: with velocity iterations first the bias-free one (its
