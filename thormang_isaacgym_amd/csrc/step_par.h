@@ -258,6 +258,19 @@ template <class M> __device__ __forceinline__ GInfo ginfo(const int *gi, int g) 
 #ifndef TG_CHAIN_SYNC
 #define TG_CHAIN_SYNC 1
 #endif
+// the passes that use the chain registers (1 pass 1a, 2 pass 2b, 4 pass 3,
+// 8 the impulse top-down pass); the others run their list-schedule form over
+// the chain schedule (duplicates then load and store like owners: the same
+// values).  7 by default: those three are bit-identical to the list schedule
+// (scripts/dev/r5_chain_mask.sh, profiles/r5/chain_mask.txt); the impulse
+// pass's chain form rounds apart from it at the 1e-5 level in a step
+// (unexplained: the values it forwards are the ones the list form stores)
+#ifndef TG_CHAIN_MASK
+#define TG_CHAIN_MASK 7
+#endif
+#ifndef TG_CH8_DBG
+#define TG_CH8_DBG 0
+#endif
 
 template <class M> struct Chain {
     struct Tab {
@@ -1293,7 +1306,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
 #endif               // replaced by the lane's own previous-step registers (1 pass 1a, 2 pass 2b, 4 pass 3, 8 impulse)
         // (chain schedule: the parent's pose and velocity are the lane's own
         // previous step's, the root's at step 0)
-        constexpr bool CH = Chain<M>::ON;
+        constexpr bool CH = Chain<M>::ON && (TG_CHAIN_MASK & 1);
         constexpr bool CH1 = CH || (TG_PROBE & 1);
         M3 pr_R = eye3();
         V3 pr_P = v3(0, 0, 0);
@@ -1597,7 +1610,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             // (chain schedule: each group on its owner lane only; the first
             // child's contribution is in this lane's registers from the step
             // before, zeros for a leaf)
-            constexpr bool CH2 = Chain<M>::ON;
+            constexpr bool CH2 = Chain<M>::ON && (TG_CHAIN_MASK & 2);
             if (g > 0 && (!CH2 || d_own(pc))) {
                 const int o = g * GF;
                 float X[6], Bm[9], ph[3], cb1[3], cb2[3];
@@ -1642,13 +1655,19 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 constexpr int smax = step_smax<M>(t);
                 if constexpr (CH2 || (TG_PROBE & 2)) {
                     // the first child from registers, then the children after it
-                    // (other chains' heads) from LDS -- the list schedule's order
+                    // (other chains' heads) from LDS -- the list schedule's order;
+                    // a leaf adds nothing (not even the zeros its registers hold:
+                    // x + 0 is not x for x = -0 and denormals under the fast-math
+                    // unit's flushing, and the chain form would then round apart
+                    // from the list schedule's, measured)
+                    if (d_nch(dc) > 0) {
 #pragma unroll
-                    for (int k = 0; k < 6; ++k) X[k] += p2X[k];
+                        for (int k = 0; k < 6; ++k) X[k] += p2X[k];
 #pragma unroll
-                    for (int k = 0; k < 9; ++k) Bm[k] += p2B[k];
+                        for (int k = 0; k < 9; ++k) Bm[k] += p2B[k];
 #pragma unroll
-                    for (int k = 0; k < 3; ++k) ph[k] += p2p[k];
+                        for (int k = 0; k < 3; ++k) ph[k] += p2p[k];
+                    }
                     if constexpr (CH2 && smax >= 2) gather2(IntC<(smax < 3 ? smax : 3)>{}, IntC<1>{});
                 } else {
                     if constexpr (smax >= 1) gather2(IntC<(smax < 3 ? smax : 3)>{}, IntC<0>{});
@@ -1806,7 +1825,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             const Own &w = ow[t % 2];
             const int g = dc.x;
             // (chain schedule: the parent's acceleration is the lane's previous step's)
-            constexpr bool CH3 = Chain<M>::ON || (TG_PROBE & 4);
+            constexpr bool CH3 = (Chain<M>::ON && (TG_CHAIN_MASK & 4)) || (TG_PROBE & 4);
             SV apar;
             if constexpr (CH3) apar = pr3;
             else apar = ldsv(s, ac_s(max(dc.y, 0)));
@@ -1820,7 +1839,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 const float qdd = (w.uu - dot(w.U, ap)) * w.dinv;
                 if constexpr (CH3) pr3 = ap + qdd * w.S;
                 else stsv(s, ac_s(g), ap + qdd * w.S);
-                if (!Chain<M>::ON || d_own(dc)) {   // (chain: the group's owner stores it)
+                if (!CH3 || d_own(dc)) {   // (chain: the group's owner stores it)
                     s(o + F_QDS) = w.qd + h * qdd;
                     if (cp == 0) {
                         s(o + F_UU) = qdd;
@@ -1832,9 +1851,9 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     }
                 }
             }
-            if constexpr (!Chain<M>::ON || TG_CHAIN_SYNC) TG_SYNC();
+            if constexpr (!(Chain<M>::ON && (TG_CHAIN_MASK & 4)) || TG_CHAIN_SYNC) TG_SYNC();
         }
-        if constexpr (Chain<M>::ON && !TG_CHAIN_SYNC) TG_SYNC();   // (the flag and F_QDS are read below)
+        if constexpr (Chain<M>::ON && (TG_CHAIN_MASK & 4) && !TG_CHAIN_SYNC) TG_SYNC();   // (the flag and F_QDS are read below)
         }
         if constexpr (PL::WOOD) {
             if (cp == 0 && s(PL::FLG) != 0.f && wood_update()) break;   // else the rerun below
@@ -2666,7 +2685,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     const int g = dc.x;
                     const int op = max(dc.y, 0) * GF;
                     // (chain schedule: the parent's responses are the lane's previous step's)
-                    constexpr bool CHI = Chain<M>::ON || (TG_PROBE & 8);
+                    constexpr bool CHI = (Chain<M>::ON && (TG_CHAIN_MASK & 8)) || (TG_PROBE & 8);
                     SV ap, av;
                     if constexpr (CHI) {
                         ap = pri;
@@ -2683,20 +2702,20 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     if (g > 0) {
                         const int o = g * GF;
                         const float x = (w.uu - dot(w.U, ap)) * w.dinv;
-                        const bool ow = !Chain<M>::ON || d_own(dc);   // (chain: the group's owner stores it)
+                        const bool ow = !CHI || d_own(dc);   // (chain: the group's owner stores it)
                         if constexpr (CHI) pri = ap + x * w.S;
-                        else stsv(s, o + F_PA, ap + x * w.S);
+                        if constexpr (!CHI || TG_CH8_DBG) stsv(s, o + F_PA, ap + x * w.S);
                         if (ow) s(o + F_QDS) = w.qds + x;
                         if (vit) {
                             const float xv = (w.uv - dot(w.U, av)) * w.dinv;
                             if constexpr (CHI) priv = av + xv * w.S;
-                            else stsv(s, o + F_V, av + xv * w.S);
+                            if constexpr (!CHI || TG_CH8_DBG) stsv(s, o + F_V, av + xv * w.S);
                             if (ow) s(o + F_QD) = w.qds + xv;
                         }
                     }
-                    if constexpr (!Chain<M>::ON || TG_CHAIN_SYNC) TG_SYNC();
+                    if constexpr (!(Chain<M>::ON && (TG_CHAIN_MASK & 8)) || TG_CHAIN_SYNC) TG_SYNC();
                 }
-                if constexpr (Chain<M>::ON && !TG_CHAIN_SYNC) TG_SYNC();
+                if constexpr (Chain<M>::ON && (TG_CHAIN_MASK & 8) && !TG_CHAIN_SYNC) TG_SYNC();
             } else {
                 // bottom-up gather, root solve, top-down -- once per multiplier
                 // set: with velocity iterations first the bias-free one (its
