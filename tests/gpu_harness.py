@@ -504,11 +504,12 @@ def n_resets(orc):
     return getattr(orc, "reset_count", 0)
 
 
-def perturbed_walk_oracle(cfg, seed, k, eps=1e-7):
-    """The fp64 oracle env with its initial pelvis height and every joint
-    position moved by +-eps (random signs, stream k): a rounding-level
-    perturbation of the reference itself (scripts/dev/standing_chaos_cpu.py)."""
-    p = OracleWalk(cfg, NumpyDraws(seed))
+def perturbed_walk_oracle(cfg, seed, k, eps=1e-7, precision="f64"):
+    """The oracle env (fp64, or the fp32 build) with its initial pelvis height
+    and every joint position moved by +-eps (random signs, stream k): a
+    rounding-level perturbation of the reference itself
+    (scripts/dev/standing_chaos_cpu.py, scripts/dev/standing_fp32_ensemble.py)."""
+    p = OracleWalk(cfg, NumpyDraws(seed), precision=precision)
     rs = np.random.default_rng(1000 + k)
     p.a["root"][:, 2] += (eps * rs.choice([-1.0, 1.0], p.n)).astype(np.float32)
     p.a["dof_state"][:, 0] += (eps * rs.choice([-1.0, 1.0], p.a["dof_state"].shape[0])).astype(np.float32)
@@ -516,14 +517,18 @@ def perturbed_walk_oracle(cfg, seed, k, eps=1e-7):
 
 
 def walk_env_vs_oracle(num_envs=32, steps=30, seed=0, task="ThormangWalk", dr=False, fix_base=False,
-                       spawn_height=None, amp=0.3, control=False, solver_type=None, perturbed=0):
+                       spawn_height=None, amp=0.3, control=False, solver_type=None, perturbed=0, f32_ensemble=0):
     """Free-running GPU walk env vs the oracle env on the same draws and
     actions U(-amp, amp) (amp 0: the PD-held default pose); with ``control``
     the fp32 oracle build runs the same episode beside the fp64 one
     (``within``); with ``perturbed`` = K also K fp64 runs from initial states
     perturbed by 1e-7 (``perturbed_walk_oracle``): ``pert_first_bad`` is the
     first step any of them leaves 1e-3 of the unperturbed reference -- the
-    reference's own predictability horizon at that precision.  Per-step
+    reference's own predictability horizon at that precision; with
+    ``f32_ensemble`` = K also K fp32 builds perturbed by 1e-7 (below an fp32
+    ulp of the joint positions: the same fp32 computation rounded
+    differently), whose departure steps (obs or reward over 1e-3, or a reset
+    flag changed) are ``f32_departures``.  Per-step
     maxima of the GPU's errors are kept in ``_obs_t`` / ``_rew_t``
     (``brief`` drops them for printing)."""
     import torch
@@ -533,6 +538,7 @@ def walk_env_vs_oracle(num_envs=32, steps=30, seed=0, task="ThormangWalk", dr=Fa
     orc = OracleWalk(mk(), NumpyDraws(seed))
     ctl = OracleWalk(mk(), NumpyDraws(seed), precision="f32") if control else None
     perts = [perturbed_walk_oracle(mk(), seed, k) for k in range(perturbed)]
+    f32s = [perturbed_walk_oracle(mk(), seed, 100 + k, precision="f32") for k in range(f32_ensemble)]
     rs = np.random.default_rng(seed + 100)
     err = {"obs": 0.0, "rew": 0.0, "reset_equal": True, "timeout_equal": True, "root": 0.0, "steps": steps,
            "_obs_t": [], "_rew_t": []}
@@ -554,6 +560,12 @@ def walk_env_vs_oracle(num_envs=32, steps=30, seed=0, task="ThormangWalk", dr=Fa
             c_obs, c_rew, c_reset = ctl.step(act)[:3]
             note_control(err, t, c_obs, c_rew, c_reset, o_obs, o_rew, o_reset)
             err["gpu_vs_f32"] = max(err["gpu_vs_f32"], float(np.abs(g_obs - c_obs).max()))
+        for k, fk in enumerate(f32s):
+            f_obs, f_rew, f_reset = fk.step(act)[:3]
+            dep = err.setdefault("f32_departures", [None] * len(f32s))
+            if dep[k] is None and (float(np.abs(f_obs - o_obs).max()) > 1e-3 or
+                                   float(np.abs(f_rew - o_rew).max()) > 1e-3 or not np.array_equal(f_reset, o_reset)):
+                dep[k] = t
         for k, pk in enumerate(perts):
             p_obs, _, p_reset = pk.step(act)[:3]
             dep = err.setdefault("pert_departures", [None] * len(perts))

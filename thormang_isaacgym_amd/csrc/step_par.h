@@ -271,6 +271,9 @@ template <class M> __device__ __forceinline__ GInfo ginfo(const int *gi, int g) 
 #ifndef TG_CH8_DBG
 #define TG_CH8_DBG 0
 #endif
+#if TG_CH8_DBG == 2
+static __device__ unsigned tg_ch8_bad[8];
+#endif
 
 template <class M> struct Chain {
     struct Tab {
@@ -487,6 +490,13 @@ template <int L> __device__ __forceinline__ float env_bcast(float v, int n, int 
 }
 // the partner lane's value (lane pairs sub, sub + 8 of a 16-lane row)
 __device__ __forceinline__ float pair_swap(float v) { return dpp<0x128>(v); }
+
+// an opaque copy of a spatial vector's registers (empty volatile asm): the
+// compiler cannot look through it, so arithmetic on a register-forwarded
+// value is formed as on the same value loaded from LDS
+__device__ __forceinline__ void launder_sv(SV &x) {
+    __asm__ volatile("" : "+v"(x.w.x), "+v"(x.w.y), "+v"(x.w.z), "+v"(x.v.x), "+v"(x.v.y), "+v"(x.v.z));
+}
 
 #define TG_SYNC()                                          \
     do {                                                   \
@@ -2691,6 +2701,23 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                         ap = pri;
                         av = priv;
                         (void)op;
+#if TG_CH8_DBG == 2   // developer check: the forwarded values against the stored ones (kept stores)
+                        if (g > 0) {
+                            const SV apL = ldsv(s, op + F_PA), avL = vit ? ldsv(s, op + F_V) : sv0();
+                            const float d[12] = {apL.w.x - ap.w.x, apL.w.y - ap.w.y, apL.w.z - ap.w.z, apL.v.x - ap.v.x,
+                                                 apL.v.y - ap.v.y, apL.v.z - ap.v.z, avL.w.x - av.w.x, avL.w.y - av.w.y,
+                                                 avL.w.z - av.w.z, avL.v.x - av.v.x, avL.v.y - av.v.y, avL.v.z - av.v.z};
+                            bool bad = false;
+                            for (int k = 0; k < 12; ++k) bad |= d[k] != 0.f;
+                            if (bad) atomicAdd(&tg_ch8_bad[0], 1u);
+                            atomicAdd(&tg_ch8_bad[1], 1u);
+                            if (bad && tg_ch8_bad[2] == 0u) {
+                                tg_ch8_bad[2] = 1u + t;
+                                tg_ch8_bad[3] = (unsigned)g;
+                                tg_ch8_bad[4] = (unsigned)sub;
+                            }
+                        }
+#endif
                     } else {
                         ap = ldsv(s, op + F_PA);
                         av = vit ? ldsv(s, op + F_V) : sv0();
@@ -2703,12 +2730,21 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                         const int o = g * GF;
                         const float x = (w.uu - dot(w.U, ap)) * w.dinv;
                         const bool ow = !CHI || d_own(dc);   // (chain: the group's owner stores it)
-                        if constexpr (CHI) pri = ap + x * w.S;
+                        if constexpr (CHI) {
+                            pri = ap + x * w.S;
+                            // (laundered: the next step's arithmetic sees an opaque
+                            // value, as the list form's LDS load, and the compiler
+                            // then contracts it the same way -- bit-identical)
+                            launder_sv(pri);
+                        }
                         if constexpr (!CHI || TG_CH8_DBG) stsv(s, o + F_PA, ap + x * w.S);
                         if (ow) s(o + F_QDS) = w.qds + x;
                         if (vit) {
                             const float xv = (w.uv - dot(w.U, av)) * w.dinv;
-                            if constexpr (CHI) priv = av + xv * w.S;
+                            if constexpr (CHI) {
+                                priv = av + xv * w.S;
+                                launder_sv(priv);
+                            }
                             if constexpr (!CHI || TG_CH8_DBG) stsv(s, o + F_V, av + xv * w.S);
                             if (ow) s(o + F_QD) = w.qds + xv;
                         }
