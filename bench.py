@@ -281,6 +281,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--solver-type", type=int, choices=(0, 1), default=None,
                     help="override the task cfg's sim.physx.solver_type (0 PGS, 1 TGS) for an A/B line")
+    ap.add_argument("--contact-offset", type=float, default=None,
+                    help="override sim.physx.contact_offset (0 = every point within contact_margin carries a row) "
+                         "for an A/B line")
     ap.add_argument("--whole-body", action="store_true",
                     help="walk tasks: env.asset.wholeBodyCollision (feet, shins and hands collide; model thormang_wb)")
     ap.add_argument("--terrain", action="store_true",
@@ -313,6 +316,8 @@ def main():
     cfg = load_task_cfg(args.task, num_envs=args.num_envs, sim_device=dev)
     if args.solver_type is not None:
         cfg["sim"]["physx"]["solver_type"] = args.solver_type
+    if args.contact_offset is not None:
+        cfg["sim"]["physx"]["contact_offset"] = args.contact_offset
     if args.whole_body:
         if not args.task.startswith("ThormangWalk"):
             ap.error("--whole-body applies to the ThormangWalk tasks")
@@ -367,7 +372,12 @@ def main():
     value = N * args.steps * world / elapsed
     bpe, breakdown = algorithmic_bytes_per_env_step(args.task, env)
     kbpe = kernel_bytes_per_env(args.task, env)
-    traffic, traffic_src = committed_traffic(args.task, N)
+    # the committed PMC / SQ summaries profile the default workload of a task
+    # (flat ground, the cfg's solver, the foot-only model): other variants
+    # carry no traffic figure rather than another workload's
+    profiled = not (args.terrain or args.whole_body or args.solver_type is not None
+                    or args.contact_offset is not None)
+    traffic, traffic_src = committed_traffic(args.task, N) if profiled else (None, None)
     achieved = bpe * N / (kern_ms * 1e-3) / 1e9
     sim_cfg = cfg["sim"]
     out = {
@@ -409,7 +419,7 @@ def main():
                      "traffic_over_algorithmic": traffic / (bpe * N) if traffic else None,
                      "traffic_source": traffic_src},
     }
-    sq = committed_sq(args.task, N)
+    sq = committed_sq(args.task, N) if profiled else None
     if sq is not None:
         out["roofline"]["issue"] = sq
     if not args.no_cpu_baseline and world == 1:

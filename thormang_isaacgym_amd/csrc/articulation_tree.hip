@@ -42,11 +42,6 @@ int tree_prof_read(unsigned long long *out, int n) {
 
 }  // namespace tg
 
-#if defined(TG_CH8_DBG) && TG_CH8_DBG == 2
-extern "C" int tg_ch8_read(unsigned *out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(tg::tg_ch8_bad), 8 * sizeof(unsigned)) == hipSuccess ? 0 : -1;
-}
-#endif
 #ifdef TG_DUMP_ENV
 // developer build only (scripts/dev/contact_dump.py): this unit's copies of
 // the dump symbols (tg_dump_* are static __device__, so each unit's step

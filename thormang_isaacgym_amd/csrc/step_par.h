@@ -261,18 +261,13 @@ template <class M> __device__ __forceinline__ GInfo ginfo(const int *gi, int g) 
 // the passes that use the chain registers (1 pass 1a, 2 pass 2b, 4 pass 3,
 // 8 the impulse top-down pass); the others run their list-schedule form over
 // the chain schedule (duplicates then load and store like owners: the same
-// values).  7 by default: those three are bit-identical to the list schedule
-// (scripts/dev/r5_chain_mask.sh, profiles/r5/chain_mask.txt); the impulse
-// pass's chain form rounds apart from it at the 1e-5 level in a step
-// (unexplained: the values it forwards are the ones the list form stores)
+// values).  All four by default, bit-identical to the list schedule
+// (scripts/dev/r5_chain_mask.sh, scripts/dev/bitcmp_libs.py, profiles/r5/).
+// (The impulse pass stores the joint velocities from every lane of a group,
+// owners and duplicates alike: gating that store on ownership changed how the
+// compiler contracted the stored sum, and with it the rounding.)
 #ifndef TG_CHAIN_MASK
-#define TG_CHAIN_MASK 7
-#endif
-#ifndef TG_CH8_DBG
-#define TG_CH8_DBG 0
-#endif
-#if TG_CH8_DBG == 2
-static __device__ unsigned tg_ch8_bad[8];
+#define TG_CHAIN_MASK 15
 #endif
 
 template <class M> struct Chain {
@@ -490,13 +485,6 @@ template <int L> __device__ __forceinline__ float env_bcast(float v, int n, int 
 }
 // the partner lane's value (lane pairs sub, sub + 8 of a 16-lane row)
 __device__ __forceinline__ float pair_swap(float v) { return dpp<0x128>(v); }
-
-// an opaque copy of a spatial vector's registers (empty volatile asm): the
-// compiler cannot look through it, so arithmetic on a register-forwarded
-// value is formed as on the same value loaded from LDS
-__device__ __forceinline__ void launder_sv(SV &x) {
-    __asm__ volatile("" : "+v"(x.w.x), "+v"(x.w.y), "+v"(x.w.z), "+v"(x.v.x), "+v"(x.v.y), "+v"(x.v.z));
-}
 
 #define TG_SYNC()                                          \
     do {                                                   \
@@ -2701,23 +2689,6 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                         ap = pri;
                         av = priv;
                         (void)op;
-#if TG_CH8_DBG == 2   // developer check: the forwarded values against the stored ones (kept stores)
-                        if (g > 0) {
-                            const SV apL = ldsv(s, op + F_PA), avL = vit ? ldsv(s, op + F_V) : sv0();
-                            const float d[12] = {apL.w.x - ap.w.x, apL.w.y - ap.w.y, apL.w.z - ap.w.z, apL.v.x - ap.v.x,
-                                                 apL.v.y - ap.v.y, apL.v.z - ap.v.z, avL.w.x - av.w.x, avL.w.y - av.w.y,
-                                                 avL.w.z - av.w.z, avL.v.x - av.v.x, avL.v.y - av.v.y, avL.v.z - av.v.z};
-                            bool bad = false;
-                            for (int k = 0; k < 12; ++k) bad |= d[k] != 0.f;
-                            if (bad) atomicAdd(&tg_ch8_bad[0], 1u);
-                            atomicAdd(&tg_ch8_bad[1], 1u);
-                            if (bad && tg_ch8_bad[2] == 0u) {
-                                tg_ch8_bad[2] = 1u + t;
-                                tg_ch8_bad[3] = (unsigned)g;
-                                tg_ch8_bad[4] = (unsigned)sub;
-                            }
-                        }
-#endif
                     } else {
                         ap = ldsv(s, op + F_PA);
                         av = vit ? ldsv(s, op + F_V) : sv0();
@@ -2729,24 +2700,20 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     if (g > 0) {
                         const int o = g * GF;
                         const float x = (w.uu - dot(w.U, ap)) * w.dinv;
-                        const bool ow = !CHI || d_own(dc);   // (chain: the group's owner stores it)
                         if constexpr (CHI) {
                             pri = ap + x * w.S;
-                            // (laundered: the next step's arithmetic sees an opaque
-                            // value, as the list form's LDS load, and the compiler
-                            // then contracts it the same way -- bit-identical)
-                            launder_sv(pri);
                         }
-                        if constexpr (!CHI || TG_CH8_DBG) stsv(s, o + F_PA, ap + x * w.S);
-                        if (ow) s(o + F_QDS) = w.qds + x;
+                        if constexpr (!CHI) stsv(s, o + F_PA, ap + x * w.S);
+                        // (every lane of the group stores, duplicates too: the same
+                        // value, and the same contraction as the list form's)
+                        s(o + F_QDS) = w.qds + x;
                         if (vit) {
                             const float xv = (w.uv - dot(w.U, av)) * w.dinv;
                             if constexpr (CHI) {
                                 priv = av + xv * w.S;
-                                launder_sv(priv);
                             }
-                            if constexpr (!CHI || TG_CH8_DBG) stsv(s, o + F_V, av + xv * w.S);
-                            if (ow) s(o + F_QD) = w.qds + xv;
+                            if constexpr (!CHI) stsv(s, o + F_V, av + xv * w.S);
+                            s(o + F_QD) = w.qds + xv;
                         }
                     }
                     if constexpr (!(Chain<M>::ON && (TG_CHAIN_MASK & 8)) || TG_CHAIN_SYNC) TG_SYNC();
