@@ -234,7 +234,7 @@ template <class M> __device__ __forceinline__ GInfo ginfo(const int *gi, int g) 
     return GInfo{p[GI_PARENT], p[GI_DOF], p[GI_JT]};
 }
 
-// Chain schedule (round 5; TG_CHAIN, the humanoid-size lane-pair trees): one
+// Chain schedule (round 5; TG_CHAIN, the lane-pair trees): one
 // schedule slot per root-to-leaf chain of the group tree -- slot s runs, at
 // step t, the group at depth t + 1 on the path from the root to its leaf --
 // so in every tree pass a group's parent (forward passes) or first child
@@ -268,6 +268,12 @@ template <class M> __device__ __forceinline__ GInfo ginfo(const int *gi, int g) 
 // compiler contracted the stored sum, and with it the rounding.)
 #ifndef TG_CHAIN_MASK
 #define TG_CHAIN_MASK 15
+#endif
+// every lane-pair tree with at least this many groups (the scooters' 6-group
+// trees gain too: Gogoro 44.9 -> 43.3 us, GogoroPaper 36.6 -> 35.4 us,
+// bit-identical, profiles/r5/scooter_chain_ab.txt; 16 = the humanoids only)
+#ifndef TG_CHAIN_MIN_NG
+#define TG_CHAIN_MIN_NG 2
 #endif
 
 template <class M> struct Chain {
@@ -311,7 +317,7 @@ template <class M> struct Chain {
         return x;
     }
     static constexpr Tab tab = make();
-    static constexpr bool ON = TG_CHAIN && M::PAIR && M::NG >= 16 && M::NG <= 128 && tab.nleaf <= M::SL &&
+    static constexpr bool ON = TG_CHAIN && M::PAIR && M::NG >= TG_CHAIN_MIN_NG && M::NG <= 128 && tab.nleaf <= M::SL &&
                                tab.depth <= M::NSTEP;
 };
 // the group (step t, slot) runs (chain: only its owner counts, for the gather widths)
