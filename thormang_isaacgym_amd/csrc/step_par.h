@@ -1312,10 +1312,20 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
         // previous step's, the root's at step 0)
         constexpr bool CH = Chain<M>::ON && (TG_CHAIN_MASK & 1);
         constexpr bool CH1 = CH || (TG_PROBE & 1);
+#ifndef TG_Q_AHEAD
+#define TG_Q_AHEAD 1   // pass 1a: q, qd loaded two steps ahead (0: in the step, the A/B control)
+#endif
         M3 pr_R = eye3();
         V3 pr_P = v3(0, 0, 0);
         SV pr_v = v0;
-        auto body1 = [&](const I4 &dc, const float *ck) {
+        // the group's joint position / velocity, loaded two steps ahead with
+        // the step's other inputs (pass 1a does not write them)
+        auto ld_q = [&](const I4 &dc, float *qq) {
+            const int o = max(dc.x, 0) * GF;
+            qq[0] = s(o + F_Q);
+            qq[1] = s(o + F_QD);
+        };
+        auto body1 = [&](const I4 &dc, const float *ck, const float *qq) {
             const int g = dc.x;
             if (g > 0) {
                 const int o = g * GF, par = dc.y, jt = d_jt(dc);
@@ -1331,7 +1341,12 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     Pp = ldv3(s, par * GF + F_P);
                     vp = ldsv(s, par * GF + F_V);
                 }
+#if TG_Q_AHEAD
+                const float qg = qq[0], qdg = qq[1];
+#else
+                (void)qq;
                 const float qg = s(o + F_Q), qdg = s(o + F_QD);
+#endif
                 M3 Rpc;   // child -> parent rotation at q, then the root-frame pose
 #pragma unroll
                 for (int k = 0; k < 9; ++k) Rpc.a[k] = ck[k];
@@ -1368,25 +1383,42 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
         // fully unrolled, inputs two steps ahead in a 3-deep ring (renamed
         // registers, no copies: the wait for step t's inputs leaves steps
         // t + 1 and t + 2 in flight)
+        float qr[3][2];
         if constexpr (KIN1) {
+            I4 dr[3];
+            dr[0] = pdsc(0);
+            if (TG_Q_AHEAD) ld_q(dr[0], qr[0]);
+            if constexpr (M::NSTEP > 1) {
+                dr[1] = pdsc(1);
+                if (TG_Q_AHEAD) ld_q(dr[1], qr[1]);
+            }
 #pragma unroll
-            for (int t = 0; t < M::NSTEP; ++t) body1(pdsc(t), kin1[t]);
+            for (int t = 0; t < M::NSTEP; ++t) {
+                if (t + 2 < M::NSTEP) {
+                    dr[(t + 2) % 3] = pdsc(t + 2);
+                    if (TG_Q_AHEAD) ld_q(dr[(t + 2) % 3], qr[(t + 2) % 3]);
+                }
+                body1(dr[t % 3], kin1[t], qr[t % 3]);
+            }
         } else {
         float kr[3][12];
         I4 dr[3];
         dr[0] = pdsc(0);
         load_kin(dr[0].x, kr[0]);
+        if (TG_Q_AHEAD) ld_q(dr[0], qr[0]);
         if constexpr (M::NSTEP > 1) {
             dr[1] = pdsc(1);
             load_kin(dr[1].x, kr[1]);
+            if (TG_Q_AHEAD) ld_q(dr[1], qr[1]);
         }
 #pragma unroll
         for (int t = 0; t < M::NSTEP; ++t) {
             if (t + 2 < M::NSTEP) {
                 dr[(t + 2) % 3] = pdsc(t + 2);
                 load_kin(dr[(t + 2) % 3].x, kr[(t + 2) % 3]);
+                if (TG_Q_AHEAD) ld_q(dr[(t + 2) % 3], qr[(t + 2) % 3]);
             }
-            body1(dr[t % 3], kr[t % 3]);
+            body1(dr[t % 3], kr[t % 3], qr[t % 3]);
         }
         }
         if constexpr (CH && !TG_CHAIN_SYNC) TG_SYNC();   // (pass 1b reads every group's pose)
