@@ -1325,7 +1325,55 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             qq[0] = s(o + F_Q);
             qq[1] = s(o + F_QD);
         };
+        // chain form without branches (TG_1A_FLAT): every lane runs its step,
+        // idle lanes on the root's inputs, and a lane that does not own its
+        // group stores into the Delassus / row area, which the contact setup
+        // rebuilds later in the substep -- straight-line code, so the
+        // compiler can overlap a step's parent-independent work (sin / cos,
+        // the joint rotation) with the previous step's chain
+#ifndef TG_1A_FLAT
+#define TG_1A_FLAT 1
+#endif
+        constexpr bool FLAT1 = CH && TG_1A_FLAT && PL::VFREE - PL::W >= F_V + 6;
+        auto body1f = [&](const I4 &dc, const float *ck, const float *qq) {
+            const int g = dc.x, jt = d_jt(dc);
+            const float qg = qq[0], qdg = qq[1];
+            M3 Rpc;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) Rpc.a[k] = ck[k];
+            V3 tr = v3(ck[9], ck[10], ck[11]);
+            float sq, cq;
+            tg_sincos(qg, &sq, &cq);
+            if (all_revolute<M>() || jt == TG_JOINT_REVOLUTE) {   // Rpc * Rz(q), else a shifted origin
+#pragma unroll
+                for (int r = 0; r < 3; ++r) {
+                    const float c0 = Rpc.a[3 * r], c1 = Rpc.a[3 * r + 1];
+                    Rpc.a[3 * r] = c0 * cq + c1 * sq;
+                    Rpc.a[3 * r + 1] = c1 * cq - c0 * sq;
+                }
+            } else {
+                tr = tr + qg * v3(Rpc.a[2], Rpc.a[5], Rpc.a[8]);
+            }
+            const M3 Rg = mul(pr_R, Rpc);
+            const V3 Pg = pr_P + mul(pr_R, tr);
+            const SV Sg = motion_Sm<M>(jt, v3(Rg.a[2], Rg.a[5], Rg.a[8]), Pg);
+            const SV vg = pr_v + qdg * Sg;
+            const int os = (g > 0 && d_own(dc)) ? g * GF : PL::W;
+            stm3(s, os + F_RT, transpose(Rg));
+            stv3(s, os + F_P, Pg);
+            stsv(s, os + F_V, vg);
+            if (g > 0) {   // (an idle lane keeps its chain registers: updating them
+                           // changed the scooters' results, bit-identical this way)
+                pr_R = Rg;
+                pr_P = Pg;
+                pr_v = vg;
+            }
+        };
         auto body1 = [&](const I4 &dc, const float *ck, const float *qq) {
+            if constexpr (FLAT1) {
+                body1f(dc, ck, qq);
+                return;
+            }
             const int g = dc.x;
             if (g > 0) {
                 const int o = g * GF, par = dc.y, jt = d_jt(dc);
@@ -1380,10 +1428,21 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             }
             if constexpr (!CH || TG_CHAIN_SYNC) TG_SYNC();
         };
+        static_assert(!FLAT1 || TG_Q_AHEAD, "the flat chain form takes q, qd from the prefetch ring");
         // fully unrolled, inputs two steps ahead in a 3-deep ring (renamed
         // registers, no copies: the wait for step t's inputs leaves steps
         // t + 1 and t + 2 in flight)
         float qr[3][2];
+#ifndef TG_1A_REPS
+#define TG_1A_REPS 1   // developer ablation: pass 1a run this many times (idempotent: its marginal cost)
+#endif
+#pragma unroll 1
+        for (int rep1 = 0; rep1 < TG_1A_REPS; ++rep1) {
+        if (rep1 > 0) {
+            pr_R = eye3();
+            pr_P = v3(0, 0, 0);
+            pr_v = v0;
+        }
         if constexpr (KIN1) {
             I4 dr[3];
             dr[0] = pdsc(0);
@@ -1401,27 +1460,30 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 body1(dr[t % 3], kin1[t], qr[t % 3]);
             }
         } else {
-        float kr[3][12];
-        I4 dr[3];
-        dr[0] = pdsc(0);
-        load_kin(dr[0].x, kr[0]);
-        if (TG_Q_AHEAD) ld_q(dr[0], qr[0]);
-        if constexpr (M::NSTEP > 1) {
-            dr[1] = pdsc(1);
-            load_kin(dr[1].x, kr[1]);
-            if (TG_Q_AHEAD) ld_q(dr[1], qr[1]);
+#ifndef TG_KIN_AHEAD
+#define TG_KIN_AHEAD 2   // pass 1a: the joint placements (composite cache) issued this many steps ahead
+#endif
+        constexpr int KA = TG_KIN_AHEAD, KR = KA + 1;
+        float kr[KR][12], qk[KR][2];
+        I4 dr[KR];
+#pragma unroll
+        for (int t = 0; t < KA && t < M::NSTEP; ++t) {
+            dr[t] = pdsc(t);
+            load_kin(dr[t].x, kr[t]);
+            if (TG_Q_AHEAD) ld_q(dr[t], qk[t]);
         }
 #pragma unroll
         for (int t = 0; t < M::NSTEP; ++t) {
-            if (t + 2 < M::NSTEP) {
-                dr[(t + 2) % 3] = pdsc(t + 2);
-                load_kin(dr[(t + 2) % 3].x, kr[(t + 2) % 3]);
-                if (TG_Q_AHEAD) ld_q(dr[(t + 2) % 3], qr[(t + 2) % 3]);
+            if (t + KA < M::NSTEP) {
+                dr[(t + KA) % KR] = pdsc(t + KA);
+                load_kin(dr[(t + KA) % KR].x, kr[(t + KA) % KR]);
+                if (TG_Q_AHEAD) ld_q(dr[(t + KA) % KR], qk[(t + KA) % KR]);
             }
-            body1(dr[t % 3], kr[t % 3], qr[t % 3]);
+            body1(dr[t % KR], kr[t % KR], qk[t % KR]);
         }
         }
-        if constexpr (CH && !TG_CHAIN_SYNC) TG_SYNC();   // (pass 1b reads every group's pose)
+        }
+        if constexpr (CH && (!TG_CHAIN_SYNC || FLAT1)) TG_SYNC();   // (pass 1b reads every group's pose)
 #ifdef TG_DUMMY_STEPS
         // developer ablation: TG_DUMMY_STEPS dependent LDS round trips with no
         // arithmetic (kind 0: one float; kind 1: pass 1a's traffic, 18 floats
