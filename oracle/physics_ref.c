@@ -511,6 +511,23 @@ static int drives_saturated(const Env *e, Work *w, real h, const real *q, const 
     return 0;
 }
 
+/* developer dump: the drive closest to its effort limit after the implicit
+ * solve -- | |te - K qdd| - effort |, and its dof in *dof */
+static real drive_margin(const Env *e, Work *w, real h, const real *q, const real *qd, const real *qdd, int *dof) {
+    real best = 1e30;
+    *dof = -1;
+    for (int g = 1; g < e->m->num_groups; ++g) {
+        int d = w->gdof[g];
+        int mode = (int)lrint(prop(e, TG_PROP_DRIVE_MODE, d));
+        if (mode != TG_DOF_MODE_POS && mode != TG_DOF_MODE_VEL) continue;
+        real kp = prop(e, TG_PROP_STIFFNESS, d), kd = prop(e, TG_PROP_DAMPING, d), eff = prop(e, TG_PROP_EFFORT, d);
+        real te = kp * (e->pos_tgt[d] - q[d] - h * qd[d]) + kd * (e->vel_tgt[d] - qd[d]);
+        real m = fabs(fabs(te - (h * kd + h * h * kp) * qdd[d]) - eff);
+        if (m < best) { best = m; *dof = d; }
+    }
+    return best;
+}
+
 /* velocity of group g's spatial velocity for generalised velocity (qd, v0) with current X */
 static void group_vels(const tg_model_desc *m, Work *w, const real *qd, const V6 v0, V6 *vg) {
     memcpy(vg[0], v0, sizeof(V6));
@@ -1017,12 +1034,19 @@ void oracle_physics_step_env(const tg_model_desc *m, const tg_sim_params *sp, fl
         memcpy(w.org, pos, sizeof(V3));
         V6 a0;
         aba(&e, &w, h, q, qd, v0, qdd, a0, 1, NULL);
-        if (drives_saturated(&e, &w, h, q, qd, qdd)) {
+        const int sat = drives_saturated(&e, &w, h, q, qd, qdd);
+        if (t_env >= 0 && t_env == oracle_dump_env && s == oracle_dump_sub) {
+            int dm;
+            oracle_dump_buf[2791] = drive_margin(&e, &w, h, q, qd, qdd, &dm);
+            oracle_dump_buf[2792] = dm;
+        }
+        if (sat) {
             real qdd0[MAXD];
             memcpy(qdd0, qdd, sizeof(real) * D);
             aba(&e, &w, h, q, qd, v0, qdd, a0, 1, qdd0);
         }
         if (t_env >= 0 && t_env == oracle_dump_env && s == oracle_dump_sub) {   /* developer dump (contact_dump.py) */
+            oracle_dump_buf[2790] = sat;
             for (int k = 0; k < 6; ++k) { oracle_dump_buf[2700 + k] = a0[k]; oracle_dump_buf[2710 + k] = v0[k]; }
             for (int d = 0; d < D; ++d) oracle_dump_buf[2800 + d] = qdd[d];
         }

@@ -16,6 +16,7 @@ GPU's yaw rate lies in the spread:
 
     python scripts/dev/gogoro_outlier_sensitivity.py study out.npz [K]
 """
+import ctypes as C
 import json
 import sys
 
@@ -56,22 +57,49 @@ def study(path, K):
     D = orcs["f64"].D
     rng = np.random.default_rng(99)
 
-    def run(p, eps):
+    def run(p, eps, pert=None, dump_sub=-1):
         orc = orcs[p]
         for k, v in snap.items():
             orc.a[k][...] = v
         orc.src.rs.bit_generator.state = state
         if eps:
+            if pert is None:
+                pert = (rng.standard_normal(13), rng.standard_normal((D, 2)))
             r = orc.a["root"][e]
-            r[:] = r * (1 + eps * rng.standard_normal(r.shape)).astype(np.float32)
+            r[:] = r * (1 + eps * pert[0]).astype(np.float32)
             ds = orc.a["dof_state"][e * D:(e + 1) * D]
-            ds[:] = ds * (1 + eps * rng.standard_normal(ds.shape)).astype(np.float32)
-        return orc.step(act[:, 0])[0][e].copy()
+            ds[:] = ds * (1 + eps * pert[1]).astype(np.float32)
+        if dump_sub >= 0:
+            orc.L.oracle_dump_set.argtypes = [C.c_int, C.c_int]
+            orc.L.oracle_dump_set(e, dump_sub)
+        o = orc.step(act[:, 0])[0][e].copy()
+        if dump_sub >= 0:
+            buf = np.zeros(4096)
+            orc.L.oracle_dump_read.argtypes = [C.c_void_p, C.c_int]
+            orc.L.oracle_dump_read(buf.ctypes.data, 4096)
+            orc.L.oracle_dump_set(-1, 0)
+            return o, buf
+        return o
 
     g = z["gpu_obs"][e]
     base = run("f64", 0.0)
     print(f"step {int(z['step'])} env {e}: yaw rate obs[2]  gpu {g[2]:.7f}  fp64 {base[2]:.7f} "
           f"(recorded {z['oracle_obs'][e][2]:.7f})  fp32 {run('f32', 0.0)[2]:.7f}")
+    # which discrete decision flips: a perturbation that lands on the GPU's
+    # value against the unperturbed replay, substep by substep (the oracle's
+    # dump: drive-clamp flag and the nearest drive's distance to its effort
+    # limit, multipliers)
+    for _ in range(4 * K):
+        pert = (rng.standard_normal(13), rng.standard_normal((D, 2)))
+        if abs(run("f64", 1e-7, pert)[2] - base[2]) > 0.5 * abs(g[2] - base[2]):
+            break
+    for sub in range(3):
+        for tag, pp in (("unperturbed", None), ("jumped     ", pert)):
+            _, b = run("f64", 1e-7 if pp is not None else 0.0, pp, dump_sub=sub)
+            k = int(b[0])
+            print(f"  substep {sub} {tag}: drive clamp {int(b[2790])}, nearest drive dof {int(b[2792])} "
+                  f"{b[2791]:.3e} from its effort limit; lam_pos {np.round(b[2600:2600 + k], 6)} "
+                  f"lam_vel {np.round(b[2500:2500 + k], 6)}")
     for p in ("f64", "f32"):
         ys = np.array([run(p, 1e-7)[2] for _ in range(K)])
         d = ys - base[2]
