@@ -219,3 +219,26 @@ def test_gpu_shared_cache_is_invisible_to_property_writes(monkeypatch):
         assert torch.equal(a, b), t
     moved = (runs[0][-1] != runs[2][-1]).any(1).nonzero().flatten().tolist()
     assert {3, 7, 11} <= set(moved), moved
+
+
+@pytest.mark.parametrize("task", ["Gogoro", "ThormangWalk", "GogoroPaper"])
+def test_gpu_step_is_deterministic(task):
+    """Two envs from one seed, stepped with the same actions, stay bitwise
+    equal (observations, rewards, resets, root states) -- the step kernels'
+    results do not depend on timing (no race between an env's lanes, no
+    order-dependent atomics).  Round 5 used this to tell a rounding-sensitive
+    step from a nondeterministic one."""
+    _cuda()
+    import thormang_isaacgym_amd as tia
+    n = 1024
+    envs = [tia.make(seed=5, task=task, num_envs=n, sim_device="cuda:0", rl_device="cuda:0") for _ in range(2)]
+    g = torch.Generator(device="cuda:0").manual_seed(7)
+    resets = 0
+    for _ in range(80):
+        a = torch.rand(n, envs[0].num_actions, device="cuda:0", generator=g) * 2 - 1
+        (o0, r0, d0, _), (o1, r1, d1, _) = (e.step(a) for e in envs)
+        assert torch.equal(o0["obs"], o1["obs"]) and torch.equal(r0, r1) and torch.equal(d0, d1), task
+        assert torch.equal(envs[0].root_tensor, envs[1].root_tensor), task
+        resets += int(d0.sum())
+    if task != "GogoroPaper":   # (its committed cfg is the fixed-base one: no falls in 80 steps)
+        assert resets > 0, task
