@@ -49,6 +49,37 @@ def test_gpu_walk_fixed_base_free_running_1000_steps():
     assert err["reset_equal"] and err["timeout_equal"], err
 
 
+def test_gpu_walk_random_actions_free_running_1000_steps():
+    """The headline walk free-running for north_star's 1000 steps with falls
+    and re-spawns (64 envs, random actions U(-0.3, 0.3), seed 21; VERDICT r4:
+    no walk test ran 1000 free-running steps with falls).  Falling humanoids
+    amplify rounding: the fp32 oracle build's own reset flags desync from the
+    fp64 reference at step 319, so no fp32 computation -- the GPU's included
+    -- tracks fp64 to 1e-3 for all 1000 steps.  As for the standing walk, the
+    yardstick is what fp32 rounding alone does: the control and 8 fp32 builds
+    started 1e-7 away (below an fp32 ulp) give 9 departure steps, and the GPU
+    must not depart before the third-earliest (obs and reward within 1e-3,
+    identical reset flags, at every step before it).  The steps after it are
+    reported, not asserted (round 4's drift study: the GPU leaves 1e-3 at
+    step 723, the fp32 build at 320; profiles/r4/drift_walk_root_relative.txt)."""
+    _cuda()
+    import numpy as np
+    from tests.gpu_harness import walk_env_vs_oracle
+    err = walk_env_vs_oracle(num_envs=64, steps=1000, seed=21, amp=0.3, control=True, f32_ensemble=8)
+    n = err["steps"]
+    deps = sorted([err.get("ctl_first_bad", n)] + [d if d is not None else n for d in err["f32_departures"]])
+    hz = deps[2]
+    gpu = min(err.get("first_bad_step", n), err.get("reset_diff_step", n) if not err["reset_equal"] else n)
+    err.update(f32_sorted=deps, horizon=hz, gpu_departure=gpu,
+               gpu_rank=int(np.searchsorted(deps, gpu, side="right")),
+               obs_pre_horizon=float(np.max(err["_obs_t"][:hz])), rew_pre_horizon=float(np.max(err["_rew_t"][:hz])))
+    print(brief(err))
+    assert err["resets"] > 0, brief(err)
+    assert hz >= 100, brief(err)
+    assert gpu >= hz, brief(err)
+    assert err["obs_pre_horizon"] < 1e-3 and err["rew_pre_horizon"] < 1e-3, brief(err)
+
+
 def test_gpu_walk_standing_free_running_1000_steps():
     """ThormangWalk standing (zero actions: the PD-held default pose), 32 envs,
     1000 free-running steps; some spawn poses topple (20 falls with seed 21).
