@@ -80,6 +80,31 @@ def test_gpu_walk_random_actions_free_running_1000_steps():
     assert err["obs_pre_horizon"] < 1e-3 and err["rew_pre_horizon"] < 1e-3, brief(err)
 
 
+def test_gpu_walk_dr_pushes_free_running_1000_steps():
+    """ThormangWalkDR (random pushes on top of the falls), 32 envs, 1000
+    free-running steps, under the same fp32-ensemble rule as the plain walk
+    (test_gpu_walk_random_actions_free_running_1000_steps): the GPU must not
+    depart from the fp64 reference (obs or reward over 1e-3, or a reset flag
+    changed) before the third-earliest of 9 fp32 evaluations of the same
+    episode (the control and 8 fp32 builds started 1e-7 away)."""
+    _cuda()
+    import numpy as np
+    from tests.gpu_harness import walk_env_vs_oracle
+    err = walk_env_vs_oracle(num_envs=32, steps=1000, seed=7, task="ThormangWalkDR", control=True, f32_ensemble=8)
+    n = err["steps"]
+    deps = sorted([err.get("ctl_first_bad", n)] + [d if d is not None else n for d in err["f32_departures"]])
+    hz = deps[2]
+    gpu = min(err.get("first_bad_step", n), err.get("reset_diff_step", n) if not err["reset_equal"] else n)
+    err.update(f32_sorted=deps, horizon=hz, gpu_departure=gpu,
+               gpu_rank=int(np.searchsorted(deps, gpu, side="right")),
+               obs_pre_horizon=float(np.max(err["_obs_t"][:hz])), rew_pre_horizon=float(np.max(err["_rew_t"][:hz])))
+    print(brief(err))
+    assert err["resets"] > 0, brief(err)
+    assert hz >= 50, brief(err)
+    assert gpu >= hz, brief(err)
+    assert err["obs_pre_horizon"] < 1e-3 and err["rew_pre_horizon"] < 1e-3, brief(err)
+
+
 def test_gpu_walk_standing_free_running_1000_steps():
     """ThormangWalk standing (zero actions: the PD-held default pose), 32 envs,
     1000 free-running steps; some spawn poses topple (20 falls with seed 21).
