@@ -173,10 +173,14 @@ def tgs_configured(cfg):
 
 
 def gogoro_env_vs_oracle(num_envs=64, steps=20, seed=0, policy=None, max_steps=1000, dr=False, fix_base=False,
-                         control=None):
+                         control=None, f32_ensemble=0):
     """Free-running GPU Gogoro env vs the oracle env on the same draws; with
     ``control`` (default: when the cfg asks for TGS) the fp32 oracle build
-    runs the same free-running episode beside the fp64 one (``within``)."""
+    runs the same free-running episode beside the fp64 one (``within``); with
+    ``f32_ensemble`` = K also K fp32 builds whose initial root and joint
+    state is moved by relative 1e-7 (about an fp32 ulp), whose departure
+    steps from fp64 (obs or reward over 1e-3, or a reset flag changed) are
+    ``f32_departures`` (as walk_env_vs_oracle's)."""
     import torch
     from thormang_isaacgym_amd.tasks import gogoro as gmod
     cfg = parity_cfg(num_envs, max_steps=max_steps, dr=dr)
@@ -190,10 +194,21 @@ def gogoro_env_vs_oracle(num_envs=64, steps=20, seed=0, policy=None, max_steps=1
         control = tgs_configured(cfg)
     ctl = OracleGogoro(parity_cfg(num_envs, max_steps=max_steps, dr=dr), NumpyDraws(seed), fix_base=fix_base,
                        precision="f32") if control else None
+    f32s = []
+    for k in range(f32_ensemble):
+        fk = OracleGogoro(parity_cfg(num_envs, max_steps=max_steps, dr=dr), NumpyDraws(seed), fix_base=fix_base,
+                          precision="f32")
+        prs = np.random.default_rng(100 + k)
+        for name in ("root", "dof_state"):
+            x = fk.a[name]
+            x[...] = (x * (1 + 1e-7 * prs.standard_normal(x.shape))).astype(x.dtype)
+        f32s.append(fk)
     err = {"obs": 0.0, "rew": 0.0, "reset_equal": True, "timeout_equal": True, "root": 0.0, "steps": steps,
            "resets": 0, "_obs_t": [], "_rew_t": []}
     if ctl is not None:
         err["obs_f32"] = err["rew_f32"] = 0.0
+    if f32s:
+        err["f32_departures"] = [None] * len(f32s)
     obs_np = orc.a["obs_buf"].copy()
     for t in range(steps):
         if dr:
@@ -206,6 +221,12 @@ def gogoro_env_vs_oracle(num_envs=64, steps=20, seed=0, policy=None, max_steps=1
         if ctl is not None:
             c_obs, c_rew, c_reset = ctl.step(act[:, 0])[:3]
             note_control(err, t, c_obs, c_rew, c_reset, o_obs, o_rew, o_reset)
+        for k, fk in enumerate(f32s):
+            f_obs, f_rew, f_reset = fk.step(act[:, 0])[:3]
+            dep = err["f32_departures"]
+            if dep[k] is None and (float(np.abs(f_obs - o_obs).max()) > 1e-3 or
+                                   float(np.abs(f_rew - o_rew).max()) > 1e-3 or not np.array_equal(f_reset, o_reset)):
+                dep[k] = t
         g_obs = obs_d["obs"].cpu().numpy()
         e_obs = float(np.abs(g_obs - o_obs).max())
         e_rew = float(np.abs(rew.cpu().numpy() - o_rew).max())
@@ -214,6 +235,8 @@ def gogoro_env_vs_oracle(num_envs=64, steps=20, seed=0, policy=None, max_steps=1
         err["obs"] = max(err["obs"], e_obs)
         err["rew"] = max(err["rew"], e_rew)
         err["root"] = max(err["root"], float(np.abs(env.root_tensor.cpu().numpy() - orc.a["root"]).max()))
+        if err["reset_equal"] and not np.array_equal(reset.cpu().numpy(), o_reset):
+            err["reset_diff_step"] = t
         err["reset_equal"] &= bool(np.array_equal(reset.cpu().numpy(), o_reset))
         err["timeout_equal"] &= bool(np.array_equal(extras["time_outs"].cpu().numpy().astype(np.uint8), o_to))
         err["resets"] += int(o_reset.sum())
