@@ -843,18 +843,20 @@ static int collect_rows(const Env *e, Work *w, real h, const V6 *vg, Row *rows, 
 static void pgs_sweeps(int K, int npatch, const Patch *patches, const Row *rows, const real *target,
                        real (*W)[3 * MAXC], const real *vfree, real *lam, int iters) {
 #define ROWV(i) ({ real v_ = vfree[i]; for (int j_ = 0; j_ < K; ++j_) v_ += W[i][j_] * lam[j_]; v_; })
+    /* a row with no response (its shape on a fixed base) takes no impulse */
+#define OVERW(x, i) (W[i][i] > 0 ? (x) / W[i][i] : 0)
     for (int it = 0; it < iters; ++it) {
         for (int p = 0; p < npatch; ++p) {
             const Patch *P = &patches[p];
             real N = 0;
             for (int i = P->n0; i < P->n0 + P->nn; ++i) {
-                real l = lam[i] + (target[i] - ROWV(i)) / W[i][i];
+                real l = lam[i] + OVERW(target[i] - ROWV(i), i);
                 lam[i] = l > 0 ? l : 0;
                 N += lam[i];
             }
             int f = P->f0;
-            lam[f] -= ROWV(f) / W[f][f];
-            lam[f + 1] -= ROWV(f + 1) / W[f + 1][f + 1];
+            lam[f] -= OVERW(ROWV(f), f);
+            lam[f + 1] -= OVERW(ROWV(f + 1), f + 1);
             real lt = sqrt(lam[f] * lam[f] + lam[f + 1] * lam[f + 1]), lim = P->mu * N;
             if (lt > lim) {
                 real sc = lt > 0 ? lim / lt : 0;
@@ -862,12 +864,13 @@ static void pgs_sweeps(int K, int npatch, const Patch *patches, const Row *rows,
                 lam[f + 1] *= sc;
             }
             if (P->nf == 3) {
-                real lt3 = lam[f + 2] - ROWV(f + 2) / W[f + 2][f + 2], lim3 = P->mu * N * P->reff;
+                real lt3 = lam[f + 2] - OVERW(ROWV(f + 2), f + 2), lim3 = P->mu * N * P->reff;
                 lam[f + 2] = lt3 > lim3 ? lim3 : (lt3 < -lim3 ? -lim3 : lt3);
             }
         }
     }
 #undef ROWV
+#undef OVERW
 }
 
 static void apply_impulses(const Env *e, Work *w, const Row *rows, int K, const real *lam, real *qd, V6 v0) {

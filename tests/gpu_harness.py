@@ -20,6 +20,16 @@ from thormang_isaacgym_amd.tasks.gogoro_cfg import ASSET_OPTIONS, env_origins, g
 from thormang_isaacgym_amd.tasks.gogoro_draws import post_draws, reset_draws
 
 
+def maxerr(a, b):
+    """max |a - b| over two arrays; inf when either holds a non-finite value
+    (a NaN would otherwise drop out of every max() and comparison here, and
+    a run where both sides blow up would pass)"""
+    a, b = np.asarray(a), np.asarray(b)
+    if not (np.isfinite(a).all() and np.isfinite(b).all()):
+        return float("inf")
+    return float(np.abs(a - b).max()) if a.size else 0.0
+
+
 class NumpyDraws:
     """DrawSource over a seeded numpy generator (U[0,1) and N(0,1), float32)."""
 
@@ -158,8 +168,8 @@ def note_control(err, t, c_obs, c_rew, c_reset, o_obs, o_rew, o_reset, tol=1e-3)
     """The fp32 rounding control's step-t errors against the fp64 oracle
     (maxima in ``obs_f32`` / ``rew_f32``) and its first departure from the
     band, ``ctl_first_bad`` (``within``)."""
-    ce = float(np.abs(c_obs - o_obs).max())
-    cr = float(np.abs(c_rew - o_rew).max())
+    ce = maxerr(c_obs, o_obs)
+    cr = maxerr(c_rew, o_rew)
     err["obs_f32"] = max(err.get("obs_f32", 0.0), ce)
     err["rew_f32"] = max(err.get("rew_f32", 0.0), cr)
     same = bool(np.array_equal(c_reset, o_reset))
@@ -224,17 +234,17 @@ def gogoro_env_vs_oracle(num_envs=64, steps=20, seed=0, policy=None, max_steps=1
         for k, fk in enumerate(f32s):
             f_obs, f_rew, f_reset = fk.step(act[:, 0])[:3]
             dep = err["f32_departures"]
-            if dep[k] is None and (float(np.abs(f_obs - o_obs).max()) > 1e-3 or
-                                   float(np.abs(f_rew - o_rew).max()) > 1e-3 or not np.array_equal(f_reset, o_reset)):
+            if dep[k] is None and (maxerr(f_obs, o_obs) > 1e-3 or
+                                   maxerr(f_rew, o_rew) > 1e-3 or not np.array_equal(f_reset, o_reset)):
                 dep[k] = t
         g_obs = obs_d["obs"].cpu().numpy()
-        e_obs = float(np.abs(g_obs - o_obs).max())
-        e_rew = float(np.abs(rew.cpu().numpy() - o_rew).max())
+        e_obs = maxerr(g_obs, o_obs)
+        e_rew = maxerr(rew.cpu().numpy(), o_rew)
         err["_obs_t"].append(e_obs)
         err["_rew_t"].append(e_rew)
         err["obs"] = max(err["obs"], e_obs)
         err["rew"] = max(err["rew"], e_rew)
-        err["root"] = max(err["root"], float(np.abs(env.root_tensor.cpu().numpy() - orc.a["root"]).max()))
+        err["root"] = max(err["root"], maxerr(env.root_tensor.cpu().numpy(), orc.a["root"]))
         if err["reset_equal"] and not np.array_equal(reset.cpu().numpy(), o_reset):
             err["reset_diff_step"] = t
         err["reset_equal"] &= bool(np.array_equal(reset.cpu().numpy(), o_reset))
@@ -294,12 +304,12 @@ def forced_step_errors(env, orc, act_fn, steps, act_to_orc=lambda a: a, ctl=None
         o_obs, o_rew, o_reset, o_to = orc.step(act_to_orc(act))
         if ctl is not None:
             c_obs, c_rew = ctl.step(act_to_orc(act))[:2]
-            err["obs_f32"] = max(err["obs_f32"], float(np.abs(c_obs - o_obs).max()))
-            err["rew_f32"] = max(err["rew_f32"], float(np.abs(c_rew - o_rew).max()))
+            err["obs_f32"] = max(err["obs_f32"], maxerr(c_obs, o_obs))
+            err["rew_f32"] = max(err["rew_f32"], maxerr(c_rew, o_rew))
         g_obs = obs_d["obs"].cpu().numpy()
-        err["obs"] = max(err["obs"], float(np.abs(g_obs - o_obs).max()))
-        err["rew"] = max(err["rew"], float(np.abs(rew.cpu().numpy() - o_rew).max()))
-        err["root"] = max(err["root"], float(np.abs(env.root_tensor.cpu().numpy() - orc.a["root"]).max()))
+        err["obs"] = max(err["obs"], maxerr(g_obs, o_obs))
+        err["rew"] = max(err["rew"], maxerr(rew.cpu().numpy(), o_rew))
+        err["root"] = max(err["root"], maxerr(env.root_tensor.cpu().numpy(), orc.a["root"]))
         err["reset_equal"] &= bool(np.array_equal(reset.cpu().numpy(), o_reset))
         err["timeout_equal"] &= bool(np.array_equal(extras["time_outs"].cpu().numpy().astype(np.uint8), o_to))
         err["resets"] += int(o_reset.sum())
@@ -368,9 +378,9 @@ def gogoro_terrain(num_envs=64, steps=300, seed=0, max_steps=300, terrain_seed=5
                     err["ties_within_tol"] = bool(np.all(np.abs(roll - 0.30) < tie))
                     err["compared_steps"] = k
                     break
-                err["obs"] = max(err["obs"], float(np.abs(obs_d["obs"].cpu().numpy() - o_obs).max()))
-                err["rew"] = max(err["rew"], float(np.abs(rew.cpu().numpy() - o_rew).max()))
-                err["root"] = max(err["root"], float(np.abs(env.root_tensor.cpu().numpy() - orc.a["root"]).max()))
+                err["obs"] = max(err["obs"], maxerr(obs_d["obs"].cpu().numpy(), o_obs))
+                err["rew"] = max(err["rew"], maxerr(rew.cpu().numpy(), o_rew))
+                err["root"] = max(err["root"], maxerr(env.root_tensor.cpu().numpy(), orc.a["root"]))
                 obs = o_obs.copy()
         err["spawn_z_max"] = float(env.root_reset_tensor[:, 2].max())
         return err
@@ -569,7 +579,7 @@ def walk_env_vs_oracle(num_envs=32, steps=30, seed=0, task="ThormangWalk", dr=Fa
         # the control's own departure from fp64: its reset flags, the first
         # step it leaves 1e-3; and the GPU's distance to the control itself
         err.update(obs_f32=0.0, rew_f32=0.0, ctl_reset_equal=True, gpu_vs_f32=0.0)
-    err["obs0"] = float(np.abs(env.obs_buf.cpu().numpy() - orc.a["obs_buf"]).max())
+    err["obs0"] = maxerr(env.obs_buf.cpu().numpy(), orc.a["obs_buf"])
     for t in range(steps):
         if dr:
             sync_dr(orc, env)
@@ -582,29 +592,29 @@ def walk_env_vs_oracle(num_envs=32, steps=30, seed=0, task="ThormangWalk", dr=Fa
         if ctl is not None:
             c_obs, c_rew, c_reset = ctl.step(act)[:3]
             note_control(err, t, c_obs, c_rew, c_reset, o_obs, o_rew, o_reset)
-            err["gpu_vs_f32"] = max(err["gpu_vs_f32"], float(np.abs(g_obs - c_obs).max()))
+            err["gpu_vs_f32"] = max(err["gpu_vs_f32"], maxerr(g_obs, c_obs))
         for k, fk in enumerate(f32s):
             f_obs, f_rew, f_reset = fk.step(act)[:3]
             dep = err.setdefault("f32_departures", [None] * len(f32s))
-            if dep[k] is None and (float(np.abs(f_obs - o_obs).max()) > 1e-3 or
-                                   float(np.abs(f_rew - o_rew).max()) > 1e-3 or not np.array_equal(f_reset, o_reset)):
+            if dep[k] is None and (maxerr(f_obs, o_obs) > 1e-3 or
+                                   maxerr(f_rew, o_rew) > 1e-3 or not np.array_equal(f_reset, o_reset)):
                 dep[k] = t
         for k, pk in enumerate(perts):
             p_obs, _, p_reset = pk.step(act)[:3]
             dep = err.setdefault("pert_departures", [None] * len(perts))
-            if dep[k] is None and (float(np.abs(p_obs - o_obs).max()) > 1e-3 or
+            if dep[k] is None and (maxerr(p_obs, o_obs) > 1e-3 or
                                    not np.array_equal(p_reset, o_reset)):
                 dep[k] = t
                 err.setdefault("pert_first_bad", t)
-        e_obs = float(np.abs(g_obs - o_obs).max())
+        e_obs = maxerr(g_obs, o_obs)
         if e_obs > 1e-3 and "first_over_tol" not in err:
             err["first_over_tol"] = t
-        e_rew = float(np.abs(rew.cpu().numpy() - o_rew).max())
+        e_rew = maxerr(rew.cpu().numpy(), o_rew)
         err["_obs_t"].append(e_obs)
         err["_rew_t"].append(e_rew)
         err["obs"] = max(err["obs"], e_obs)
         err["rew"] = max(err["rew"], e_rew)
-        err["root"] = max(err["root"], float(np.abs(env.root_tensor.cpu().numpy() - orc.a["root"]).max()))
+        err["root"] = max(err["root"], maxerr(env.root_tensor.cpu().numpy(), orc.a["root"]))
         r_g = reset.cpu().numpy()
         if err["reset_equal"] and not np.array_equal(r_g, o_reset):
             # the first reset-mask disagreement: the envs' termination margins
@@ -617,7 +627,7 @@ def walk_env_vs_oracle(num_envs=32, steps=30, seed=0, task="ThormangWalk", dr=Fa
                                 np.abs(-o_obs[bad, 9] - orc.p.termination_up))
             err.update(reset_diff_step=t, reset_diff_envs=bad.tolist(),
                        reset_diff_margin=[float(x) for x in margin],
-                       reset_diff_obs_err=float(np.abs(g_obs[bad] - o_obs[bad]).max()),
+                       reset_diff_obs_err=maxerr(g_obs[bad], o_obs[bad]),
                        reset_diff_tie=bool(np.all(margin < 1e-3)))
         err["reset_equal"] &= bool(np.array_equal(r_g, o_reset))
         err["timeout_equal"] &= bool(np.array_equal(extras["time_outs"].cpu().numpy().astype(np.uint8), o_to))

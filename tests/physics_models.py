@@ -110,3 +110,27 @@ def landing_checks(zs, vs, rest_offset=0.0, half=0.05):
                      out["max_up_velocity"] < 0.02 and out["min_height"] > -0.002 and
                      abs(out["final_height"]) < 5e-4 and abs(out["final_vz"]) < 1e-3)
     return out
+
+
+def jit_walker():
+    """A URDF that is not compiled into libtgsim.so (run-time load_asset /
+    tg_model_jit test): a box torso with two legs, hips driven, one knee
+    locked, sphere feet and a box body shape."""
+    from thormang_isaacgym_amd.model.kat_models import _inertial, urdf_model
+    from thormang_isaacgym_amd.model.urdf import Shape
+    eye = np.eye(3).tolist()
+    legs = ""
+    for side, y in (("l", 0.12), ("r", -0.12)):
+        legs += (f'<link name="{side}_thigh">{_inertial(0.8, (0, 0, -0.15), (0.006, 0.006, 0.001))}</link>'
+                 f'<link name="{side}_shin">{_inertial(0.5, (0, 0, -0.12), (0.003, 0.003, 0.0005))}</link>'
+                 f'<joint name="{side}_hip" type="revolute"><parent link="torso"/><child link="{side}_thigh"/>'
+                 f'<origin xyz="0 {y} -0.1" rpy="0.05 0 0"/><axis xyz="0 1 0"/>'
+                 '<limit lower="-1.2" upper="1.2" effort="80" velocity="10"/></joint>'
+                 f'<joint name="{side}_knee" type="revolute"><parent link="{side}_thigh"/><child link="{side}_shin"/>'
+                 '<origin xyz="0 0 -0.3"/><axis xyz="0 1 0"/>'
+                 '<limit lower="-0.5" upper="1.5" effort="80" velocity="10"/></joint>')
+    shapes = [Shape("box", "torso", [0, 0, 0], eye, [0.12, 0.18, 0.1], 0.9),
+              Shape("sphere", "l_shin", [0, 0, -0.26], eye, [0.04], 1.0),
+              Shape("sphere", "r_shin", [0, 0, -0.26], eye, [0.04], 1.0)]
+    return urdf_model("jit_walker", f'<link name="torso">{_inertial(4.0, (0, 0, 0.02), (0.05, 0.04, 0.03))}</link>'
+                      + legs, shapes, locked=["r_knee"])

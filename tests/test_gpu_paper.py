@@ -14,6 +14,7 @@ import numpy as np
 import pytest
 import torch
 from tests.gpu_harness import within
+from tests.gpu_harness import maxerr
 
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
@@ -80,7 +81,7 @@ def test_gpu_paper_kernels_replay_reference(name):
         np.testing.assert_array_equal(env.steer_delay.cpu().numpy(), f["steer_delay"][t])
         np.testing.assert_allclose(env.head_perturbation.cpu().numpy(), f["perturbation"][t], atol=2e-5)
         np.testing.assert_allclose(env.root_tensor.cpu().numpy(), f["root_after"][t], atol=1e-6)
-        err = max(err, float(np.abs(obs["obs"].cpu().numpy() - f["obs"][t]).max()))
+        err = max(err, maxerr(obs["obs"].cpu().numpy(), f["obs"][t]))
     assert src.i == len(f["draw_kind"])
     print(name, "max obs err", err)
 
@@ -122,10 +123,10 @@ def _env_vs_oracle(sw, n=64, steps=80, seed=3, forced=False):
             ctl.pre(act[:, 0])
             ctl.physics()
             c_obs, c_rew = ctl.post()[:2]
-            err["obs_f32"] = max(err["obs_f32"], float(np.abs(c_obs - o_obs).max()))
-            err["rew_f32"] = max(err["rew_f32"], float(np.abs(c_rew - o_rew).max()))
-        err["obs"] = max(err["obs"], float(np.abs(od["obs"].cpu().numpy() - o_obs).max()))
-        err["rew"] = max(err["rew"], float(np.abs(rew.cpu().numpy() - o_rew).max()))
+            err["obs_f32"] = max(err["obs_f32"], maxerr(c_obs, o_obs))
+            err["rew_f32"] = max(err["rew_f32"], maxerr(c_rew, o_rew))
+        err["obs"] = max(err["obs"], maxerr(od["obs"].cpu().numpy(), o_obs))
+        err["rew"] = max(err["rew"], maxerr(rew.cpu().numpy(), o_rew))
         err["reset_equal"] &= bool(np.array_equal(reset.cpu().numpy(), o_reset))
         err["timeout_equal"] &= bool(np.array_equal(ex["time_outs"].cpu().numpy().astype(np.uint8), o_to))
         err["resets"] += int(o_reset.sum())

@@ -12,28 +12,7 @@ from thormang_isaacgym_amd.abi import TG_PROP_DAMPING, TG_PROP_DRIVE_MODE, TG_PR
 pytestmark = pytest.mark.gpu
 
 
-def jit_walker():
-    """A URDF that is not compiled into libtgsim.so (run-time load_asset /
-    tg_model_jit test): a box torso with two legs, hips driven, one knee
-    locked, sphere feet and a box body shape."""
-    from thormang_isaacgym_amd.model.kat_models import _inertial, urdf_model
-    from thormang_isaacgym_amd.model.urdf import Shape
-    eye = np.eye(3).tolist()
-    legs = ""
-    for side, y in (("l", 0.12), ("r", -0.12)):
-        legs += (f'<link name="{side}_thigh">{_inertial(0.8, (0, 0, -0.15), (0.006, 0.006, 0.001))}</link>'
-                 f'<link name="{side}_shin">{_inertial(0.5, (0, 0, -0.12), (0.003, 0.003, 0.0005))}</link>'
-                 f'<joint name="{side}_hip" type="revolute"><parent link="torso"/><child link="{side}_thigh"/>'
-                 f'<origin xyz="0 {y} -0.1" rpy="0.05 0 0"/><axis xyz="0 1 0"/>'
-                 '<limit lower="-1.2" upper="1.2" effort="80" velocity="10"/></joint>'
-                 f'<joint name="{side}_knee" type="revolute"><parent link="{side}_thigh"/><child link="{side}_shin"/>'
-                 '<origin xyz="0 0 -0.3"/><axis xyz="0 1 0"/>'
-                 '<limit lower="-0.5" upper="1.5" effort="80" velocity="10"/></joint>')
-    shapes = [Shape("box", "torso", [0, 0, 0], eye, [0.12, 0.18, 0.1], 0.9),
-              Shape("sphere", "l_shin", [0, 0, -0.26], eye, [0.04], 1.0),
-              Shape("sphere", "r_shin", [0, 0, -0.26], eye, [0.04], 1.0)]
-    return urdf_model("jit_walker", f'<link name="torso">{_inertial(4.0, (0, 0, 0.02), (0.05, 0.04, 0.03))}</link>'
-                      + legs, shapes, locked=["r_knee"])
+from tests.physics_models import jit_walker  # noqa: E402  (the run-time URDF's model)
 
 
 def gpu_sim(model, sp, n, root, dof, props, pt, vt):
@@ -64,10 +43,18 @@ def side_by_side(model, steps, n=16, seed=0, setup=None, **simkw):
         gr = g.root_state.cpu().numpy()
         gd = g.dof_state.cpu().numpy()
         scale = max(1.0, float(np.abs(root).max()))
-        worst = max(worst, float(np.abs(gr - root).max()) / scale)
+        worst = max(worst, _maxerr(gr, root) / scale)
         if dof.size:
-            worst = max(worst, float(np.abs(gd - dof).max()) / scale)
+            worst = max(worst, _maxerr(gd, dof) / scale)
     return worst, g, root, dof
+
+
+def _maxerr(a, b):
+    """max |a - b|, inf when either side is not finite (a NaN would otherwise
+    vanish in max(), and a run where both sides blow up would pass)"""
+    if not (np.isfinite(a).all() and np.isfinite(b).all()):
+        return float("inf")
+    return float(np.abs(a - b).max())
 
 
 def _spin(rs, root, dof, props, pt, vt):
@@ -98,7 +85,7 @@ def test_gpu_matches_oracle_on_kat_models(name):
             pt[:, 0] = rs.uniform(-0.5, 0.5, pt.shape[0])
     worst, *_ = side_by_side(m, 100, setup=setup, **kw)
     print({"model": name, "worst_state_err": worst})
-    assert worst < 2e-3, worst
+    assert worst < 1e-3, worst
 
 
 @pytest.mark.parametrize("solver", [0, 1])
@@ -117,7 +104,7 @@ def test_gpu_contact_matches_oracle_and_rests(shape, solver):
     gr = g.root_state.cpu().numpy()
     print({"shape": shape, "solver": solver, "worst_state_err": worst, "rest_err": float(np.abs(gr[:, 2] - z_rest).max())})
     assert np.abs(gr[:, 2] - z_rest).max() < 3e-3
-    assert worst < 5e-3, worst
+    assert worst < 1e-3, worst
 
 
 @pytest.mark.parametrize("solver,viters,rest", [(1, 1, 0.0), (1, 4, 0.002), (0, 1, 0.0)])
@@ -265,9 +252,12 @@ def test_gpu_runtime_loaded_model_matches_oracle():
         dof.reshape(n, -1, 2)[:, k, 0] = 0.30005
         dof.reshape(n, -1, 2)[:, dl["r_hip"], 1] = rs.normal(0, 2, n)
 
-    worst, g, *_ = side_by_side(m, 150, n=32, setup=setup, dt=0.01, substeps=2, fix_base_link=True)
+    worst, g, _, dof = side_by_side(m, 150, n=32, setup=setup, dt=0.01, substeps=2, fix_base_link=True)
     assert g.jit, "expected a run-time specialisation"
-    assert worst < 2e-3, worst
+    moved = float(np.abs(dof.reshape(32, -1, 2)[:, dl["l_hip"], 0]).max())
+    print({"runtime_model_worst_state_err": worst, "l_hip_max_abs_q": moved})
+    assert moved > 0.05, moved          # the drives moved the legs (the comparison is not of a still body)
+    assert worst < 1e-3, worst
 
 
 @pytest.mark.parametrize("name", ["kat_box", "thormang"])
@@ -355,9 +345,9 @@ def test_gpu_native_urdf_load_through_the_c_abi_alone():
     for _ in range(40):
         physics_step(desc, sp, root, dof, props, pt, vt)
         g.simulate()
-        worst = max(worst, float(np.abs(g.root_state.cpu().numpy() - root).max()),
-                    float(np.abs(g.dof_state.cpu().numpy() - dof).max()))
-    assert np.isfinite(worst) and worst < 2e-3, worst
+        worst = max(worst, _maxerr(g.root_state.cpu().numpy(), root), _maxerr(g.dof_state.cpu().numpy(), dof))
+    print({"native_urdf_worst_state_err": worst})
+    assert np.isfinite(worst) and worst < 1e-3, worst
 
 
 def test_gpu_solver_type_switches_at_runtime():
@@ -389,8 +379,10 @@ def test_gpu_solver_type_switches_at_runtime():
         physics_step(desc, so, r, d, props, pt, vt)
         g.simulate()
         gr = g.root_state.cpu().numpy()
-        assert np.abs(gr[:, :7] - r[:, :7]).max() < 1e-4, solver
-        assert np.abs(gr[:, 7:] - r[:, 7:]).max() < 5e-3, solver
+        print({"solver": solver, "pose_err": float(np.abs(gr[:, :7] - r[:, :7]).max()),
+               "vel_err": float(np.abs(gr[:, 7:] - r[:, 7:]).max())})
+        assert _maxerr(gr[:, :7], r[:, :7]) < 1e-4, solver
+        assert _maxerr(gr[:, 7:], r[:, 7:]) < 1e-3, solver
         after.setdefault(solver, (r0, gr.copy()))
     # the same start state under the other solver differs
     r0, g0 = after[0]

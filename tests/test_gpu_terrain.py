@@ -9,6 +9,7 @@ import torch
 from tests import physics_models as pm
 from tests.oracle_lib import physics_step, set_heightfield
 from tests.gpu_harness import within
+from tests.gpu_harness import maxerr
 
 pytestmark = pytest.mark.gpu
 
@@ -63,8 +64,8 @@ def test_gpu_terrain_contact_matches_oracle(shape):
             physics_step(desc, sp, r, d, props, pt, vt)
             g.simulate()
             gr = g.root_state.cpu().numpy()
-            pose_err = max(pose_err, float(np.abs(gr[:, :7] - r[:, :7]).max()))
-            vel_err = max(vel_err, float(np.abs(gr[:, 7:] - r[:, 7:]).max()))
+            pose_err = max(pose_err, maxerr(gr[:, :7], r[:, :7]))
+            vel_err = max(vel_err, maxerr(gr[:, 7:], r[:, 7:]))
     finally:
         set_heightfield(None)
     print(shape, "pose", pose_err, "vel", vel_err)
@@ -145,14 +146,14 @@ def test_gpu_gogoro_terrain_step_matches_oracle_along_300_steps():
 
 
 def test_gpu_gogoro_terrain_free_running_matches_oracle():
-    """Free-running fp32 GPU vs fp64 oracle on the Perlin terrain.  The
-    heightfield is piecewise planar, so a ~1e-4 state difference can put a
-    tyre's support point on the other side of a triangle edge for one step
-    (the contact normal jumps) and the difference spikes before the two
-    trajectories re-converge: seed 6 shows one env at one step at 1.26e-3
-    (scripts/terrain_free_drift.py), while the teacher-forced one-step errors
-    along the same start stay below 1.1e-4 (next test).  Hence the free-running
-    bound is 2e-3.  Resets must agree on every step, except a threshold tie: an
+    """Free-running fp32 GPU vs fp64 oracle on the Perlin terrain, at
+    north_star's 1e-3.  The heightfield is piecewise planar, so a small state
+    difference can put a tyre's support point on the other side of a triangle
+    edge for one step (the contact normal jumps): round 3 measured a 1.26e-3
+    spike on this seed (scripts/terrain_free_drift.py) and bounded the run at
+    2e-3; since round 4's TGS conditioning fixes the run stays at 5e-5 (round
+    5, profiles/r5/gpu_tests.log), so the bar is the strict one again.
+    Resets must agree on every step, except a threshold tie: an
     env whose clean roll lies within 1e-3 of the 0.30 fall threshold may fall
     one step apart (seed 6, step 27: |roll| = 0.30 +- 4.5e-5); the comparison
     ends there, because the reset draws then desynchronise the streams."""
@@ -160,7 +161,7 @@ def test_gpu_gogoro_terrain_free_running_matches_oracle():
     from tests.gpu_harness import gogoro_terrain
     err = gogoro_terrain(num_envs=64, steps=60, seed=6, forced=False)
     print(err)
-    assert within(err, tol=2e-3) and within(err, "rew", tol=2e-3), err
+    assert within(err) and within(err, "rew"), err
     assert err["reset_equal"] or err["ties_within_tol"], err
     assert err["compared_steps"] >= 25, err
 

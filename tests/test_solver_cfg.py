@@ -210,3 +210,22 @@ def test_tgs_without_velocity_iterations_stores_the_bias():
     z1, v1 = pm.drop_box(1, viters=1, steps=120)
     assert abs(z0[-1] - z0[-20]) < 1e-6 and 1e-3 < v0[-1] < 1e-2, (z0[-1], v0[-1])
     assert abs(v1[-1]) < 1e-3, v1[-1]
+
+
+@pytest.mark.parametrize("solver", [0, 1])
+def test_rows_on_a_fixed_base_take_no_impulse(solver):
+    """A shape on a fixed base has no contact response (its Delassus diagonal
+    is 0): its rows must take no impulse rather than divide by zero -- a
+    fixed-base torso pushed 3 cm into the ground stays where it is, its legs
+    swing, everything finite
+    (round 5: the 1/W of such rows made every state NaN, in the oracle and
+    the kernel, for any fixed-base model with a shape on its root)."""
+    m = pm.jit_walker()   # a box torso (the root) on two legs
+    desc, sp, root, dof, props, pt, vt = pm.sim(m, n=2, dt=0.01, substeps=2, solver_type=solver, fix_base_link=True)
+    root[:, 2] = 0.02   # the torso box's half height is 0.05: 3 cm into the plane
+    r0 = root.copy()
+    for _ in range(5):
+        physics_step(desc, sp, root, dof, props, pt, vt)
+    assert np.isfinite(root).all() and np.isfinite(dof).all()
+    np.testing.assert_array_equal(root, r0)
+    assert np.abs(dof[:, 1]).max() > 0   # the legs swing under gravity

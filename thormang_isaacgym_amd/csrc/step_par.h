@@ -492,6 +492,11 @@ template <int L> __device__ __forceinline__ float env_bcast(float v, int n, int 
 // the partner lane's value (lane pairs sub, sub + 8 of a 16-lane row)
 __device__ __forceinline__ float pair_swap(float v) { return dpp<0x128>(v); }
 
+// a contact row's inverse Delassus diagonal; a row with no response (its
+// shape on a fixed base) gets 0, so it takes no impulse (1/0 would be inf,
+// and inf * 0 NaN, in every sweep)
+__device__ __forceinline__ float inv_diag(float w) { return w > 0.f ? 1.0f / w : 0.f; }
+
 #define TG_SYNC()                                          \
     do {                                                   \
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); \
@@ -2437,7 +2442,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
 #pragma unroll
                 for (int i = 0; i < K; ++i) {
                     if constexpr (!T) tg[i] = s(PL::ROW + i * 8 + 6);   // the target (0 on friction rows)
-                    wd[i] = 1.0f / s(PL::W + i * K + i);   // (the inverse diagonal, formed once)
+                    wd[i] = inv_diag(s(PL::W + i * K + i));   // (the inverse diagonal, formed once)
                     lam[i] = 0.f;
                     if constexpr (T) lbar[i] = 0.f;
                 }
@@ -2601,7 +2606,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     lbar[i] = 0.f;
                     tg[i] = (tgs && row_normal<M>(i)) ? contact_target(a, phi[i], hs) : phi[i];
                     onr[i] = s(PL::ROW + i * 8 + 7);
-                    wd[i] = 1.0f / s(PL::W + i * K + i);   // (the inverse diagonal, formed once)
+                    wd[i] = inv_diag(s(PL::W + i * K + i));   // (the inverse diagonal, formed once)
                     lam[i] = 0.f;
                 }
 #pragma unroll
