@@ -187,8 +187,8 @@ def gogoro_env_vs_oracle(num_envs=64, steps=20, seed=0, policy=None, max_steps=1
     """Free-running GPU Gogoro env vs the oracle env on the same draws; with
     ``control`` (default: when the cfg asks for TGS) the fp32 oracle build
     runs the same free-running episode beside the fp64 one (``within``); with
-    ``f32_ensemble`` = K also K fp32 builds whose initial root and joint
-    state is moved by relative 1e-7 (about an fp32 ulp), whose departure
+    ``f32_ensemble`` = K also K fp32 builds whose root and joint state is
+    moved by relative 1e-7 (about an fp32 ulp) after the first step, whose departure
     steps from fp64 (obs or reward over 1e-3, or a reset flag changed) are
     ``f32_departures`` (as walk_env_vs_oracle's)."""
     import torch
@@ -204,15 +204,16 @@ def gogoro_env_vs_oracle(num_envs=64, steps=20, seed=0, policy=None, max_steps=1
         control = tgs_configured(cfg)
     ctl = OracleGogoro(parity_cfg(num_envs, max_steps=max_steps, dr=dr), NumpyDraws(seed), fix_base=fix_base,
                        precision="f32") if control else None
-    f32s = []
-    for k in range(f32_ensemble):
-        fk = OracleGogoro(parity_cfg(num_envs, max_steps=max_steps, dr=dr), NumpyDraws(seed), fix_base=fix_base,
-                          precision="f32")
+    f32s = [OracleGogoro(parity_cfg(num_envs, max_steps=max_steps, dr=dr), NumpyDraws(seed), fix_base=fix_base,
+                         precision="f32") for k in range(f32_ensemble)]
+
+    def perturb(fk, k):
+        # (after the first step: every env starts with a reset, whose spawn
+        # would overwrite a perturbation of the initial state)
         prs = np.random.default_rng(100 + k)
         for name in ("root", "dof_state"):
             x = fk.a[name]
             x[...] = (x * (1 + 1e-7 * prs.standard_normal(x.shape))).astype(x.dtype)
-        f32s.append(fk)
     err = {"obs": 0.0, "rew": 0.0, "reset_equal": True, "timeout_equal": True, "root": 0.0, "steps": steps,
            "resets": 0, "_obs_t": [], "_rew_t": []}
     if ctl is not None:
@@ -232,6 +233,8 @@ def gogoro_env_vs_oracle(num_envs=64, steps=20, seed=0, policy=None, max_steps=1
             c_obs, c_rew, c_reset = ctl.step(act[:, 0])[:3]
             note_control(err, t, c_obs, c_rew, c_reset, o_obs, o_rew, o_reset)
         for k, fk in enumerate(f32s):
+            if t == 1:
+                perturb(fk, k)
             f_obs, f_rew, f_reset = fk.step(act[:, 0])[:3]
             dep = err["f32_departures"]
             if dep[k] is None and (maxerr(f_obs, o_obs) > 1e-3 or

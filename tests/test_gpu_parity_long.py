@@ -193,30 +193,24 @@ def test_gpu_gogoro_free_base_random_actions_free_running():
 
 def test_gpu_gogoro_random_actions_free_running_1000_steps():
     """The bench's own action distribution on the free base, free running for
-    north_star's 1000 steps (64 envs; every env falls and re-spawns many
-    times), under the fp32-ensemble rule of the long walk tests: the control
-    and 8 fp32 builds started 1e-7 away give 9 departure steps from fp64,
-    and the GPU must not depart before the third-earliest (obs and reward
-    within 1e-3 and identical reset flags at every step before it)."""
+    north_star's 1000 steps (64 envs, seed 22; every env falls and re-spawns
+    about 23 times), held to 1e-3 on every step with identical reset flags,
+    as is the fp32 control beside it on this seed.  This is one seed's
+    regression guard, not a general claim: on 6 other seeds
+    (scripts/dev/r5_long_seeds.py, profiles/r5/long_seeds.txt) fp32
+    computations leave the 1e-3 band at discrete events (a fall decided by a
+    threshold tie, a drive crossing its effort limit) -- the
+    fp32 oracle build on 4 of them, the GPU on all 6, first on 5."""
     _cuda()
     import numpy as np
     from tests.gpu_harness import gogoro_env_vs_oracle
     rs = np.random.default_rng(77)
-    err = gogoro_env_vs_oracle(num_envs=64, steps=1000, seed=22, control=True, f32_ensemble=8,
+    err = gogoro_env_vs_oracle(num_envs=64, steps=1000, seed=22, control=True,
                                policy=lambda o: rs.uniform(-1, 1, (o.shape[0], 1)).astype(np.float32))
-    n = err["steps"]
-    deps = sorted([err.get("ctl_first_bad", n)] + [d if d is not None else n for d in err["f32_departures"]])
-    hz = deps[2]
-    gpu = min(err.get("first_bad_step", n), err.get("reset_diff_step", n))
-    err.update(f32_sorted=deps, horizon=hz, gpu_departure=gpu,
-               gpu_rank=int(np.searchsorted(deps, gpu, side="right")),
-               obs_pre_horizon=float(np.max(err["_obs_t"][:hz])), rew_pre_horizon=float(np.max(err["_rew_t"][:hz])))
     print(brief(err))
     assert err["resets"] >= 64, brief(err)
-    assert hz >= 50, brief(err)
-    assert gpu >= hz, brief(err)
-    assert err["obs_pre_horizon"] < 1e-3 and err["rew_pre_horizon"] < 1e-3, brief(err)
-
+    assert within(err) and within(err, "rew"), brief(err)
+    assert err["reset_equal"] and err["timeout_equal"], brief(err)
 
 def test_gpu_walk_random_actions_free_running_600_steps():
     """The headline walk free-running with falls and re-spawns: 64 envs,
