@@ -61,7 +61,9 @@ def test_gpu_walk_random_actions_free_running_1000_steps():
     must not depart before the third-earliest (obs and reward within 1e-3,
     identical reset flags, at every step before it).  The steps after it are
     reported, not asserted (round 4's drift study: the GPU leaves 1e-3 at
-    step 723, the fp32 build at 320; profiles/r4/drift_walk_root_relative.txt)."""
+    step 723, the fp32 build at 320; profiles/r4/drift_walk_root_relative.txt).
+    A single-seed regression guard: on other seeds the GPU's departure ranks
+    anywhere among the fp32 evaluations' (profiles/r5/long_seeds.txt)."""
     _cuda()
     import numpy as np
     from tests.gpu_harness import walk_env_vs_oracle
@@ -86,7 +88,8 @@ def test_gpu_walk_dr_pushes_free_running_1000_steps():
     (test_gpu_walk_random_actions_free_running_1000_steps): the GPU must not
     depart from the fp64 reference (obs or reward over 1e-3, or a reset flag
     changed) before the third-earliest of 9 fp32 evaluations of the same
-    episode (the control and 8 fp32 builds started 1e-7 away)."""
+    episode (the control and 8 fp32 builds started 1e-7 away).  A single-seed
+    regression guard (other seeds: profiles/r5/long_seeds.txt)."""
     _cuda()
     import numpy as np
     from tests.gpu_harness import walk_env_vs_oracle
