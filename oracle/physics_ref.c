@@ -843,8 +843,11 @@ static int collect_rows(const Env *e, Work *w, real h, const V6 *vg, Row *rows, 
 static void pgs_sweeps(int K, int npatch, const Patch *patches, const Row *rows, const real *target,
                        real (*W)[3 * MAXC], const real *vfree, real *lam, int iters) {
 #define ROWV(i) ({ real v_ = vfree[i]; for (int j_ = 0; j_ < K; ++j_) v_ += W[i][j_] * lam[j_]; v_; })
-    /* a row with no response (its shape on a fixed base) takes no impulse */
-#define OVERW(x, i) (W[i][i] > 0 ? (x) / W[i][i] : 0)
+    /* a row with no response (a shape on a fixed base, a normal row through a
+     * fixed-base scooter's wheel) takes no impulse; real rows have W_ii of
+     * 1e-3 .. 1e1, the threshold only catches rounding residue (the kernel's
+     * inv_diag) */
+#define OVERW(x, i) (W[i][i] > 1e-9 ? (x) / W[i][i] : 0)
     for (int it = 0; it < iters; ++it) {
         for (int p = 0; p < npatch; ++p) {
             const Patch *P = &patches[p];
