@@ -492,12 +492,12 @@ template <int L> __device__ __forceinline__ float env_bcast(float v, int n, int 
 // the partner lane's value (lane pairs sub, sub + 8 of a 16-lane row)
 __device__ __forceinline__ float pair_swap(float v) { return dpp<0x128>(v); }
 
-// a contact row's inverse Delassus diagonal; a row with no response gets 0,
-// so it takes no impulse (1/0 would be inf, and inf * 0 NaN, in every sweep):
-// a shape on a fixed base, or a normal row through a wheel of a fixed-base
-// scooter (the wheel spins along the tangent only).  Real rows have W_ii of
-// 1e-3 .. 1e1 (inverse effective masses); 1e-9 only catches rounding residue.
-__device__ __forceinline__ float inv_diag(float w) { return w > 1e-9f ? 1.0f / w : 0.f; }
+// a contact row without response: its Delassus diagonal at most this (real
+// rows have 1e-3 .. 1e1, inverse effective masses; this only catches the
+// rounding residue of an exact 0)
+#define TG_W_DEAD 1e-9f
+// (the 8-lane PGS's inverse diagonal: 0 for such a row, no impulse)
+__device__ __forceinline__ float inv_diag(float w) { return w > TG_W_DEAD ? 1.0f / w : 0.f; }
 
 #define TG_SYNC()                                          \
     do {                                                   \
@@ -2354,6 +2354,13 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 }
 #pragma unroll
                 for (int i = 0; i < K; ++i) s(PL::W + i * K + j) = rvel(i, dvc[M::shape_cg[row_shape<M>(i)]]);
+                // a row with no response (W_jj ~ 0: a shape on a fixed base, a
+                // normal row through a fixed-base scooter's wheel) gets a huge
+                // diagonal, so the sweeps give it a multiplier ~1e-30 times its
+                // target -- no impulse -- instead of 1/0 and then inf * 0 = NaN
+                // (the oracle's OVERW gives it exactly 0).  Off the sweeps'
+                // register peak: a guard there cost 1-5 %.
+                if (!(s(PL::W + j * K + j) > TG_W_DEAD)) s(PL::W + j * K + j) = 1e30f;
             }
             TG_SYNC();
             if constexpr (PL::WOOD) {
@@ -2415,13 +2422,8 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             // vector in registers, no LDS traffic in the sweeps)
             // (instantiated per solver: the PGS build carries none of the TGS
             // state -- one more live array in this section cost the walk 1 us)
-            // (instantiated per base too: only a fixed base can leave a row
-            // without response -- a free one moves along every row -- so only
-            // the fixed-base instantiation carries inv_diag's guard, and the
-            // free-base code is the unguarded one, register allocation included)
-            auto pgs16 = [&](auto TC, auto FBC) {
+            auto pgs16 = [&](auto TC) {
                 constexpr bool T = decltype(TC)::value != 0;
-                constexpr bool FB = decltype(FBC)::value != 0;
                 constexpr int JL = (K + LPE - 1) / LPE;
                 constexpr int JT = T ? JL : 1, KT = T ? K : 1;
                 // (the lane's own rows: W rows, velocities, targets; TGS: their
@@ -2449,8 +2451,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
 #pragma unroll
                 for (int i = 0; i < K; ++i) {
                     if constexpr (!T) tg[i] = s(PL::ROW + i * 8 + 6);   // the target (0 on friction rows)
-                    // (the inverse diagonal, formed once)
-                    wd[i] = FB ? inv_diag(s(PL::W + i * K + i)) : 1.0f / s(PL::W + i * K + i);
+                    wd[i] = 1.0f / s(PL::W + i * K + i);   // (the inverse diagonal, formed once)
                     lam[i] = 0.f;
                     if constexpr (T) lbar[i] = 0.f;
                 }
@@ -2587,13 +2588,8 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     for (int i = 0; i < K; ++i) s(PL::LAM + i) = lam[i];
                 }
             };
-            if (fix_base) {
-                if (tgs) pgs16(IntC<1>{}, IntC<1>{});
-                else pgs16(IntC<0>{}, IntC<1>{});
-            } else {
-                if (tgs) pgs16(IntC<1>{}, IntC<0>{});
-                else pgs16(IntC<0>{}, IntC<0>{});
-            }
+            if (tgs) pgs16(IntC<1>{});
+            else pgs16(IntC<0>{});
             } else {   // 8-lane envs: the row velocity by an 8-lane reduction (two broadcasts
                        // and a select measured slower than the three DPP levels; W and the
                        // row velocities in every lane, kept incrementally as for 16 lanes:
