@@ -110,7 +110,7 @@ def _env_vs_oracle(sw, n=64, steps=80, seed=3, forced=False):
     if forced:
         from tests.gpu_harness import forced_step_errors
         return forced_step_errors(env, orc, lambda o: rs.uniform(-1, 1, (n, 1)).astype(np.float32), steps, ctl=ctl)
-    err = {"obs": 0.0, "rew": 0.0, "reset_equal": True, "timeout_equal": True, "resets": 0}
+    err = {"obs": 0.0, "rew": 0.0, "reset_equal": True, "timeout_equal": True, "resets": 0, "root": 0.0, "dof": 0.0}
     if ctl is not None:
         err["obs_f32"] = err["rew_f32"] = 0.0
     for t in range(steps):
@@ -130,6 +130,10 @@ def _env_vs_oracle(sw, n=64, steps=80, seed=3, forced=False):
         err["reset_equal"] &= bool(np.array_equal(reset.cpu().numpy(), o_reset))
         err["timeout_equal"] &= bool(np.array_equal(ex["time_outs"].cpu().numpy().astype(np.uint8), o_to))
         err["resets"] += int(o_reset.sum())
+        # the whole simulated state too, not only what the observations see
+        # (round 5: a fixed-base wheel ran away unseen by obs and reward)
+        err["root"] = max(err["root"], maxerr(env.sim.root_state.cpu().numpy(), orc.a["root"]))
+        err["dof"] = max(err["dof"], maxerr(env.sim.dof_state.cpu().numpy()[:, 0], orc.a["dof_state"][:, 0]))
     return err
 
 
@@ -140,6 +144,7 @@ def test_gpu_paper_env_matches_oracle_fixed_base():
     print(err)
     assert within(err) and within(err, "rew"), err
     assert err["reset_equal"] and err["timeout_equal"], err
+    assert err["root"] < 1e-3 and err["dof"] < 1e-3, err   # the joints too (a wheel ran away unseen, round 5)
 
 
 def test_gpu_paper_fixed_base_free_running_1000_steps():
@@ -152,6 +157,7 @@ def test_gpu_paper_fixed_base_free_running_1000_steps():
     assert err["resets"] >= 64 * 16, err     # every env re-spawned along the way
     assert within(err) and within(err, "rew"), err
     assert err["reset_equal"] and err["timeout_equal"], err
+    assert err["root"] < 1e-3 and err["dof"] < 1e-3, err
 
 
 FLIPPED = dict(DEBUGFIXBASE=False, USE_STEER_DELAY=True, RANDOM_DAMPING=True, CENTER_ROBOT=False)
@@ -167,6 +173,7 @@ def test_gpu_paper_env_matches_oracle_free_base_flags_flipped():
     print(err)
     assert within(err) and within(err, "rew"), err
     assert err["reset_equal"] and err["timeout_equal"], err
+    assert err["root"] < 1e-3 and err["dof"] < 1e-3, err
 
 
 def test_gpu_paper_free_base_step_matches_oracle_along_300_steps():
