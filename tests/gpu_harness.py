@@ -30,6 +30,16 @@ def maxerr(a, b):
     return float(np.abs(a - b).max()) if a.size else 0.0
 
 
+def maxrel(a, b):
+    """max |a - b| / max(1, |b|): the error measure for unbounded
+    coordinates (a continuous wheel's angle grows by tens of radians over
+    1000 steps and carries the fp32 ulp of its magnitude)"""
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    if not (np.isfinite(a).all() and np.isfinite(b).all()):
+        return float("inf")
+    return float((np.abs(a - b) / np.maximum(1.0, np.abs(b))).max()) if a.size else 0.0
+
+
 class NumpyDraws:
     """DrawSource over a seeded numpy generator (U[0,1) and N(0,1), float32)."""
 
@@ -248,6 +258,10 @@ def gogoro_env_vs_oracle(num_envs=64, steps=20, seed=0, policy=None, max_steps=1
         err["obs"] = max(err["obs"], e_obs)
         err["rew"] = max(err["rew"], e_rew)
         err["root"] = max(err["root"], maxerr(env.root_tensor.cpu().numpy(), orc.a["root"]))
+        q_g, q_o = env.sim.dof_state.cpu().numpy()[:, 0], orc.a["dof_state"][:, 0]
+        err["dof"] = max(err.get("dof", 0.0), maxerr(q_g, q_o))
+        err["dof_rel"] = max(err.get("dof_rel", 0.0), maxrel(q_g, q_o))
+        err["dof_abs_max"] = max(err.get("dof_abs_max", 0.0), float(np.abs(q_o).max()))
         if err["reset_equal"] and not np.array_equal(reset.cpu().numpy(), o_reset):
             err["reset_diff_step"] = t
         err["reset_equal"] &= bool(np.array_equal(reset.cpu().numpy(), o_reset))
@@ -618,6 +632,10 @@ def walk_env_vs_oracle(num_envs=32, steps=30, seed=0, task="ThormangWalk", dr=Fa
         err["obs"] = max(err["obs"], e_obs)
         err["rew"] = max(err["rew"], e_rew)
         err["root"] = max(err["root"], maxerr(env.root_tensor.cpu().numpy(), orc.a["root"]))
+        q_g, q_o = env.sim.dof_state.cpu().numpy()[:, 0], orc.a["dof_state"][:, 0]
+        err["dof"] = max(err.get("dof", 0.0), maxerr(q_g, q_o))
+        err["dof_rel"] = max(err.get("dof_rel", 0.0), maxrel(q_g, q_o))
+        err["dof_abs_max"] = max(err.get("dof_abs_max", 0.0), float(np.abs(q_o).max()))
         r_g = reset.cpu().numpy()
         if err["reset_equal"] and not np.array_equal(r_g, o_reset):
             # the first reset-mask disagreement: the envs' termination margins
