@@ -27,6 +27,39 @@ __device__ __forceinline__ V3 mul(const M3 &m, V3 v) {
     return V3{m.a[0] * v.x + m.a[1] * v.y + m.a[2] * v.z, m.a[3] * v.x + m.a[4] * v.y + m.a[5] * v.z,
               m.a[6] * v.x + m.a[7] * v.y + m.a[8] * v.z};
 }
+#ifndef TG_PK
+#define TG_PK 0   // developer switch, measured off (round 5, profiles/r5/packed_m3_static.txt)
+#endif
+#if TG_PK
+// packed FP32 (v_pk_mul_f32 / v_pk_fma_f32, two products in one VALU issue):
+// a row-major row pair times a broadcast scalar (op_sel picks the scalar's
+// half); the same products and contraction order as the scalar forms, so the
+// results are bit-identical.  Off: on the walk kernel it turns 316 scalar
+// multiply-adds into 159 packed ones but adds 211 v_mov_b32 (the M3 values
+// live in arbitrary registers, a packed operand needs an aligned pair), net
+// +114 VALU instructions
+typedef float tg_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ tg_f2 f2of(float a, float b) { return tg_f2{a, b}; }
+__device__ __forceinline__ tg_f2 f2bc(float a) { return tg_f2{a, a}; }
+__device__ __forceinline__ tg_f2 fma2(tg_f2 a, tg_f2 b, tg_f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ V3 mulT(const M3 &m, V3 v) {
+    const tg_f2 p = fma2(f2of(m.a[6], m.a[7]), f2bc(v.z),
+                         fma2(f2of(m.a[3], m.a[4]), f2bc(v.y), f2of(m.a[0], m.a[1]) * f2bc(v.x)));
+    return V3{p.x, p.y, __builtin_fmaf(m.a[8], v.z, __builtin_fmaf(m.a[5], v.y, m.a[2] * v.x))};
+}
+__device__ __forceinline__ M3 mul(const M3 &x, const M3 &y) {
+    M3 o;
+    const tg_f2 y0 = f2of(y.a[0], y.a[1]), y1 = f2of(y.a[3], y.a[4]), y2 = f2of(y.a[6], y.a[7]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const tg_f2 p = fma2(f2bc(x.a[3 * i + 2]), y2, fma2(f2bc(x.a[3 * i + 1]), y1, f2bc(x.a[3 * i]) * y0));
+        o.a[3 * i] = p.x;
+        o.a[3 * i + 1] = p.y;
+        o.a[3 * i + 2] = __builtin_fmaf(x.a[3 * i + 2], y.a[8], __builtin_fmaf(x.a[3 * i + 1], y.a[5], x.a[3 * i] * y.a[2]));
+    }
+    return o;
+}
+#else
 __device__ __forceinline__ V3 mulT(const M3 &m, V3 v) {
     return V3{m.a[0] * v.x + m.a[3] * v.y + m.a[6] * v.z, m.a[1] * v.x + m.a[4] * v.y + m.a[7] * v.z,
               m.a[2] * v.x + m.a[5] * v.y + m.a[8] * v.z};
@@ -39,6 +72,7 @@ __device__ __forceinline__ M3 mul(const M3 &x, const M3 &y) {
         for (int j = 0; j < 3; ++j) o.a[3 * i + j] = x.a[3 * i] * y.a[j] + x.a[3 * i + 1] * y.a[3 + j] + x.a[3 * i + 2] * y.a[6 + j];
     return o;
 }
+#endif
 __device__ __forceinline__ M3 transpose(const M3 &m) {
     return M3{{m.a[0], m.a[3], m.a[6], m.a[1], m.a[4], m.a[7], m.a[2], m.a[5], m.a[8]}};
 }
