@@ -452,8 +452,12 @@ template <class M> __device__ __forceinline__ SV ldSm(const LE &s, int g, int jt
 // s_waitcnt on the prefetched global loads still in flight).
 // sum over the 8 lanes of an env with DPP moves (row half-mirror, then quad
 // swaps): every lane ends with the total, no LDS round trip
+// (every lane of the permutations used here has a valid source, so the old
+// operand is dead: mov_dpp with bound_ctrl needs no zero-initialised
+// destination and lets the compiler fold the move into the add; round 5,
+// 103 moves fewer in the walk kernel, bit-identical, profiles/r5/dpp_ab.txt)
 template <int CTRL> __device__ __forceinline__ float dpp(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 __device__ __forceinline__ float sum8(float v) {
     v += dpp<0x141>(v);   // row_half_mirror: lane i <-> 7 - i
@@ -1342,6 +1346,17 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
 #define TG_1A_FLAT 1
 #endif
         constexpr bool FLAT1 = CH && TG_1A_FLAT && PL::VFREE - PL::W >= F_V + 6;
+// an idle lane (its chain ended) updates its chain registers too -- they
+// are dead after the pass -- so the update is a register rename, not a
+// divergent branch of 18 moves: on trees of at least TG_1A_IDLE_FREE groups
+// (the humanoids: ThormangWalk 49.4 -> 48.1 us, bit-identical,
+// profiles/r5/idle_free_ab.txt).  The scooters keep the branch: without it
+// the compiler fuses some multiply-adds differently (fp-contract works per
+// basic block), which changes their rounding (1e-4 after 100 steps).
+#ifndef TG_1A_IDLE_FREE
+#define TG_1A_IDLE_FREE 16
+#endif
+        constexpr bool IDLE_FREE = TG_1A_IDLE_FREE > 0 && M::NG >= TG_1A_IDLE_FREE;
         auto body1f = [&](const I4 &dc, const float *ck, const float *qq) {
             const int g = dc.x, jt = d_jt(dc);
             const float qg = qq[0], qdg = qq[1];
@@ -1369,8 +1384,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             stm3(s, os + F_RT, transpose(Rg));
             stv3(s, os + F_P, Pg);
             stsv(s, os + F_V, vg);
-            if (g > 0) {   // (an idle lane keeps its chain registers: updating them
-                           // changed the scooters' results, bit-identical this way)
+            if (IDLE_FREE || g > 0) {   // (see TG_1A_IDLE_FREE)
                 pr_R = Rg;
                 pr_P = Pg;
                 pr_v = vg;

@@ -27,7 +27,7 @@ __global__ __launch_bounds__(256) void walk_pre_kernel(tg_walk_params p, tg_walk
 // sum over the wavefront, returned to every lane: DPP within each 16-lane row
 // (half-mirror, quad swaps, row rotate by 8), then the four row totals
 template <int CTRL> __device__ __forceinline__ float dppw(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 __device__ __forceinline__ float wave_total(float v) {
     v += dppw<0x141>(v);
