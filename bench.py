@@ -2,9 +2,10 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--task Gogoro] [--num-envs 4096]
 
-One process per GPU (torchrun for N>1, RANK/LOCAL_RANK/WORLD_SIZE from the
-env); every rank owns its own env batch (weak scaling, no collective on the
-hot path).  A "step" is one ``env.step(actions)`` call: pre-physics kernel,
+One process per GPU: under torchrun RANK/LOCAL_RANK/WORLD_SIZE come from the
+env (WORLD_SIZE must equal --gpus); a plain ``python bench.py --gpus N`` with
+N > 1 starts the N ranks itself (torch.distributed.run children).  Every
+rank owns its own env batch (weak scaling, no collective on the hot path).  A "step" is one ``env.step(actions)`` call: pre-physics kernel,
 ``sim.substeps`` articulation substeps, post-physics kernel (observations,
 reward, masked resets, timeouts) -- inputs resident in HBM, synthetic
 actions U(-1,1) from torch.Generator(seed 1234 + rank).  Rank 0 prints one
@@ -271,6 +272,40 @@ def solver_desc(env) -> str:
             f"{' (sub-steps)' if sp.solver_type == 1 else ''} + {sp.velocity_iterations} velocity iterations")
 
 
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """``python bench.py --gpus N`` (N > 1, no WORLD_SIZE in the env): run the N
+    ranks as fresh child processes under torch.distributed.run (one per GPU,
+    LOCAL_RANK = i, rendezvous on 127.0.0.1), wait for them and return their
+    exit status.  The caller has touched no GPU; rank 0 prints the JSON line.
+    (reference: isaacgymenvs/train.py:74-82 -- one process per GPU, LOCAL_RANK
+    -> device, seed + rank)"""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+    return subprocess.call(cmd)
+
+
+def stub_run(args, world: int, rank: int, local: int, rccl_world):
+    """TG_BENCH_STUB=1: the launch / rank / timing path with a sleep in place of
+    env.step and no GPU (CPU tests only; never a measured line)."""
+    def step():
+        time.sleep(0.001)
+    for _ in range(args.warmup):
+        step()
+    elapsed = timed_region(step, args.steps, world, "cpu", lambda: None)
+    if rank == 0:
+        print(json.dumps({"metric": "stub", "value": args.num_envs * args.steps * world / elapsed,
+                          "n_gpus": world, "steps": args.steps, "local_rank": local,
+                          "dist": {"world_size": rccl_world or 1}}), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -292,7 +327,15 @@ def main():
     if args.terrain and args.task != "Gogoro":
         ap.error("--terrain applies to the Gogoro task (the reference has terrain only there)")
 
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # launched as `python bench.py --gpus N`: start the N ranks ourselves,
+        # as child processes, before this process makes any GPU call
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: the launcher and the flag disagree")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # developer rehearsal of the N > 1 path on a one-GPU box (not a scaling
@@ -301,6 +344,9 @@ def main():
     backend = os.environ.get("TG_BENCH_DIST_BACKEND", "nccl")
     if os.environ.get("TG_BENCH_SHARE_GPU"):
         local = 0
+    stub = os.environ.get("TG_BENCH_STUB") == "1"
+    if stub:   # CPU test of the launch path (tests/test_bench_dist.py): no GPU, gloo
+        backend = "gloo"
     rccl_world = None
     if world > 1:
         import torch.distributed as dist
@@ -308,6 +354,9 @@ def main():
         rccl_world = dist.get_world_size()   # what RCCL itself reports (the SCALE runs are checked on it)
         if rccl_world != world:
             raise RuntimeError(f"WORLD_SIZE {world} but the process group has {rccl_world} ranks")
+    if stub:
+        stub_run(args, world, rank, local, rccl_world)
+        return
     torch.cuda.set_device(local)
     dev = f"cuda:{local}"
 

@@ -18,7 +18,7 @@ export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 if [ -n "${ONLY_PROF:-}" ]; then SKIP_TESTS=1; SKIP_BENCH=1; fi
 if [ -z "${SKIP_TESTS:-}" ]; then
   timeout -k 10 700 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
-  rc=$?; tail -2 $OUT/gpu_tests.log; [ $rc -le 1 ] || exit $rc
+  rc=$?; tail -2 $OUT/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit $?
   tail -1 $OUT/smoke.log
 fi

@@ -62,25 +62,28 @@ def system_com(m, root, q):
 
 
 def drop_box(solver_type, iters=4, viters=1, rest_offset=0.0, z0=0.25, steps=90, dt=1.0 / 60.0, substeps=2,
-             step_fn=None):
+             step_fn=None, contact_offset=None, vz0=0.0):
     """A 0.1 m box (kat_models.box_body, half height 0.05) released at rest
     ``z0`` above the ground under gravity, with the walk cfg's solver
     (cfg/task/ThormangWalk.yaml: dt 1/60 x 2 substeps, TGS 4 position + 1
     velocity iterations).  Returns the per-step root height and vertical
     velocity.  ``step_fn(desc, sp, root, dof, props, pt, vt)`` steps one env
-    (default: the CPU oracle)."""
+    (default: the CPU oracle).  ``contact_offset`` sets sim.physx's key (None:
+    the default), ``vz0`` the initial vertical velocity."""
     from tests.oracle_lib import physics_step
     m = box_body(mu=0.8)
     sp = sim_params_from_cfg({"dt": dt, "substeps": substeps, "gravity": [0, 0, -9.81],
                               "physx": {"num_position_iterations": iters, "num_velocity_iterations": viters,
                                         "rest_offset": rest_offset, "max_depenetration_velocity": 1.0,
-                                        "solver_type": solver_type}},
+                                        "solver_type": solver_type,
+                                        **({} if contact_offset is None else {"contact_offset": contact_offset})}},
                              dict(angular_damping=0.0, linear_damping=0.0, ground_friction=0.8), 1, warn=False)
     desc = ModelDesc(m)
     props = default_dof_props(m, 1)
     root = np.zeros((1, 13), np.float32)
     root[0, 2] = z0
     root[0, 6] = 1.0
+    root[0, 9] = vz0
     dof = np.zeros((0, 2), np.float32)
     z = np.zeros((1, 0), np.float32)
     step = step_fn or physics_step
@@ -134,3 +137,26 @@ def jit_walker():
               Shape("sphere", "r_shin", [0, 0, -0.26], eye, [0.04], 1.0)]
     return urdf_model("jit_walker", f'<link name="torso">{_inertial(4.0, (0, 0, 0.02), (0.05, 0.04, 0.03))}</link>'
                       + legs, shapes, locked=["r_knee"])
+
+
+def contact_offset_checks(make_step=None, solver_type=1, contact_offset=0.02):
+    """Known answers of the contact_offset gate, for the oracle or
+    the GPU (``step_fn`` as in drop_box), with the walk cfg's step (dt 1/60 x
+    2 substeps, h = 1/120) and contact_margin 0.05:
+
+    * ``rest_gap``: a box at rest whose separation (3 cm) lies between the
+      offset (2 cm) and the margin takes no normal impulse -- one step is the
+      exact semi-implicit free fall, z0 - 3 g h^2, vz = -2 g h;
+    * ``fast``: the same box approaching at 6 m/s (0.05 m per substep, more
+      than its 3 cm gap) gets a row from its free approach and lands on the
+      ground instead of tunnelling (free flight would end 2 cm below it).
+    Returns a dict of the measured quantities."""
+    g, h, half = 9.81, 1.0 / 120.0, 0.05
+    z0 = half + 0.03
+    mk = make_step or (lambda: None)
+    zs, vs = drop_box(solver_type, z0=z0, steps=1, step_fn=mk(), contact_offset=contact_offset)
+    out = {"rest_gap_dz": float(zs[0] - (z0 - 3 * g * h * h)), "rest_gap_dvz": float(vs[0] + 2 * g * h)}
+    zs, vs = drop_box(solver_type, z0=z0, steps=20, step_fn=mk(), contact_offset=contact_offset, vz0=-6.0)
+    out.update(fast_min_z=float(zs.min()) - half, fast_z1=float(zs[0]) - half, fast_vz1=float(vs[0]),
+               fast_final=float(zs[-1]) - half, free_flight_z1=float(z0 - 2 * 6.0 * h - 3 * g * h * h) - half)
+    return out

@@ -108,3 +108,37 @@ def test_two_rank_env_creator_and_episode_gather():
         assert abs(g["mean_length"] - 2.5) < 1e-12
         assert abs(g["mean_return"] - (1 * 10 + 2 * 10) / 8) < 1e-12
         assert again["episodes"] == 0          # sums reset after each gather
+
+
+def _bench(args, extra_env=None, timeout=240):
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(TG_BENCH_STUB="1", **(extra_env or {}))
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], env=env, cwd=REPO,
+                       capture_output=True, text=True, timeout=timeout)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r, [json.loads(ln) for ln in lines]
+
+
+def test_bench_gpus_n_launches_n_ranks():
+    """`python bench.py --gpus 2` (no WORLD_SIZE) starts two ranks itself; rank 0
+    alone prints the line, with n_gpus and the process group's size both 2."""
+    r, lines = _bench(["--gpus", "2", "--steps", "5", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert len(lines) == 1, r.stdout
+    assert lines[0]["n_gpus"] == 2 and lines[0]["dist"]["world_size"] == 2
+    assert lines[0]["steps"] == 5 and lines[0]["local_rank"] == 0
+
+
+def test_bench_gpus_mismatch_with_world_size_raises():
+    r, lines = _bench(["--gpus", "2", "--steps", "2", "--warmup", "0"],
+                      extra_env=dict(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"))
+    assert r.returncode != 0 and not lines
+    assert "--gpus 2 but WORLD_SIZE=1" in r.stderr
+
+
+def test_bench_gpus_one_runs_in_process():
+    r, lines = _bench(["--gpus", "1", "--steps", "3", "--warmup", "0"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert lines[0]["n_gpus"] == 1 and lines[0]["dist"]["world_size"] == 1

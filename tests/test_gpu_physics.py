@@ -129,6 +129,32 @@ def test_gpu_landing_known_answer_no_rebound_and_rest_height(solver, viters, res
     assert r["ok"], r
 
 
+@pytest.mark.parametrize("solver", [0, 1])
+def test_gpu_contact_offset_known_answers(solver):
+    """The contact_offset known answers of tests/test_solver_cfg.py on the GPU
+    kernel: a 3 cm resting gap beyond the 2 cm offset is exact
+    free flight; a 6 m/s approach closing it within the substep lands
+    without tunnelling."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs the MI355X")
+
+    def make_step():
+        sims = []
+
+        def gpu_step(desc, sp, root, dof, props, pt, vt):
+            if not sims:
+                sims.append(gpu_sim(pm.box_body(mu=0.8), sp, 1, root, dof, props, pt, vt))
+            sims[0].simulate()
+            root[...] = sims[0].root_state.cpu().numpy()
+        return gpu_step
+
+    g = pm.contact_offset_checks(make_step, solver_type=solver)
+    print({"gpu": g, "oracle": pm.contact_offset_checks(solver_type=solver)})
+    assert abs(g["rest_gap_dz"]) < 1e-6 and abs(g["rest_gap_dvz"]) < 1e-5, g
+    assert g["fast_min_z"] > -0.002 and g["fast_z1"] > -0.002, g
+    assert g["fast_vz1"] > -0.5 and abs(g["fast_final"]) < 1e-3, g
+
+
 def test_gpu_free_fall_exact():
     if not torch.cuda.is_available():
         pytest.skip("needs the MI355X")

@@ -188,7 +188,7 @@ def test_native_loader_parses_numbers_as_python_float(tmp_path):
     for text in ("inf", "-Infinity", "NaN", "1e999"):   # accepted by float(); the parse itself must not fail
         rc, msg = _parse_text(tmp_path, MINI.format(m=text, extra=ok))
         assert "malformed number" not in msg, (text, msg)
-    for text in ("0x1p3", "1__0", "_1", "1_", "1.5 2", "nan1"):
+    for text in ("0x1p3", "1__0", "_1", "1_", "1.5 2", "nan1", "nan(123)", "NAN()"):   # strtod takes nan(...)
         rc, msg = _parse_text(tmp_path, MINI.format(m=text, extra=ok))
         assert rc == TG_ERR_MODEL and "malformed number" in msg, (text, msg)
 

@@ -229,3 +229,37 @@ def test_rows_on_a_fixed_base_take_no_impulse(solver):
     assert np.isfinite(root).all() and np.isfinite(dof).all()
     np.testing.assert_array_equal(root, r0)
     assert np.abs(dof[:, 1]).max() > 0   # the legs swing under gravity
+
+
+def test_contact_offset_default_follows_the_vec_task_base():
+    """without a sim.physx.contact_offset key the default is the one
+    the reference's base class leaves -- IsaacGym's 0.02 under
+    vec_task.VecTask (Gogoro), 0.016 under multi_vec_task.MA_VecTask
+    (multi_vec_task.py:322, the walk's MA_OP3 template); no asset option
+    overrides it."""
+    from thormang_isaacgym_amd import abi
+    from thormang_isaacgym_amd.tasks.base.vec_task import VecTask
+    from thormang_isaacgym_amd.tasks.thormang_walk import ThormangWalk
+    sim = {"dt": 0.01, "substeps": 1, "physx": {}}
+    assert VecTask.default_contact_offset == 0.02 and ThormangWalk.default_contact_offset == 0.016
+    sp = abi.sim_params_from_cfg(sim, {"contact_offset": 0.5}, 1, warn=False)
+    assert abs(sp.contact_offset - 0.02) < 1e-9
+    sp = abi.sim_params_from_cfg(sim, {}, 1, warn=False, default_contact_offset=ThormangWalk.default_contact_offset)
+    assert abs(sp.contact_offset - 0.016) < 1e-9
+
+
+@pytest.mark.parametrize("solver", [0, 1])
+def test_contact_offset_known_answers(solver):
+    """the contact_offset gate checked against what it must do, not
+    against the kernel (both restate the same rule): a resting gap wider than
+    the offset is free flight, exactly; a fast approach that closes the gap
+    within the substep gets a row and does not tunnel
+    (tests/physics_models.contact_offset_checks; GPU twin in
+    tests/test_gpu_physics.py).  The gate is one offset plus the free
+    approach; PhysX's is the sum of both shapes' offsets without the approach
+    term."""
+    r = pm.contact_offset_checks(solver_type=solver)
+    assert abs(r["rest_gap_dz"]) < 1e-7 and abs(r["rest_gap_dvz"]) < 1e-6, r   # (the state is stored in fp32)
+    assert r["free_flight_z1"] < -0.015, r                    # without a row it would end below the ground
+    assert r["fast_min_z"] > -0.002 and r["fast_z1"] > -0.002, r
+    assert r["fast_vz1"] > -0.5 and abs(r["fast_final"]) < 1e-3, r

@@ -262,7 +262,8 @@ def unhonoured_physx_keys(physx: dict, asset_opts: dict | None = None) -> Dict[s
 
 
 def sim_params_from_cfg(cfg_sim: dict, asset_opts: dict | None = None, num_envs: int = 1,
-                        env_spacing: float = 1.0, warn: bool = True) -> tg_sim_params:
+                        env_spacing: float = 1.0, warn: bool = True,
+                        default_contact_offset: float = 0.02) -> tg_sim_params:
     """Map the reference cfg 'sim' block (vec_task.py:442-490) onto tg_sim_params.
 
     ``num_position_iterations`` is the number of biased PGS sweeps per substep
@@ -288,9 +289,12 @@ def sim_params_from_cfg(cfg_sim: dict, asset_opts: dict | None = None, num_envs:
     sp.max_depenetration_velocity = float(physx.get("max_depenetration_velocity", 100.0))
     sp.rest_offset = float(physx.get("rest_offset", 0.001))
     sp.contact_margin = float(ao.get("contact_margin", 0.05))
-    # IsaacGym's default contact_offset is 0.02 (an asset option overrides it;
-    # <= 0 keeps every point speculative, the rounds 1-4 behaviour)
-    sp.contact_offset = float(ao.get("contact_offset", physx.get("contact_offset", 0.02)))
+    # contact_offset: the cfg's sim.physx key.  Without it, the default of the
+    # VecTask base the task derives from: vec_task.py:442-482 leaves IsaacGym's
+    # own 0.02 (Gogoro), multi_vec_task.py:322 sets 0.016 before the cfg keys
+    # (the MA_OP3 template of the walk), passed in by the task as
+    # ``default_contact_offset``.  <= 0 keeps every point speculative
+    sp.contact_offset = float(physx.get("contact_offset", default_contact_offset))
     sp.ground_friction = float(ao.get("ground_friction", 1.0))
     sp.baumgarte = float(ao.get("baumgarte", 0.2))
     sp.limit_stiffness = float(ao.get("limit_stiffness", 1.0))

@@ -212,7 +212,7 @@ bool parse_float(const std::string &tok, double &out) {
     std::string t;
     for (size_t k = b; k <= e; ++k) {
         const char c = tok[k];
-        if (c == 'x' || c == 'X') return false;
+        if (c == 'x' || c == 'X' || c == '(') return false;   // no hex floats, no strtod "nan(n-char-seq)"
         if (c == '_') {   // float("1_000.5") == 1000.5; "1__0", "_1", "1_" are errors
             if (k == b || k == e || !std::isdigit((unsigned char)tok[k - 1]) || !std::isdigit((unsigned char)tok[k + 1]))
                 return false;
@@ -221,6 +221,7 @@ bool parse_float(const std::string &tok, double &out) {
         t += c;
     }
     static const locale_t c_loc = newlocale(LC_ALL_MASK, "C", (locale_t)0);
+    if (c_loc == (locale_t)0) return false;   // no "C" locale object: report the value malformed, never UB
     char *end = nullptr;
     errno = 0;
     const double v = strtod_l(t.c_str(), &end, c_loc);

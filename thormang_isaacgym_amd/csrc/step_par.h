@@ -184,7 +184,11 @@ template <class M> struct ParLayout {
     // unit-torque responses of up to WCM clamped drives.  Per env: G (the
     // responses' joint accelerations per group), R (root accelerations), A
     // (contact-group accelerations), J (row velocities, = J G), Minv
+#ifdef TG_NO_SUPER   // developer build: the bottom-up impulse application (A/B)
+    static constexpr bool SUPER = false;
+#else
     static constexpr bool SUPER = K > 0 && K * (M::MAXD + 6) <= M::NG * 21;
+#endif
 #ifdef TG_NO_WOOD   // developer build: the drive-clamp rerun instead (A/B)
     static constexpr bool WOOD = false;
 #else
@@ -634,7 +638,11 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
     // then the top-down pass.  Models whose columns do not fit keep the
     // bottom-up pass.
     constexpr int SW = M::MAXD + 6;
+#ifdef TG_NO_SUPER
+    constexpr bool SUPER = false;
+#else
     constexpr bool SUPER = K > 0 && K * SW <= M::NG * 21;
+#endif
     constexpr bool SEPC = PL::SEPC;
     auto ia_c = [](int g) { return SEPC ? PL::CB + 32 * g : g * GF + F_IA; };        // pass-2 contribution I^a
     auto pa_c = [](int g) { return SEPC ? PL::CB + 32 * g + 24 : g * GF + F_PA; };   // pass-2 contribution p^a

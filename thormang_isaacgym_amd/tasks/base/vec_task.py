@@ -154,6 +154,9 @@ def mass_scale(sample: torch.Tensor, operation: str, base_mass: torch.Tensor) ->
 
 class VecTask(Env):
     metadata = {"render.modes": ["human", "rgb_array"], "video.frames_per_second": 24}
+    #: sim.physx.contact_offset when the cfg has none: vec_task.py:442-482 sets
+    #: no value, so IsaacGym's own 0.02 applies
+    default_contact_offset = 0.02
 
     def __init__(self, config, rl_device, sim_device, graphics_device_id, headless, virtual_screen_capture: bool = False,
                  force_render: bool = False):
@@ -197,7 +200,8 @@ class VecTask(Env):
     def create_sim_object(self, model, asset_options: Dict[str, Any], env_spacing: float = 1.0):
         """gym.create_sim + load_asset + create_env/actor in one call (vec_task.py:279-295)."""
         from ...sim import Sim
-        sp = abi.sim_params_from_cfg(self.sim_params, asset_options, self.num_envs, env_spacing)
+        sp = abi.sim_params_from_cfg(self.sim_params, asset_options, self.num_envs, env_spacing,
+                                     default_contact_offset=self.default_contact_offset)
         return Sim(model, sp, self.num_envs, self.device)
 
     def allocate_buffers(self):

@@ -35,6 +35,10 @@ def _p(t):
 
 
 class ThormangWalk(VecTask):
+    #: the walk's template task (MA_OP3) derives from multi_vec_task.MA_VecTask,
+    #: whose __parse_sim_params sets contact_offset 0.016 before the cfg keys
+    #: (multi_vec_task.py:322)
+    default_contact_offset = 0.016
     #: optional DrawSource (uniform(n)/normal(n)) replacing the in-kernel Philox draws
     draw_source = None
 
