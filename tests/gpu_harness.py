@@ -424,8 +424,20 @@ def walk_forced(num_envs=32, steps=1000, seed=0, task="ThormangWalk", dr=False, 
     orc = OracleWalk(mk(), NumpyDraws(seed))
     ctl = OracleWalk(mk(), NumpyDraws(seed), precision="f32") if control else None
     rs = np.random.default_rng(seed + 100)
-    return forced_step_errors(env, orc, lambda o: rs.uniform(-0.5, 0.5, (num_envs, orc.D)).astype(np.float32), steps,
-                              ctl=ctl)
+    err = forced_step_errors(env, orc, lambda o: rs.uniform(-0.5, 0.5, (num_envs, orc.D)).astype(np.float32), steps,
+                             ctl=ctl)
+    if dr:
+        note_dr_ranges(err, env)
+    return err
+
+
+def note_dr_ranges(err, env):
+    """The spread of the per-env mass scales and shape frictions the GPU env
+    drew (and the oracle was handed, sync_dr): a DR run whose draws never
+    left 1.0 would compare nothing."""
+    sim = env.sim
+    err["mass_scale_range"] = [float(sim.body_mass_scale.min()), float(sim.body_mass_scale.max())]
+    err["friction_range"] = [float(sim.shape_friction.min()), float(sim.shape_friction.max())]
 
 
 # ----------------------------------------------------------------------------- ThormangWalk
@@ -610,9 +622,8 @@ def walk_env_vs_oracle(num_envs=32, steps=30, seed=0, task="ThormangWalk", dr=Fa
     err["obs0"] = maxerr(env.obs_buf.cpu().numpy(), orc.a["obs_buf"])
     for t in range(steps):
         if dr:
-            sync_dr(orc, env)
-            if ctl is not None:
-                sync_dr(ctl, env)
+            for o in [orc] + ([ctl] if ctl is not None else []) + f32s:
+                sync_dr(o, env)
         act = rs.uniform(-amp, amp, (num_envs, orc.D)).astype(np.float32)
         obs_d, rew, reset, extras = env.step(torch.from_numpy(act).to("cuda:0"))
         o_obs, o_rew, o_reset, o_to = orc.step(act)
@@ -667,4 +678,6 @@ def walk_env_vs_oracle(num_envs=32, steps=30, seed=0, task="ThormangWalk", dr=Fa
             err["first_bad_step"] = t
     err["resets"] = int(n_resets(orc))
     err["min_height"] = float(orc.a["root"][:, 2].min())
+    if dr:
+        note_dr_ranges(err, env)
     return err

@@ -80,16 +80,21 @@ def test_gpu_walk_8192_envs_step_matches_oracle():
 
 
 def test_gpu_walk_dr_16384_envs():
-    """BASELINE config 5's per-GPU batch: ThormangWalkDR at 16384 envs.  The
-    pushes path is checked step by step against the oracle env (100
-    teacher-forced steps; the mass / friction draws off there, as in every
-    forced walk run), then the full DR env (mass, friction, pushes live) runs
-    150 steps."""
+    """BASELINE config 5's per-GPU batch: ThormangWalkDR at 16384 envs, its
+    whole DR live: per-env link masses and shape
+    frictions (the task's randomize draws) and pushes, 100 teacher-forced
+    steps against the oracle env, which is handed the GPU env's draws every
+    step (sync_dr; vec_task.py:538-768's schema, as on Gogoro).  Then the
+    env runs 150 more steps free, for finiteness."""
     _cuda()
     from tests.gpu_harness import walk_forced
-    err = walk_forced(num_envs=16384, steps=100, seed=12, task="ThormangWalkDR")
+    err = walk_forced(num_envs=16384, steps=100, seed=12, task="ThormangWalkDR", dr=True)
     print(brief(err))
-    assert err["reset_equal"], err
+    lo, hi = err["mass_scale_range"]
+    assert lo < 0.97 and hi > 1.03, err          # the mass draws really spread
+    flo, fhi = err["friction_range"]
+    assert fhi - flo > 0.1, err
+    assert err["reset_equal"] and err["timeout_equal"], err
     # (round 4: reward 1.6e-4 with the contact geometry formed about the root
     # origin; 1.08e-3 while it was formed in world coordinates, whose fp32
     # rounding ~158 m from the world origin perturbed the lever arms,
@@ -105,6 +110,20 @@ def test_gpu_walk_dr_16384_envs():
         resets += int(reset.sum())
     assert torch.isfinite(obs["obs"]).all() and torch.isfinite(rew).all() and torch.isfinite(env.root_tensor).all()
     assert resets > 0
+
+
+def test_gpu_walk_dr_mass_friction_free_running():
+    """ThormangWalkDR with its mass / friction randomisation and pushes live,
+    32 envs free running for 200 steps against the oracle env handed the GPU
+    env's draws (sync_dr), the fp32 control beside it."""
+    _cuda()
+    from tests.gpu_harness import walk_env_vs_oracle
+    err = walk_env_vs_oracle(num_envs=32, steps=200, seed=7, task="ThormangWalkDR", dr=True, control=True)
+    print(brief(err))
+    lo, hi = err["mass_scale_range"]
+    assert lo < 0.97 and hi > 1.03, brief(err)
+    assert within(err) and within(err, "rew"), brief(err)
+    assert err["reset_equal"] and err["timeout_equal"], brief(err)
 
 
 def test_gpu_walk_fused_step_equals_separate_calls():
