@@ -25,16 +25,20 @@ def test_gpu_walk_matches_oracle_env():
 
 def test_gpu_walk_dr_pushes_match_oracle_env():
     """ThormangWalkDR (pushes), 32 envs, 200 free-running steps, with the fp32
-    rounding control beside it, recorded only: on this seed the control's own
-    reward error reaches 1.45e-3 (round 4), i.e. the trajectory is
-    rounding-sensitive past the bar, but the GPU meets it (8.6e-4), so the
-    GPU is held to 1e-3 over all 200 steps -- the control does not shorten
-    the asserted span here."""
+    rounding control beside it.  On this seed the control's own reward error
+    leaves 1e-3 at step 190 (1.45e-3): the trajectory is rounding-sensitive
+    past the bar there.  Rounds 4-5 held the GPU to 1e-3 over all 200 steps
+    because it happened to stay inside (8.6e-4); since round 6's contact-local
+    rows the GPU leaves at the same step 190 as the control (1.03e-3), so the
+    test holds it to the harness's rule: within 1e-3 at every step before
+    the control's departure, and not departing before the control does."""
     _cuda()
     from tests.gpu_harness import walk_env_vs_oracle
     err = walk_env_vs_oracle(num_envs=32, steps=200, seed=7, task="ThormangWalkDR", control=True)
     print(brief(err))
-    assert err["obs"] < 1e-3 and err["rew"] < 1e-3, brief(err)
+    n = err["steps"]
+    assert within(err) and within(err, "rew"), brief(err)
+    assert err.get("first_bad_step", n) >= err.get("ctl_first_bad", n), brief(err)
     assert err["reset_equal"], err
 
 

@@ -449,6 +449,26 @@ template <class M> __device__ __forceinline__ SV motion_Sm(int jt, V3 ax, V3 P) 
 template <class M> __device__ __forceinline__ SV ldSm(const LE &s, int g, int jt) {
     return motion_Sm<M>(jt, ldv3(s, g * GF + F_AX), ldv3(s, g * GF + F_P));
 }
+// Contact quantities at the contact group's own origin (round 6).  The passes
+// carry spatial vectors about the ROOT origin; a contact group far from it (a
+// scooter wheel 0.8 m away, a humanoid foot 0.9 m below the pelvis) then has
+// a linear velocity dominated by its joint's qd (P x a) term, which the
+// contact point's r x w cancels again when a row velocity is formed -- the
+// fp32 digits lost there made the kernel's Delassus matrix and free row
+// velocities 4-6x less accurate than the fp32 oracle's, which works in group
+// frames (profiles/r6/gogoro_dump_stats*.txt).  So the rows' Jacobians are
+// (r_l x d, d) with r_l the point about the contact group's origin pc, and the
+// velocities they meet are formed at pc term by term: the root's shifted by
+// w0 x pc, each path joint's as qd (a, a x (pc - P)) -- a wheel's own spin
+// adds nothing to its centre's velocity, exactly.
+// (w, v) about the root origin -> (w, v + w x pc)
+__device__ __forceinline__ SV shift_to(const SV &x, V3 pc) { return SV{x.w, x.v + cross(x.w, pc)}; }
+// a joint's motion subspace about pc (its axis a through P): (a, a x (pc - P))
+// revolute, (0, a) prismatic
+template <class M> __device__ __forceinline__ SV motion_at(int jt, V3 ax, V3 P, V3 pc) {
+    if constexpr (all_revolute<M>()) return SV{ax, cross(ax, pc - P)};
+    else return jt == TG_JOINT_REVOLUTE ? SV{ax, cross(ax, pc - P)} : SV{v3(0, 0, 0), ax};
+}
 
 // The LPE lanes of an env are consecutive lanes of one wavefront, whose LDS
 // operations execute in program order: an env-level "barrier" only has to stop
@@ -1174,7 +1194,9 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 }
                 const SV ar = fix_base ? sv0() : ldl6_solve(rf, -1.0f * dp);
                 SV acc[M::NG];
+                float qgs[M::NG];
                 acc[0] = ar;
+                qgs[0] = 0.f;
 #pragma unroll
                 for (int g = 1; g < M::NG; ++g) {
                     const SV ap = acc[M::parent[g]];
@@ -1182,11 +1204,25 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     const float di = s(g * GF + F_DINV);
                     const float qg = (dus[g] - dot(Ug, ap)) * di;
                     acc[g] = ap + qg * ldSm<M>(s, g, M::jtype[g]);
+                    qgs[g] = qg;
                     s(PL::WB_G + 8 * sub + g) = qg;
                 }
                 stsv(s, PL::WB_R + 6 * sub, ar);
+                // (the contact groups' responses about their own origins, as the rows take them)
 #pragma unroll
-                for (int c = 0; c < M::NCG; ++c) stsv(s, PL::WB_A + 6 * (M::NCG * sub + c), acc[M::cgroup[c]]);
+                for (int c = 0; c < M::NCG; ++c) {
+                    const V3 pcc = ldv3(s, M::cgroup[c] * GF + F_P);
+                    SV al = shift_to(ar, pcc);
+#pragma unroll
+                    for (int i = 0; i < M::MAXD; ++i) {
+                        if (i < M::cpath_len[c]) {
+                            const int hg = M::cpath[c][i];
+                            al = al + qgs[hg] * motion_at<M>(M::jtype[hg], ldv3(s, hg * GF + F_AX),
+                                                             ldv3(s, hg * GF + F_P), pcc);
+                        }
+                    }
+                    stsv(s, PL::WB_A + 6 * (M::NCG * sub + c), al);
+                }
             } else if (sub < WCM) {
                 // the unused response slots (wn < WCM): zeros, because the
                 // fixed-size WCM sums below multiply them by zero weights, and
@@ -2034,16 +2070,21 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 // the world origin was 1.5e-5 m -- a lever-arm error that the
                 // speculative contact bound amplified)
                 stv3(s, PL::CGP + 12 * c + 9, mul(R, ldv3(s, cg * GF + F_P)));
-                SV v = v0s;   // root frame: the root velocity plus the path's joint terms
+                // root frame, at the contact group's own origin pc (round 6, see
+                // at_group_origin): the root velocity shifted to pc plus the
+                // path's joint terms, each about its own joint point
+                const V3 pc = ldv3(s, cg * GF + F_P);
                 float qv[M::MAXD];
-                SV sv[M::MAXD];
+                V3 ax[M::MAXD], Pj[M::MAXD];
 #pragma unroll
                 for (int i = 0; i < M::MAXD; ++i) {
                     qv[i] = i < lk ? s(pk[i] * GF + F_QDS) : 0.f;
-                    sv[i] = ldSm<M>(s, pk[i], pj[i]);
+                    ax[i] = ldv3(s, pk[i] * GF + F_AX);
+                    Pj[i] = ldv3(s, pk[i] * GF + F_P);
                 }
+                SV v = shift_to(v0s, pc);
 #pragma unroll
-                for (int i = 0; i < M::MAXD; ++i) v = v + qv[i] * sv[i];
+                for (int i = 0; i < M::MAXD; ++i) v = v + qv[i] * motion_at<M>(pj[i], ax[i], Pj[i], pc);
                 stsv(s, PL::CGV + 6 * c, v);
             }
             TG_SYNC();
@@ -2077,7 +2118,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     cl = v3(CP(CL::shape(sh) + 9), CP(CL::shape(sh) + 10), CP(CL::shape(sh) + 11));
                 }
                 const M3 Rs = mul(Rwg, Rsl);
-                const V3 cw = pwg + mul(Rwg, cl);
+                const V3 cw = mul(Rwg, cl);   // (points about the contact group's origin pwg, world-oriented)
                 V3 pts[4];
                 const int nr = M::shape_nrows[sh];
                 const int kind = M::shape_kind[sh];
@@ -2110,9 +2151,9 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 };
                 if constexpr (HF) {
                     bool th;
-                    ground_at(a, pos.x + cw.x, pos.y + cw.y, n, th);
+                    ground_at(a, pos.x + (pwg.x + cw.x), pos.y + (pwg.y + cw.y), n, th);
                     support(n);
-                    ground_at(a, pos.x + pts[0].x, pos.y + pts[0].y, n, th);
+                    ground_at(a, pos.x + (pwg.x + pts[0].x), pos.y + (pwg.y + pts[0].y), n, th);
                     if (th) gmu = a.hf_mu;
                 }
                 support(n);
@@ -2122,13 +2163,13 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     if (k >= nr) continue;
-                    // (pts: relative to the root origin, world-oriented)
-                    float phi = pos.z + pts[k].z;
+                    // (pts: about the contact group's origin, world-oriented)
+                    float phi = pos.z + (pwg.z + pts[k].z);
                     if constexpr (HF) {
                         V3 nk;
                         bool th;
-                        const float gz = ground_at(a, pos.x + pts[k].x, pos.y + pts[k].y, nk, th);
-                        phi = (pos.z + pts[k].z - gz) * nk.z;
+                        const float gz = ground_at(a, pos.x + (pwg.x + pts[k].x), pos.y + (pwg.y + pts[k].y), nk, th);
+                        phi = (pos.z + (pwg.z + pts[k].z) - gz) * nk.z;
                     }
                     phk = k == kr ? phi : phk;
                     // (component-wise: a select of whole V3s becomes a pointer
@@ -2142,7 +2183,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     cen0 = cen0 + pts[k];
                 }
                 const int ro = PL::ROW + i * 8;
-                if (kr < nr) {   // normal row kr: Jacobian about the root origin, separation
+                if (kr < nr) {   // normal row kr: Jacobian about the contact group's origin, separation
                     const SV J = SV{cross(mulT(R, pk), dl), dl};
                     stsv(s, ro, J);
                     // (contact_offset: no row beyond the offset plus the point's free approach)
@@ -2200,7 +2241,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     cl = v3(CP(CL::shape(sh) + 9), CP(CL::shape(sh) + 10), CP(CL::shape(sh) + 11));
                 }
                 const M3 Rs = mul(Rwg, Rsl);
-                const V3 cw = pwg + mul(Rwg, cl);
+                const V3 cw = mul(Rwg, cl);   // (points about the contact group's origin pwg, world-oriented)
                 V3 pts[4];
                 const int nr = M::shape_nrows[sh];
                 const int kind = M::shape_kind[sh];
@@ -2237,9 +2278,9 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 };
                 if constexpr (HF) {
                     bool th;
-                    ground_at(a, pos.x + cw.x, pos.y + cw.y, n, th);
+                    ground_at(a, pos.x + (pwg.x + cw.x), pos.y + (pwg.y + cw.y), n, th);
                     support(n);
-                    ground_at(a, pos.x + pts[0].x, pos.y + pts[0].y, n, th);
+                    ground_at(a, pos.x + (pwg.x + pts[0].x), pos.y + (pwg.y + pts[0].y), n, th);
                     if (th) gmu = a.hf_mu;
                 }
                 support(n);
@@ -2252,15 +2293,15 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 for (int k = 0; k < 4; ++k) {
                     if (k >= nr) break;
                     const int ro = PL::ROW + (rb + k) * 8;
-                    // (pts: relative to the root origin, world-oriented)
-                    float phi = pos.z + pts[k].z;
+                    // (pts: about the contact group's origin, world-oriented)
+                    float phi = pos.z + (pwg.z + pts[k].z);
                     if constexpr (HF) {   // separation along the normal of the point's own triangle
                         V3 nk;
                         bool th;
-                        const float gz = ground_at(a, pos.x + pts[k].x, pos.y + pts[k].y, nk, th);
-                        phi = (pos.z + pts[k].z - gz) * nk.z;
+                        const float gz = ground_at(a, pos.x + (pwg.x + pts[k].x), pos.y + (pwg.y + pts[k].y), nk, th);
+                        phi = (pos.z + (pwg.z + pts[k].z) - gz) * nk.z;
                     }
-                    // row Jacobian in the root frame: (r x d, d), r = the point about the root origin
+                    // row Jacobian in the root frame: (r x d, d), r = the point about the contact group's origin
                     const SV J = SV{cross(mulT(R, pts[k]), dl), dl};
                     stsv(s, ro, J);
                     // (TGS: the separation itself, the PGS forms the sub-step targets;
@@ -2306,9 +2347,15 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             }
             }   // ROWPAR
             TG_SYNC();
-            // row i: root-frame Jacobian J_i (6) -> velocity J_i . v, impulse lam J_i
+            // row i: root-frame Jacobian J_i (6) about its contact group's origin
+            // pc -> velocity J_i . v (v about pc), impulse about the root origin
+            // lam (J.w + pc x J.v, J.v)
             auto rvel = [&](int i, const SV &vg) { return dot(ldsv(s, PL::ROW + i * 8), vg); };
-            auto rforce = [&](int i, float lam) { return lam * ldsv(s, PL::ROW + i * 8); };
+            auto rforce = [&](int i, float lam) {
+                const SV J = ldsv(s, PL::ROW + i * 8);
+                const V3 pc = ldv3(s, M::cgroup[row_cg<M>(i)] * GF + F_P);
+                return lam * SV{J.w + cross(pc, J.v), J.v};
+            };
             for (int i = sub; i < K; i += LPE) {
                 s(PL::VFREE + i) = rvel(i, ldsv(s, PL::CGV + 6 * row_cg<M>(i)));
                 s(PL::LAM + i) = 0.f;
@@ -2339,13 +2386,20 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     }
                 }
                 SV p = -1.0f * rforce(j, 1.0f);
+                const SV Jl = ldsv(s, PL::ROW + j * 8);
                 float du[M::MAXD];
 #pragma unroll
                 for (int i = M::MAXD - 1; i >= 0; --i) {
                     du[i] = 0.f;
                     if (i < lk) {
                         const int g = pk[i];
-                        const float u = -dot(ldSm<M>(s, g, pj[i]), p);
+                        // the contact group's own joint (its axis through pc):
+                        // S . J_root = a . J.w exactly (revolute), a . J.v
+                        // (prismatic) -- not a sum of two ~|pc|-sized terms
+                        const V3 axg = ldv3(s, g * GF + F_AX);
+                        const float uo = (all_revolute<M>() || pj[i] == TG_JOINT_REVOLUTE) ? dot(axg, Jl.w)
+                                                                                            : dot(axg, Jl.v);
+                        const float u = i == lk - 1 ? uo : -dot(ldSm<M>(s, g, pj[i]), p);
                         du[i] = u;
                         p = p + (u * s(g * GF + F_DINV)) * ldsv(s, g * GF + F_U);
                     }
@@ -2362,17 +2416,23 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 SV dvc[M::NCG];
 #pragma unroll
                 for (int c = 0; c < M::NCG; ++c) {
+                    // av about the root origin (the ABA's x needs it), dvc[c]
+                    // about the contact group's origin (the rows')
                     SV av = aj;
+                    const V3 pcc = ldv3(s, M::cgroup[c] * GF + F_P);
+                    SV al = shift_to(aj, pcc);
 #pragma unroll
                     for (int i = 0; i < M::MAXD; ++i) {
                         if (i < M::cpath_len[c]) {
                             const int hg = M::cpath[c][i];
                             const float dui = (i < lk && pk[i] == hg) ? du[i] : 0.0f;
                             const float x = (dui - dot(ldsv(s, hg * GF + F_U), av)) * s(hg * GF + F_DINV);
-                            av = av + x * ldSm<M>(s, hg, M::jtype[hg]);
+                            const V3 axh = ldv3(s, hg * GF + F_AX), Ph = ldv3(s, hg * GF + F_P);
+                            av = av + x * motion_Sm<M>(M::jtype[hg], axh, Ph);
+                            al = al + x * motion_at<M>(M::jtype[hg], axh, Ph, pcc);
                         }
                     }
-                    dvc[c] = av;
+                    dvc[c] = al;
                 }
 #pragma unroll
                 for (int i = 0; i < K; ++i) s(PL::W + i * K + j) = rvel(i, dvc[M::shape_cg[row_shape<M>(i)]]);
