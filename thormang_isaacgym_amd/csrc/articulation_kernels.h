@@ -1076,6 +1076,17 @@ template <class M> __device__ __forceinline__ int row_cg(int i) {
     }
     return r;
 }
+// the contact group's GROUP of row i (lane-dependent i): compares and
+// selects, no table load
+template <class M> __device__ __forceinline__ int row_group(int i) {
+    int r = M::cgroup[M::shape_cg[0]], base = 0;
+#pragma unroll
+    for (int sh = 0; sh < M::NS; ++sh) {
+        r = i >= base ? M::cgroup[M::shape_cg[sh]] : r;
+        base += M::shape_nrows[sh] + shape_nfric<M>(sh);
+    }
+    return r;
+}
 // the most contact points (normal rows) of any shape of the model
 template <class M> __device__ __forceinline__ constexpr int max_shape_rows() {
     int m = 0;

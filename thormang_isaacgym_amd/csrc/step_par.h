@@ -2353,7 +2353,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             auto rvel = [&](int i, const SV &vg) { return dot(ldsv(s, PL::ROW + i * 8), vg); };
             auto rforce = [&](int i, float lam) {
                 const SV J = ldsv(s, PL::ROW + i * 8);
-                const V3 pc = ldv3(s, M::cgroup[row_cg<M>(i)] * GF + F_P);
+                const V3 pc = ldv3(s, row_group<M>(i) * GF + F_P);
                 return lam * SV{J.w + cross(pc, J.v), J.v};
             };
             for (int i = sub; i < K; i += LPE) {
@@ -2386,19 +2386,27 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     }
                 }
                 SV p = -1.0f * rforce(j, 1.0f);
-                const SV Jl = ldsv(s, PL::ROW + j * 8);
+                // the contact group's own joint (its axis through pc): S . J_root
+                // = a . J.w exactly (revolute), a . J.v (prismatic) -- not a sum of
+                // two ~|pc|-sized terms
+                float uo;
+                {
+                    const SV Jl = ldsv(s, PL::ROW + j * 8);
+                    const int go = row_group<M>(j);
+                    const V3 axo = ldv3(s, go * GF + F_AX);
+                    bool rev = true;
+                    if constexpr (!all_revolute<M>()) {
+#pragma unroll
+                        for (int g = 1; g < M::NG; ++g) rev = go == g ? M::jtype[g] == TG_JOINT_REVOLUTE : rev;
+                    }
+                    uo = rev ? dot(axo, Jl.w) : dot(axo, Jl.v);
+                }
                 float du[M::MAXD];
 #pragma unroll
                 for (int i = M::MAXD - 1; i >= 0; --i) {
                     du[i] = 0.f;
                     if (i < lk) {
                         const int g = pk[i];
-                        // the contact group's own joint (its axis through pc):
-                        // S . J_root = a . J.w exactly (revolute), a . J.v
-                        // (prismatic) -- not a sum of two ~|pc|-sized terms
-                        const V3 axg = ldv3(s, g * GF + F_AX);
-                        const float uo = (all_revolute<M>() || pj[i] == TG_JOINT_REVOLUTE) ? dot(axg, Jl.w)
-                                                                                            : dot(axg, Jl.v);
                         const float u = i == lk - 1 ? uo : -dot(ldSm<M>(s, g, pj[i]), p);
                         du[i] = u;
                         p = p + (u * s(g * GF + F_DINV)) * ldsv(s, g * GF + F_U);
@@ -2413,12 +2421,39 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
 #pragma unroll
                     for (int k = 0; k < 6; ++k) s(scr(j * SW + M::MAXD + k)) = av[k];
                 }
-                SV dvc[M::NCG];
+                if constexpr (M::NG <= 8) {
+                    // small trees: the ABA's x from the walk about the root
+                    // origin as before, the response about pcc accumulated
+                    // beside it (A/B round 6: the form below cost the scooter
+                    // +1.6 us, this one +0.3)
+                    SV dvc[M::NCG];
+#pragma unroll
+                    for (int c = 0; c < M::NCG; ++c) {
+                        SV av = aj;
+                        const V3 pcc = ldv3(s, M::cgroup[c] * GF + F_P);
+                        SV al = shift_to(aj, pcc);
+#pragma unroll
+                        for (int i = 0; i < M::MAXD; ++i) {
+                            if (i < M::cpath_len[c]) {
+                                const int hg = M::cpath[c][i];
+                                const float dui = (i < lk && pk[i] == hg) ? du[i] : 0.0f;
+                                const float x = (dui - dot(ldsv(s, hg * GF + F_U), av)) * s(hg * GF + F_DINV);
+                                const V3 axh = ldv3(s, hg * GF + F_AX), Ph = ldv3(s, hg * GF + F_P);
+                                av = av + x * motion_Sm<M>(M::jtype[hg], axh, Ph);
+                                al = al + x * motion_at<M>(M::jtype[hg], axh, Ph, pcc);
+                            }
+                        }
+                        dvc[c] = al;
+                    }
+#pragma unroll
+                    for (int i = 0; i < K; ++i) s(PL::W + i * K + j) = rvel(i, dvc[M::shape_cg[row_shape<M>(i)]]);
+                } else {
 #pragma unroll
                 for (int c = 0; c < M::NCG; ++c) {
-                    // av about the root origin (the ABA's x needs it), dvc[c]
-                    // about the contact group's origin (the rows')
-                    SV av = aj;
+                    // large trees: one accumulator, the walk carried about the
+                    // contact group's origin pcc (two per path cost the humanoid
+                    // 60 more registers, spilled): U . a is invariant, so each U
+                    // moves to pcc with it (moment - pcc x force)
                     const V3 pcc = ldv3(s, M::cgroup[c] * GF + F_P);
                     SV al = shift_to(aj, pcc);
 #pragma unroll
@@ -2426,16 +2461,18 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                         if (i < M::cpath_len[c]) {
                             const int hg = M::cpath[c][i];
                             const float dui = (i < lk && pk[i] == hg) ? du[i] : 0.0f;
-                            const float x = (dui - dot(ldsv(s, hg * GF + F_U), av)) * s(hg * GF + F_DINV);
-                            const V3 axh = ldv3(s, hg * GF + F_AX), Ph = ldv3(s, hg * GF + F_P);
-                            av = av + x * motion_Sm<M>(M::jtype[hg], axh, Ph);
-                            al = al + x * motion_at<M>(M::jtype[hg], axh, Ph, pcc);
+                            const SV Uh = ldsv(s, hg * GF + F_U);
+                            const float x = (dui - dot(SV{Uh.w - cross(pcc, Uh.v), Uh.v}, al)) * s(hg * GF + F_DINV);
+                            al = al + x * motion_at<M>(M::jtype[hg], ldv3(s, hg * GF + F_AX), ldv3(s, hg * GF + F_P), pcc);
                         }
                     }
-                    dvc[c] = al;
-                }
+                    // column j's entries of the rows on contact group c (no
+                    // per-group response array held across the groups)
 #pragma unroll
-                for (int i = 0; i < K; ++i) s(PL::W + i * K + j) = rvel(i, dvc[M::shape_cg[row_shape<M>(i)]]);
+                    for (int i = 0; i < K; ++i)
+                        if (M::shape_cg[row_shape<M>(i)] == c) s(PL::W + i * K + j) = rvel(i, al);
+                }
+                }
                 // a row with no response (W_jj ~ 0: a shape on a fixed base, a
                 // normal row through a fixed-base scooter's wheel) gets a huge
                 // diagonal, so the sweeps give it a multiplier ~1e-30 times its
