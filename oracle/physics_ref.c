@@ -729,16 +729,18 @@ static int support_points(const tg_model_desc *m, int s, const M3 R, const V3 c,
     return 0;
 }
 
-/* physx.contact_offset (round 5): a point whose separation above the rest
- * offset is not below the contact offset plus its free approach over the
- * substep, max(0, -vn) h, has no normal row this substep -- its separation
- * becomes NO_ROW, whose target -NO_ROW/h no row velocity reaches, so its
- * multiplier stays 0 (the kernel's contact_row_phi, articulation_kernels.h).
- * contact_offset <= 0: every point speculative (rounds 1-4). */
+/* physx.contact_offset (round 6: PhysX's pair rule): a point
+ * generates a contact (a speculative normal row) only while its separation is
+ * below the pair's contact distance, the sum of the shape's and the ground
+ * plane's offsets, both the scene's contact_offset -- 2 x contact_offset.
+ * Beyond it the separation becomes NO_ROW, whose target -NO_ROW/h no row
+ * velocity reaches, so its multiplier stays 0 (the kernel's contact_row_phi,
+ * articulation_kernels.h, which records why round 5's velocity-dependent
+ * gate was dropped).  contact_offset <= 0: every point speculative. */
 #define NO_ROW ((real)1e30f)
-static real contact_row_phi(const tg_sim_params *sp, real phi, real vn, real h) {
-    const real off = sp->contact_offset, ap = vn < 0 ? -vn : 0;
-    return (off > 0 && !(phi - sp->rest_offset < off + ap * h)) ? NO_ROW : phi;
+static real contact_row_phi(const tg_sim_params *sp, real phi) {
+    const real off = sp->contact_offset;
+    return (off > 0 && !(phi < 2 * off)) ? NO_ROW : phi;
 }
 
 static int collect_rows(const Env *e, Work *w, real h, const V6 *vg, Row *rows, Patch *patches, int *npatch) {
@@ -789,7 +791,7 @@ static int collect_rows(const Env *e, Work *w, real h, const V6 *vg, Row *rows, 
             for (int j = 0; j < 3; ++j) rel[j] = pts[k][j] - w->pw[g][j];
             m3T_v(w->Rw[g], rel, r->r);
             memcpy(r->d, n, sizeof(V3));
-            r->phi = contact_row_phi(e->sp, phi, row_vel(w, r, vg), h);
+            r->phi = contact_row_phi(e->sp, phi);
             r->target = row_target(e->sp, r->phi, h);
             real wv = (margin - phi) / margin;
             wk[k] = wv < 0 ? 0 : (wv > 1 ? 1 : wv);

@@ -564,8 +564,14 @@ def walk_kneel_forced(num_envs=32, steps=200, seed=0, amp=0.2):
     return err
 
 
-def make_gpu_walk(cfg, draws):
+def make_gpu_walk(cfg, draws, torch_seed=0):
+    """The GPU walk env, its task draws replayed from ``draws``.  The
+    randomization_params samples (vec_task.apply_randomizations) come from
+    torch's global generator, as in the reference: seeded here so a DR run
+    is the same whatever ran before it in the process."""
+    import torch
     from thormang_isaacgym_amd.tasks.thormang_walk import ThormangWalk
+    torch.manual_seed(torch_seed)
 
     class ReplayWalk(ThormangWalk):
         draw_source = draws

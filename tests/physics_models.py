@@ -141,22 +141,33 @@ def jit_walker():
 
 def contact_offset_checks(make_step=None, solver_type=1, contact_offset=0.02):
     """Known answers of the contact_offset gate, for the oracle or
-    the GPU (``step_fn`` as in drop_box), with the walk cfg's step (dt 1/60 x
-    2 substeps, h = 1/120) and contact_margin 0.05:
+    the GPU (``make_step()`` returns a fresh drop_box ``step_fn`` per run),
+    with the walk cfg's step (dt 1/60 x 2 substeps, h = 1/120) and
+    contact_margin 0.05.  The rule is PhysX's: a contact exists while the
+    separation is below the pair's contact distance, the shape's plus the
+    ground plane's offset (2 x 0.02 = 4 cm here).
 
-    * ``rest_gap``: a box at rest whose separation (3 cm) lies between the
-      offset (2 cm) and the margin takes no normal impulse -- one step is the
-      exact semi-implicit free fall, z0 - 3 g h^2, vz = -2 g h;
-    * ``fast``: the same box approaching at 6 m/s (0.05 m per substep, more
-      than its 3 cm gap) gets a row from its free approach and lands on the
-      ground instead of tunnelling (free flight would end 2 cm below it).
+    * ``rest_gap``: a box at rest 4.5 cm up (beyond the pair distance, within
+      the margin) takes no normal impulse -- one step is the exact
+      semi-implicit free fall, z0 - 3 g h^2, vz = -2 g h;
+    * ``fast``: a box 3.5 cm up (inside the pair distance) approaching at
+      6 m/s (0.05 m per substep) has its speculative row and lands on the
+      ground in the first substep (free flight would end 1.6 cm below it);
+    * ``beyond``: the same approach from 4.5 cm up has no row in the first
+      substep (PhysX without CCD: it passes the surface by ~6 mm), then the
+      row and the push-out bring it back to rest.
     Returns a dict of the measured quantities."""
     g, h, half = 9.81, 1.0 / 120.0, 0.05
-    z0 = half + 0.03
     mk = make_step or (lambda: None)
+    z0 = half + 0.045
     zs, vs = drop_box(solver_type, z0=z0, steps=1, step_fn=mk(), contact_offset=contact_offset)
     out = {"rest_gap_dz": float(zs[0] - (z0 - 3 * g * h * h)), "rest_gap_dvz": float(vs[0] + 2 * g * h)}
+    z0 = half + 0.035
     zs, vs = drop_box(solver_type, z0=z0, steps=20, step_fn=mk(), contact_offset=contact_offset, vz0=-6.0)
     out.update(fast_min_z=float(zs.min()) - half, fast_z1=float(zs[0]) - half, fast_vz1=float(vs[0]),
                fast_final=float(zs[-1]) - half, free_flight_z1=float(z0 - 2 * 6.0 * h - 3 * g * h * h) - half)
+    z0 = half + 0.045
+    zs, vs = drop_box(solver_type, z0=z0, steps=40, substeps=2, step_fn=mk(), contact_offset=contact_offset,
+                      vz0=-6.0)
+    out.update(beyond_min_z=float(zs.min()) - half, beyond_final=float(zs[-1]) - half, beyond_vz_final=float(vs[-1]))
     return out

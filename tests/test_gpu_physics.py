@@ -132,9 +132,10 @@ def test_gpu_landing_known_answer_no_rebound_and_rest_height(solver, viters, res
 @pytest.mark.parametrize("solver", [0, 1])
 def test_gpu_contact_offset_known_answers(solver):
     """The contact_offset known answers of tests/test_solver_cfg.py on the GPU
-    kernel: a 3 cm resting gap beyond the 2 cm offset is exact
-    free flight; a 6 m/s approach closing it within the substep lands
-    without tunnelling."""
+    kernel (PhysX's pair rule): a resting gap beyond 2 x the offset
+    is exact free flight; a 6 m/s approach from inside it lands without
+    tunnelling; from beyond it, passes the surface in one substep and
+    recovers."""
     if not torch.cuda.is_available():
         pytest.skip("needs the MI355X")
 
@@ -153,6 +154,8 @@ def test_gpu_contact_offset_known_answers(solver):
     assert abs(g["rest_gap_dz"]) < 1e-6 and abs(g["rest_gap_dvz"]) < 1e-5, g
     assert g["fast_min_z"] > -0.002 and g["fast_z1"] > -0.002, g
     assert g["fast_vz1"] > -0.5 and abs(g["fast_final"]) < 1e-3, g
+    assert g["beyond_min_z"] < -0.003, g
+    assert abs(g["beyond_final"]) < 2e-3 and abs(g["beyond_vz_final"]) < 0.05, g
 
 
 def test_gpu_free_fall_exact():

@@ -251,15 +251,17 @@ def test_contact_offset_default_follows_the_vec_task_base():
 @pytest.mark.parametrize("solver", [0, 1])
 def test_contact_offset_known_answers(solver):
     """the contact_offset gate checked against what it must do, not
-    against the kernel (both restate the same rule): a resting gap wider than
-    the offset is free flight, exactly; a fast approach that closes the gap
-    within the substep gets a row and does not tunnel
+    against the kernel (both restate the same rule), PhysX's pair rule (a
+    contact while the separation is below the shape's plus the plane's
+    offset): a resting gap beyond it is free flight, exactly; a fast approach
+    from inside it lands without tunnelling; the same approach from beyond it
+    gets no row in its first substep (no CCD), then comes back to rest
     (tests/physics_models.contact_offset_checks; GPU twin in
-    tests/test_gpu_physics.py).  The gate is one offset plus the free
-    approach; PhysX's is the sum of both shapes' offsets without the approach
-    term."""
+    tests/test_gpu_physics.py)."""
     r = pm.contact_offset_checks(solver_type=solver)
     assert abs(r["rest_gap_dz"]) < 1e-7 and abs(r["rest_gap_dvz"]) < 1e-6, r   # (the state is stored in fp32)
-    assert r["free_flight_z1"] < -0.015, r                    # without a row it would end below the ground
+    assert r["free_flight_z1"] < -0.01, r                     # without a row it would end below the ground
     assert r["fast_min_z"] > -0.002 and r["fast_z1"] > -0.002, r
     assert r["fast_vz1"] > -0.5 and abs(r["fast_final"]) < 1e-3, r
+    assert r["beyond_min_z"] < -0.003, r                      # passed the surface in the row-less substep
+    assert abs(r["beyond_final"]) < 2e-3 and abs(r["beyond_vz_final"]) < 0.05, r

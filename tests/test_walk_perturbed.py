@@ -1,5 +1,5 @@
 """CPU tests of the standing-walk yardstick (tests/gpu_harness.py
-perturbed_walk_oracle, used by test_gpu_walk_standing_free_running_1000_steps):
+perturbed_walk_oracle, used by the fp32 ensembles of tests/test_gpu_parity_seeds.py):
 the perturbation is a rounding-level, reproducible change of the initial
 state, and it leaves the reference's first steps inside the 1e-3 band."""
 import numpy as np

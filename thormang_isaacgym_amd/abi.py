@@ -244,8 +244,9 @@ def unhonoured_physx_keys(physx: dict, asset_opts: dict | None = None) -> Dict[s
     the reason.  ``solver_type`` 0 (PGS) and 1 (TGS, the position iterations
     as sub-steps with re-formed contact targets, DESIGN.md §4 "Solver cfg")
     are honoured, any other value is reported; ``contact_offset`` is honoured
-    since round 5 (a point's normal row exists only within the offset plus
-    its free approach over the substep, ``tg_sim_params.contact_offset``);
+    since round 5 (round 6: PhysX's pair rule -- a point's normal row exists
+    only while its separation is below the shape's plus the ground plane's
+    offset, 2 x ``tg_sim_params.contact_offset``);
     ``bounce_threshold_velocity`` is inert (``PHYSX_INERT_KEYS``).  Unknown
     keys are reported too."""
     ao = asset_opts or {}

@@ -1125,17 +1125,24 @@ template <class M> __device__ __forceinline__ bool row_normal(int k) {
 __device__ __forceinline__ float contact_target(const StepArgs &a, float phi, float dt) {
     return phi > a.rest ? -(phi - a.rest) / dt : fminf(a.baumgarte * (a.rest - phi) / dt, a.max_depen);
 }
-// physx.contact_offset (round 5): a point whose separation
-// above the rest offset is not below the contact offset plus its free
-// approach over the substep, max(0, -vn) h, has no normal row this substep --
-// its separation becomes TG_NO_ROW, whose target (-TG_NO_ROW / h) no row
-// velocity reaches, so its multiplier stays 0 in every sweep (PGS and TGS
-// sub-steps alike) and its patch's friction limit counts nothing from it.
-// vn: the point's free normal velocity (row Jacobian . contact group's free
-// velocity).  oracle/physics_ref.c collect_rows applies the same rule.
+// physx.contact_offset: PhysX's pair rule (round 6).  A point
+// generates a contact -- a speculative normal row -- only while its separation
+// is below the pair's contact distance, the sum of the two shapes' offsets:
+// the shape's and the ground plane's, both the scene's contact_offset, so 2 x
+// contact_offset.  Beyond it the separation becomes TG_NO_ROW, whose target
+// (-TG_NO_ROW / h) no row velocity reaches, so its multiplier stays 0 in every
+// sweep (PGS and TGS sub-steps alike) and its patch's friction limit counts
+// nothing from it.  Round 5's rule (one offset plus the point's free approach
+// over the substep) gated rows in exactly where they start to matter: a foot
+// corner whose free approach just reached the gate took a 1.15 N s impulse
+// when present and none when absent, a discontinuity that rounding alone
+// crossed (a GPU-only 0.2 rad/s outlier at 16384 envs, 24 of 48 one-ulp
+// perturbed oracle replays on either side).  Distance alone
+// gates at a separation no foot or wheel closes within a substep.
+// oracle/physics_ref.c collect_rows applies the same rule.
 #define TG_NO_ROW 1e30f
-__device__ __forceinline__ float contact_row_phi(const StepArgs &a, float phi, float vn, float h) {
-    return (a.coff > 0.f && !(phi - a.rest < a.coff + fmaxf(-vn, 0.f) * h)) ? TG_NO_ROW : phi;
+__device__ __forceinline__ float contact_row_phi(const StepArgs &a, float phi) {
+    return (a.coff > 0.f && !(phi < 2.f * a.coff)) ? TG_NO_ROW : phi;
 }
 
 }  // namespace tg

@@ -2186,8 +2186,8 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 if (kr < nr) {   // normal row kr: Jacobian about the contact group's origin, separation
                     const SV J = SV{cross(mulT(R, pk), dl), dl};
                     stsv(s, ro, J);
-                    // (contact_offset: no row beyond the offset plus the point's free approach)
-                    const float phr = contact_row_phi(a, phk, dot(J, ldsv(s, PL::CGV + 6 * cgi)), h);
+                    // (contact_offset: no row beyond the pair's contact distance)
+                    const float phr = contact_row_phi(a, phk);
                     s(ro + 6) = a.tgs ? phr : contact_target(a, phr, h);
                     s(ro + 7) = 1.f;
                 } else {         // friction row t of the patch
@@ -2305,8 +2305,8 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     const SV J = SV{cross(mulT(R, pts[k]), dl), dl};
                     stsv(s, ro, J);
                     // (TGS: the separation itself, the PGS forms the sub-step targets;
-                    // contact_offset: no row beyond the offset plus the point's free approach)
-                    const float phr = contact_row_phi(a, phi, dot(J, ldsv(s, PL::CGV + 6 * cgi)), h);
+                    // contact_offset: no row beyond the pair's contact distance)
+                    const float phr = contact_row_phi(a, phi);
                     s(ro + 6) = a.tgs ? phr : contact_target(a, phr, h);
                     s(ro + 7) = 1.f;
                     wk[k] = fminf(fmaxf((a.margin - phi) / a.margin, 0.f), 1.f);
