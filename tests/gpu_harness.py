@@ -309,14 +309,49 @@ def sync_dr(orc, env):
               "gravity": np.asarray(sim.gravity, np.float32)}
 
 
-def forced_step_errors(env, orc, act_fn, steps, act_to_orc=lambda a: a, ctl=None):
+def certify_discontinuity(orc, e, gpu_root, tol=1e-3, draws=48, seed=5):
+    """Is env ``e``'s one-step GPU-vs-oracle disagreement a discontinuity of
+    the restated physics that rounding alone crosses?  The oracle env (one
+    that keeps its physics inputs, ``OracleWalk.replay_env``) steps the env
+    again from ``draws`` inputs each moved by about one fp32 ulp (relative
+    1.2e-7, random signs): if any replay lands within ``tol`` of the GPU's
+    root state, the GPU's result is one the fp64 oracle itself produces from
+    inputs indistinguishable in fp32, i.e. the step is bimodal at rounding
+    level (round 6: a foot corner at the contact gate, PhysX's pair rule,
+    that takes ~1 N s when present and none when absent).
+    An env whose unperturbed replay already matches the GPU's root is not
+    certified (its disagreement is elsewhere).  Returns (certified, the
+    nearest replay's distance)."""
+    if not hasattr(orc, "replay_env"):
+        return False, float("inf")
+    rs = np.random.default_rng(seed)
+    root0, dof0 = orc.phys_inputs(e)
+    if float(np.abs(orc.replay_env(e, root0, dof0) - gpu_root).max()) < tol:
+        return False, 0.0   # the root agrees: whatever differs is not a jump of the physics
+    best = float("inf")
+    for _ in range(draws):
+        r = (root0 * (1 + rs.choice([-1.0, 1.0], root0.shape) * 1.2e-7)).astype(np.float32)
+        d = (dof0 * (1 + rs.choice([-1.0, 1.0], dof0.shape) * 1.2e-7)).astype(np.float32)
+        best = min(best, float(np.abs(orc.replay_env(e, r, d) - gpu_root).max()))
+        if best < tol:
+            return True, best
+    return False, best
+
+
+def forced_step_errors(env, orc, act_fn, steps, act_to_orc=lambda a: a, ctl=None, certify=False):
     """1-step GPU-vs-oracle errors along a GPU trajectory (oracle re-synced from
     the GPU state before every step).  Returns max errors and exact-match flags;
     with ``ctl`` (the fp32 oracle build, re-synced alike) also its one-step
-    errors against the fp64 oracle (``within``)."""
+    errors against the fp64 oracle (``within``).
+
+    ``certify`` (oracles with ``replay_env``): an env-step whose GPU result
+    leaves 1e-3 of the oracle's is checked with ``certify_discontinuity``; a
+    certified one is left out of the maxima and the reset comparison of that
+    step and listed in ``err["certified"]`` (step, env, its error, the
+    nearest perturbed replay's distance) -- an uncertified one counts in full."""
     import torch
     err = {"obs": 0.0, "rew": 0.0, "root": 0.0, "reset_equal": True, "timeout_equal": True, "steps": steps,
-           "resets": 0}
+           "resets": 0, "certified": []}
     if ctl is not None:
         err["obs_f32"] = err["rew_f32"] = 0.0
     obs = orc.a["obs_buf"].copy()
@@ -334,10 +369,20 @@ def forced_step_errors(env, orc, act_fn, steps, act_to_orc=lambda a: a, ctl=None
             err["obs_f32"] = max(err["obs_f32"], maxerr(c_obs, o_obs))
             err["rew_f32"] = max(err["rew_f32"], maxerr(c_rew, o_rew))
         g_obs = obs_d["obs"].cpu().numpy()
-        err["obs"] = max(err["obs"], maxerr(g_obs, o_obs))
-        err["rew"] = max(err["rew"], maxerr(rew.cpu().numpy(), o_rew))
-        err["root"] = max(err["root"], maxerr(env.root_tensor.cpu().numpy(), orc.a["root"]))
-        err["reset_equal"] &= bool(np.array_equal(reset.cpu().numpy(), o_reset))
+        g_rew, g_root, g_reset = rew.cpu().numpy(), env.root_tensor.cpu().numpy(), reset.cpu().numpy()
+        keep = np.ones(len(g_rew), bool)
+        if certify:
+            pe = np.maximum(np.abs(g_obs - o_obs).reshape(len(g_rew), -1).max(1),
+                            np.maximum(np.abs(g_rew - o_rew), np.abs(g_root - orc.a["root"]).max(1)))
+            for i in np.nonzero(~(pe < 1e-3) | (g_reset != o_reset))[0]:
+                ok, dist = certify_discontinuity(orc, int(i), g_root[i])
+                if ok:
+                    keep[i] = False
+                    err["certified"].append((t, int(i), float(pe[i]), dist))
+        err["obs"] = max(err["obs"], maxerr(g_obs[keep], o_obs[keep]))
+        err["rew"] = max(err["rew"], maxerr(g_rew[keep], o_rew[keep]))
+        err["root"] = max(err["root"], maxerr(g_root[keep], orc.a["root"][keep]))
+        err["reset_equal"] &= bool(np.array_equal(g_reset[keep], o_reset[keep]))
         err["timeout_equal"] &= bool(np.array_equal(extras["time_outs"].cpu().numpy().astype(np.uint8), o_to))
         err["resets"] += int(o_reset.sum())
         obs = g_obs
@@ -425,7 +470,7 @@ def walk_forced(num_envs=32, steps=1000, seed=0, task="ThormangWalk", dr=False, 
     ctl = OracleWalk(mk(), NumpyDraws(seed), precision="f32") if control else None
     rs = np.random.default_rng(seed + 100)
     err = forced_step_errors(env, orc, lambda o: rs.uniform(-0.5, 0.5, (num_envs, orc.D)).astype(np.float32), steps,
-                             ctl=ctl)
+                             ctl=ctl, certify=True)
     if dr:
         note_dr_ranges(err, env)
     return err
@@ -498,11 +543,30 @@ class OracleWalk:
         self.L.oracle_walk_post_physics(C.byref(self.p), C.byref(self.b), None, ptr(zeros))
         a["progress_buf"][:] = saved
 
+    def phys_inputs(self, e):
+        """Env e's root and dof state as the last step's physics started from."""
+        return self._pin["root"][e].copy(), self._pin["dof"][e * self.D:(e + 1) * self.D].copy()
+
+    def replay_env(self, e, root, dof, precision="f64"):
+        """The last step's physics of env e alone from the given root / dof
+        state (every other input as that step had it); returns the root after
+        it (certify_discontinuity)."""
+        pin, D = self._pin, self.D
+        r, d = np.array(root[None], np.float32), np.array(dof, np.float32)   # (copies: stepped in place)
+        dr = {k: (np.ascontiguousarray(v[e:e + 1]) if k != "gravity" else v) for k, v in pin["dr"].items()}
+        physics_step(self.desc, self.sp, r, d, np.ascontiguousarray(self.props[:, e:e + 1, :]),
+                     pin["pos_target"][e:e + 1].copy(), np.zeros((1, D), np.float32),
+                     force=None if pin["force"] is None else pin["force"][e:e + 1].copy(), threads=1,
+                     L=lib(precision), **dr)
+        return r[0]
+
     def step(self, actions):
         a, n, D = self.a, self.n, self.D
         self.L.oracle_walk_pre_physics(C.byref(self.p), C.byref(self.b),
                                        ptr(np.ascontiguousarray(actions, np.float32)))
         force = a["body_force"] if self.push else None
+        self._pin = {"root": a["root"].copy(), "dof": a["dof_state"].copy(), "pos_target": a["pos_target"].copy(),
+                     "force": None if force is None else force.copy(), "dr": dict(self.dr)}
         physics_step(self.desc, self.sp, a["root"], a["dof_state"], self.props, a["pos_target"],
                      np.zeros((n, D), np.float32), force=force, threads=self.threads, L=self.L, **self.dr)
         ids = np.nonzero(a["reset_buf"])[0]
@@ -557,7 +621,7 @@ def walk_kneel_forced(num_envs=32, steps=200, seed=0, amp=0.2):
     def act_fn(obs):
         zmin[0] = min(zmin[0], float(env.root_tensor[:, 2].min()))
         return rs.uniform(-amp, amp, (num_envs, orc.D)).astype(np.float32)
-    err = forced_step_errors(env, orc, act_fn, steps)
+    err = forced_step_errors(env, orc, act_fn, steps, certify=True)
     torch.cuda.synchronize()
     err["pelvis_zmin"] = min(zmin[0], float(env.root_tensor[:, 2].min()))
     err["shapes"] = len(env.model.shapes)

@@ -138,6 +138,12 @@ __device__ __forceinline__ int scr(int x) { return (x / 21) * GF + F_IA + x % 21
 __device__ __forceinline__ M3 ldR(const LE &s, int g) { return transpose(ldm3(s, g * GF + F_RT)); }
 __device__ __forceinline__ void stR(const LE &s, int g, const M3 &R) { stm3(s, g * GF + F_RT, transpose(R)); }
 
+// round 6: leaf groups' joint-space inertia from their local rigid inertia
+// (step_par_kernel d0l); 0 = pass 2b's root-origin form for every group (A/B)
+#ifndef TG_LEAF_D0
+#define TG_LEAF_D0 1
+#endif
+
 // per-group model table in LDS (ints; axis as float bits), built once per block
 enum : int { GI_PARENT = 0, GI_DOF = 1, GI_JT = 2, GI_NCH = 3, GI_CH = 4 };
 
@@ -1334,6 +1340,15 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             vlim[r] = g < M::NG ? PR(TG_PROP_VELOCITY, bounded(gi[g * GIW + GI_DOF], 0, 1 << 16)) : 0.f;
         }
         }
+        // a leaf group's joint-space inertia D0 = S.I.S from its own rigid
+        // inertia about its joint (group frame: the axis is e_z), Izz + m (cx^2
+        // + cy^2) (revolute) or m (prismatic) -- pass 2b's S.(I^A S) forms it
+        // from the inertia about the ROOT origin, where a wheel 0.8 m away
+        // carries m |P|^2 ~ 35x its spin inertia and loses those digits
+        // (round 6); -1 = not a leaf.  Formed in pass 1b, used by pass 2a.
+        float d0l[NR1];
+#pragma unroll
+        for (int r = 0; r < NR1; ++r) d0l[r] = -1.f;
 #pragma unroll 1
         for (int cp = 0; cp < 2; ++cp) {
 #if defined(TG_SECTION_PROF) && defined(TG_CLAMP_COUNT)
@@ -1603,6 +1618,13 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
         for (int r = 0; r < NRX; ++r) {
             const int g = sub + r * LPE;
             if (g < M::NG) body_bias(g, ldsv(s, g * GF + F_V), ldR(s, g), ldv3(s, g * GF + F_P), gr, cin[r]);
+            if constexpr (TG_LEAF_D0) {
+                const int gl = min(g, M::NG - 1);
+                const bool leaf = g > 0 && g < M::NG && gi[gl * GIW + GI_NCH] == 0;
+                const bool rev = all_revolute<M>() || gi[gl * GIW + GI_JT] == TG_JOINT_REVOLUTE;
+                const float *ci = cin[r];
+                d0l[r] = leaf ? (rev ? ci[6] + ci[0] * (ci[1] * ci[1] + ci[2] * ci[2]) : ci[0]) : -1.f;
+            }
         }
         TG_SYNC();
         }   // pass 1
@@ -1674,10 +1696,12 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                     s(o + F_CL + 2) = eff;
                 }
                 if (!SEPC || cp == 0) stsv(s, o + F_V, cbv);
-                s(o + F_DINV) = (1.f + be) * cd[0] + Dimp;
-                s(o + F_UU) = tau + al * cd[0];
-                s(o + F_QDS) = al;
-                s(o + F_C1) = 1.f + be;
+                // (a leaf: D and u complete here from its local D0, pass 2b adds 0 x D0)
+                const bool lf = TG_LEAF_D0 && d0l[r] >= 0.f;
+                s(o + F_DINV) = (1.f + be) * cd[0] + Dimp + (lf ? (1.f + be) * d0l[r] : 0.f);
+                s(o + F_UU) = tau + al * cd[0] + (lf ? al * d0l[r] : 0.f);
+                s(o + F_QDS) = lf ? 0.f : al;
+                s(o + F_C1) = lf ? 0.f : 1.f + be;
             }
         }
         } else {   // one round (small trees): loads consumed at once, branches kept
@@ -1733,10 +1757,12 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 // cb replaces v (dead after pass 1b) in F_V; on a SEPC rerun pass 1
                 // was not rerun and F_V already holds cb
                 if (!SEPC || cp == 0) stsv(s, o + F_V, crm(ldsv(s, o + F_V), qd * ldSm<M>(s, g, bounded(gi[g * GIW + GI_JT], 0, 4))));
-                s(o + F_DINV) = (1.f + be) * cd[0] + Dimp;
-                s(o + F_UU) = tau + al * cd[0];
-                s(o + F_QDS) = al;
-                s(o + F_C1) = 1.f + be;
+                // (a leaf: D and u complete here from its local D0, pass 2b adds 0 x D0)
+                const bool lf = TG_LEAF_D0 && d0l[r] >= 0.f;
+                s(o + F_DINV) = (1.f + be) * cd[0] + Dimp + (lf ? (1.f + be) * d0l[r] : 0.f);
+                s(o + F_UU) = tau + al * cd[0] + (lf ? al * d0l[r] : 0.f);
+                s(o + F_QDS) = lf ? 0.f : al;
+                s(o + F_C1) = lf ? 0.f : 1.f + be;
             }
         }
         }
