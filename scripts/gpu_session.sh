@@ -7,17 +7,17 @@
 # step paths, the HBM PMC passes and the SQ / LDS counter passes of the two
 # headline workloads, and the register / scratch use of every step kernel.
 # Every GPU step has its own time limit; a failure stops the script.
-#   ROUND=5 bash scripts/gpu_session.sh            (everything, into gpurun_out/final$ROUND)
+#   ROUND=6 bash scripts/gpu_session.sh            (everything, into gpurun_out/final$ROUND)
 #   SKIP_TESTS=1 SKIP_PROF=1 ... / ONLY_PROF=1     (parts; the GPU call's time limit is 20 min)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-ROUND=${ROUND:-5}
+ROUND=${ROUND:-6}
 OUT=${OUT_DIR:-gpurun_out/final$ROUND}
 mkdir -p $OUT
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 if [ -n "${ONLY_PROF:-}" ]; then SKIP_TESTS=1; SKIP_BENCH=1; fi
 if [ -z "${SKIP_TESTS:-}" ]; then
-  timeout -k 10 700 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -v -s --timeout 600 --timeout-method thread > $OUT/gpu_tests.log 2>  timeout -k 10 700 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&11
   rc=$?; tail -2 $OUT/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit $?
   tail -1 $OUT/smoke.log
