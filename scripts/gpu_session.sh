@@ -17,7 +17,7 @@ mkdir -p $OUT
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 if [ -n "${ONLY_PROF:-}" ]; then SKIP_TESTS=1; SKIP_BENCH=1; fi
 if [ -z "${SKIP_TESTS:-}" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -v -s --timeout 600 --timeout-method thread > $OUT/gpu_tests.log 2>  timeout -k 10 700 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&11
+  timeout -k 10 900 python -u -m pytest tests -m gpu -v -s --timeout 600 --timeout-method thread > $OUT/gpu_tests.log 2>&1
   rc=$?; tail -2 $OUT/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit $?
   tail -1 $OUT/smoke.log
