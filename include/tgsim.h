@@ -153,11 +153,12 @@ typedef struct tg_sim_params {
                                      before each sweep a normal row's target is re-formed from its
                                      separation advanced by the row's accumulated displacement, and
                                      the positions integrate the mean of the sweeps' multipliers */
-    float contact_offset;         /* physx.contact_offset (IsaacGym default 0.02): a shape point gets a
-                                     normal row in a substep only while its separation above the rest
-                                     offset is below contact_offset plus its free approach over the
-                                     substep (max(0, -v_n) h); <= 0: every point speculative (the
-                                     rounds 1-4 behaviour) */
+    float contact_offset;         /* physx.contact_offset (IsaacGym default 0.02): PhysX's pair rule --
+                                     a shape point carries a (speculative) normal row only while its
+                                     separation is below the pair's contact distance, the shape's plus
+                                     the ground plane's offset, 2 x contact_offset (round 6; round 5
+                                     used one offset plus the point's free approach); <= 0: every
+                                     point speculative (the rounds 1-4 behaviour) */
 } tg_sim_params;
 
 /* zero-copy device views (gymtorch.wrap_tensor equivalents) */
