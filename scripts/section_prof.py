@@ -31,11 +31,13 @@ def main():
     buf = (C.c_ulonglong * 24)()
     L.tg_prof_read(buf, 24)
     # sub-sections [16..] are cut out of the section that follows them
+    if os.environ.get("TG_PROF_RAW"):
+        print("raw slots:", list(buf))
     sec = list(buf[:len(NAMES)])
-    sec[1] += buf[16]
+    sec[1] += buf[16] + buf[20]
     sec[2] += buf[17] + buf[18]
     tot = sum(sec)
-    subs = {1: [("1a schedule fwd", 16), ("1b all groups", None)],
+    subs = {1: [("1a schedule fwd", 16), ("1a, substep 0 (TG_PROF_SPLIT0)", 20), ("1b all groups", None)],
             2: [("2a all groups", 17), ("2b schedule bwd", 18), ("root solve", None)]}
     for i, (n, v) in enumerate(zip(NAMES, sec)):
         print(f"{n:14s} {v / tot * 100:6.2f} %  {v:14d}")

@@ -45,24 +45,37 @@ namespace tg {
 #ifdef TG_SECTION_PROF
 // developer build only: per-section cycle counts summed over thread 0 of every block
 static __device__ unsigned long long tg_prof_acc[24];   // [16..]: sub-sections (see scripts/section_prof.py)
-#define TG_PROF_INIT unsigned long long tg_t0 = clock64();
+// (round 6: the per-block sums accumulate in LDS and reach the global
+// counters once, at the kernel's end -- a global atomic per stamp made every
+// block wait on the same address after the synchronised stamps, which
+// inflated the section after them, pass 1a of substeps 2 and 3 most)
+#define TG_PROF_INIT                                                            \
+    __shared__ unsigned long long tg_prof_l[24];                                \
+    if (threadIdx.x == 0)                                                       \
+        for (int k_ = 0; k_ < 24; ++k_) tg_prof_l[k_] = 0ull;                   \
+    unsigned long long tg_t0 = clock64();
 #define TG_PROF(k)                                                              \
     {                                                                           \
         const unsigned long long t1 = clock64();                               \
-        if (threadIdx.x == 0) atomicAdd(&tg_prof_acc[k], t1 - tg_t0);           \
+        if (threadIdx.x == 0) tg_prof_l[k] += t1 - tg_t0;                       \
         tg_t0 = t1;                                                             \
     }
+#define TG_PROF_FLUSH                                                           \
+    if (threadIdx.x == 0)                                                       \
+        for (int k_ = 0; k_ < 24; ++k_) atomicAdd(&tg_prof_acc[k_], tg_prof_l[k_]);
 #elif defined(TG_STOP_AT)
 // developer build only: the kernel ends at the first stamp TG_STOP_AT (every
 // wave at the same point), so PMC counters of successive stop points
 // attribute LDS bank conflicts to sections (scripts/dev/lds_attrib.sh)
 #define TG_PROF_INIT
+#define TG_PROF_FLUSH
 #define TG_PROF(k)                                                              \
     {                                                                           \
         if ((k) == TG_STOP_AT) return;                                          \
     }
 #else
 #define TG_PROF_INIT
+#define TG_PROF_FLUSH
 #define TG_PROF(k)
 #endif
 
@@ -1613,7 +1626,11 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
             }
         }
 #endif
+#ifdef TG_PROF_SPLIT0   // developer: pass 1a of the first substep into its own slot (20)
+        TG_PROF(sub_i == 0 ? 20 : 16)
+#else
         TG_PROF(16)
+#endif
 #pragma unroll
         for (int r = 0; r < NRX; ++r) {
             const int g = sub + r * LPE;
@@ -3175,6 +3192,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
         }
     }
     TG_PROF(9)
+    TG_PROF_FLUSH
 }
 
 #undef TG_SYNC
