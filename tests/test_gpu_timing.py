@@ -50,3 +50,29 @@ def test_gpu_windowed_kernel_timing():
     env.sim.set_kernel_timing(0)
     _, n_d = env.sim.read_kernel_timing()
     assert n_d == 8, n_d                   # the first window was dropped, the second kept
+
+
+def test_gpu_bench_gpus_two_launches_two_ranks_on_one_gpu():
+    """`python bench.py --gpus 2` on the one-GPU box: the
+    parent touches no GPU and starts two torch.distributed.run ranks, which
+    share cuda:0 over gloo (TG_BENCH_SHARE_GPU: RCCL refuses two ranks on one
+    device -- a rehearsal of the launch path, not a scaling number); rank 0
+    prints one line with n_gpus 2 and the process group's size 2."""
+    _cuda()
+    import json
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(TG_BENCH_DIST_BACKEND="gloo", TG_BENCH_SHARE_GPU="1")
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "20", "--warmup", "5",
+                        "--num-envs", "1024", "--no-cpu-baseline"], env=env, cwd=repo, capture_output=True, text=True,
+                       timeout=300)
+    lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = lines[0]
+    print({k: d[k] for k in ("value", "n_gpus", "ms_per_step")}, d["dist"])
+    assert d["n_gpus"] == 2 and d["dist"]["world_size"] == 2
+    assert d["value"] > 0 and d["config"]["parallelism"] == "env-dp2"
