@@ -677,6 +677,16 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
     // then the top-down pass.  Models whose columns do not fit keep the
     // bottom-up pass.
     constexpr int SW = M::MAXD + 6;
+    // column j's superposition scratch (its up-walk impulses, then its root
+    // response), element x: one dead I^A slot per column when every column
+    // has its own group slot -- the address is then affine in x, one base
+    // register plus an immediate per element (round 6: the packed form's
+    // (jSW+x)/21 per element made the apply loop hoist a register per row,
+    // the whole-body model's spills); else packed across the slots.  Humanoid
+    // trees only: A/B (profiles/r6/sw_slot_ab.txt) walk 49.25 -> 48.4 us, AGPRs
+    // 59 -> 39; Gogoro 43.1 -> 43.8 us, so the scooters keep the packed form
+    constexpr bool SW_SLOT = K <= M::NG && SW <= 21 && M::NG >= 16;
+    auto swa = [](int j, int x) { return SW_SLOT ? j * GF + F_IA + x : scr(j * SW + x); };
 #ifdef TG_NO_SUPER
     constexpr bool SUPER = false;
 #else
@@ -2459,10 +2469,10 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                 if constexpr (SUPER) {
 #pragma unroll
                     for (int i = 0; i < M::MAXD; ++i)
-                        if (i < lk) s(scr(j * SW + i)) = du[i];
+                        if (i < lk) s(swa(j, i)) = du[i];
                     const float av[6] = {aj.w.x, aj.w.y, aj.w.z, aj.v.x, aj.v.y, aj.v.z};
 #pragma unroll
-                    for (int k = 0; k < 6; ++k) s(scr(j * SW + M::MAXD + k)) = av[k];
+                    for (int k = 0; k < 6; ++k) s(swa(j, M::MAXD + k)) = av[k];
                 }
                 if constexpr (M::NG <= 8) {
                     // small trees: the ABA's x from the walk about the root
@@ -2903,7 +2913,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
 #pragma unroll
                         for (int j = 0; j < K; ++j)
                             if (M::shape_cg[row_shape<M>(j)] == c) {
-                                const float du = s(scr(j * SW + i));
+                                const float du = s(swa(j, i));
                                 acc += s(LP + j) * du;
                                 accv += s(PL::LAM + j) * du;
                             }
@@ -2923,7 +2933,7 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
                         const float l = s(LP + j), lv = s(PL::LAM + j);
 #pragma unroll
                         for (int k = 0; k < 6; ++k) {
-                            const float aj = s(scr(j * SW + M::MAXD + k));
+                            const float aj = s(swa(j, M::MAXD + k));
                             d6[k] += l * aj;
                             v6[k] += lv * aj;
                         }
