@@ -219,7 +219,14 @@ template <class M> struct ParLayout {
     static constexpr int WB_A = WB_R + WCM * 6;             // [WCM][NCG][6]
     static constexpr int WB_J = WB_A + WCM * 6 * M::NCG;    // [WCM][K]
     static constexpr int WB_M = WB_J + WCM * (K > 0 ? K : 1);   // [WCM][WCM]
-    static constexpr int TOTAL = WOOD ? WB_M + WCM * WCM : TOTAL0;
+    static constexpr int TOTAL1 = WOOD ? WB_M + WCM * WCM : TOTAL0;
+    // superposition scratch past the group slots (humanoid trees with more
+    // Delassus columns than groups, the whole-body model): columns NG .. K-1,
+    // 21 floats each, when the LDS has room (step_par_kernel swa)
+    static constexpr int SWX = (TOTAL1 + 3) & ~3;
+    static constexpr bool SWXON = SUPER && K > M::NG && M::NG >= 16 && M::MAXD + 6 <= 21 &&
+                                  ((size_t)M::EPB * (SWX + 21 * (K - M::NG) + 4) + T_TOTAL) * 4 <= 160 * 1024;
+    static constexpr int TOTAL = SWXON ? SWX + 21 * (K - M::NG) : TOTAL1;
     // env stride.  Large trees (Thormang): 2 mod 4 floats, so the two envs
     // of a 32-lane b32/b64 bank group fall on disjoint bank classes (bank
     // conflicts 27 % -> 17 % of LDS cycles, kernel -0.25 %; the env base is
@@ -685,8 +692,10 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
     // the whole-body model's spills); else packed across the slots.  Humanoid
     // trees only: A/B (profiles/r6/sw_slot_ab.txt) walk 49.25 -> 48.4 us, AGPRs
     // 59 -> 39; Gogoro 43.1 -> 43.8 us, so the scooters keep the packed form
-    constexpr bool SW_SLOT = K <= M::NG && SW <= 21 && M::NG >= 16;
-    auto swa = [](int j, int x) { return SW_SLOT ? j * GF + F_IA + x : scr(j * SW + x); };
+    constexpr bool SW_SLOT = (K <= M::NG || PL::SWXON) && SW <= 21 && M::NG >= 16;
+    auto swa = [](int j, int x) {
+        return SW_SLOT ? (j < M::NG ? j * GF + F_IA + x : PL::SWX + 21 * (j - M::NG) + x) : scr(j * SW + x);
+    };
 #ifdef TG_NO_SUPER
     constexpr bool SUPER = false;
 #else
