@@ -47,7 +47,7 @@ HBM_PEAK_GBS = 8000.0
 TIMING_PERIOD = 16
 TIMING_WINDOW = 16
 MIN_KERNEL_SAMPLES = 32
-ONE_LAUNCH_TASKS = ("ThormangWalk", "ThormangWalkDR", "Gogoro")
+ONE_LAUNCH_TASKS = ("ThormangWalk", "ThormangWalkDR", "Gogoro", "GogoroPaper")
 
 
 def algorithmic_bytes_per_env_step(task_name: str, env) -> tuple[int, dict]:

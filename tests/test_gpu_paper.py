@@ -197,35 +197,100 @@ def test_gpu_paper_2048_envs_run():
     assert float(env.head_perturbation.abs().max()) > 0.0   # pushes happened
 
 
-def test_gpu_paper_fused_step_equals_separate_calls(monkeypatch):
-    """tg_paper_step (the pre-physics inside the step kernel, which also forms
-    reward term 7's per-env partials, and a post launch that sums the batch
-    itself) against the three separate calls (TG_PAPER_UNFUSED=1: post kernel
-    partials, finish launch): the same operations in the same order, so every
-    buffer agrees bit for bit -- including the head pushes, which tg_paper_step
-    reduces inside its post launch, after a root write between two steps
-    (the pre-reduced wrenches then give way to the next simulate's reduction)."""
-    _cuda()
+def _paper_trace(monkeypatch, env_vars, n=256, steps=150, timing_window=0):
+    """Step a GogoroPaper env under the given library switches (read when the
+    sim is created) with seeded random actions and a root write after step 60
+    (the pushes of the next simulate see the new pose); returns its buffers
+    and, with timing_window > 0, the step-kernel launches windowed timing saw
+    over the last 48 steps (a window any other launch falls into is dropped)."""
     import thormang_isaacgym_amd as tia
-    out = []
-    for unfused in ("0", "1"):
-        monkeypatch.setenv("TG_PAPER_UNFUSED", unfused)
-        env = tia.make(seed=11, task="GogoroPaper", num_envs=256, sim_device="cuda:0", rl_device="cuda:0")
-        g = torch.Generator(device="cuda:0").manual_seed(9)
-        ids = torch.arange(0, 256, 3, device="cuda:0", dtype=torch.int32)
-        for i in range(150):
-            obs, rew, reset, extras = env.step(torch.rand(256, 1, device="cuda:0", generator=g) * 2 - 1)
-            if i == 60:   # a root write after the step: the pushes of the next simulate see the new pose
-                r = env.root_tensor.clone()
-                r[:, 3:7] = torch.tensor([0.0, 0.0, 0.2955202, 0.9553365], device="cuda:0")
-                env.sim.set_actor_root_state_indexed(r, ids)
-        torch.cuda.synchronize()
-        out.append([t.detach().cpu().clone() for t in (obs["obs"], rew, reset, extras["time_outs"], env.root_tensor,
-                                                        env.sim.dof_pos_target, env.sim.dof_vel_target,
-                                                        env.progress_buf)])
-        assert int(out[-1][2].sum()) >= 0
-    for a, b in zip(*out):
-        assert torch.equal(a, b)
+    for k in ("TG_PAPER_UNFUSED", "TG_PAPER_TWO_LAUNCH"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env_vars.items():
+        monkeypatch.setenv(k, v)
+    env = tia.make(seed=11, task="GogoroPaper", num_envs=n, sim_device="cuda:0", rl_device="cuda:0")
+    g = torch.Generator(device="cuda:0").manual_seed(9)
+    ids = torch.arange(0, n, 3, device="cuda:0", dtype=torch.int32)
+    launches = None
+    for i in range(steps):
+        if timing_window and i == steps - 48:
+            env.sim.read_kernel_timing()
+            env.sim.set_kernel_timing(-timing_window)
+        obs, rew, reset, extras = env.step(torch.rand(n, 1, device="cuda:0", generator=g) * 2 - 1)
+        if i == 60:
+            r = env.root_tensor.clone()
+            r[:, 3:7] = torch.tensor([0.0, 0.0, 0.2955202, 0.9553365], device="cuda:0")
+            env.sim.set_actor_root_state_indexed(r, ids)
+    torch.cuda.synchronize()
+    if timing_window:
+        env.sim.set_kernel_timing(0)
+        launches = env.sim.read_kernel_timing()[1]
+    env.sim.sync()   # (raises if a one-launch batch sum had timed out)
+    out = [t.detach().cpu().clone() for t in (obs["obs"], rew, reset, extras["time_outs"], env.root_tensor,
+                                              env.sim.dof_pos_target, env.sim.dof_vel_target, env.progress_buf,
+                                              env.head_perturbation, env.sim.dof_state)]
+    return out, launches
+
+
+PAPER_FIELDS = ("obs", "rew", "reset", "time_outs", "root", "pos_target", "vel_target", "progress", "pushes", "dof")
+
+
+def test_gpu_paper_two_launch_step_equals_separate_calls(monkeypatch):
+    """tg_paper_step as two launches (TG_PAPER_TWO_LAUNCH=1: the pre-physics
+    inside the step kernel, which also forms reward term 7's per-env
+    partials, and a post launch that sums the batch itself) against the three
+    separate calls (TG_PAPER_UNFUSED=1: post kernel partials, finish launch):
+    the same operations in the same order, so every buffer agrees bit for bit
+    -- including the head pushes, which tg_paper_step reduces inside its post
+    launch, after a root write between two steps (the pre-reduced wrenches
+    then give way to the next simulate's reduction)."""
+    _cuda()
+    a, _ = _paper_trace(monkeypatch, {"TG_PAPER_TWO_LAUNCH": "1"})
+    b, _ = _paper_trace(monkeypatch, {"TG_PAPER_UNFUSED": "1"})
+    assert int(a[2].sum()) >= 0
+    for x, y, what in zip(a, b, PAPER_FIELDS):
+        assert torch.equal(x, y), what
+
+
+def test_gpu_paper_one_launch_step_matches_two_launch(monkeypatch):
+    """tg_paper_step in ONE launch (the default when the batch fits one
+    workgroup per CU: the post-physics as the step kernel's PaperPost
+    epilogue, reward term 7's batch sum exchanged inside the launch, the
+    pushes reduced to the next simulate's wrenches by the env's 16 lanes)
+    against the two-launch form.  Resets, time-outs, progress and the pushes'
+    timing are identical; the rest agrees to fp32 rounding (the epilogue's
+    unit is the fast-math physics unit: its libm and the link kinematics of
+    the push reduction round differently), far inside north_star's 1e-3.  The
+    windowed kernel timing sees only step kernels in the one-launch run (any
+    other launch drops its window) and none in the two-launch run."""
+    _cuda()
+    one, n_one = _paper_trace(monkeypatch, {}, timing_window=4)
+    two, n_two = _paper_trace(monkeypatch, {"TG_PAPER_TWO_LAUNCH": "1"}, timing_window=4)
+    assert n_one >= 40 and n_two == 0, (n_one, n_two)
+    diffs = {}
+    for x, y, what in zip(one, two, PAPER_FIELDS):
+        if what in ("reset", "time_outs", "progress"):
+            assert torch.equal(x, y), what
+        else:
+            diffs[what] = float((x.float() - y.float()).abs().max())
+    print(diffs)
+    assert all(d <= 1e-4 for d in diffs.values()), diffs
+    assert float(one[8].abs().max()) > 0.0   # pushes happened
+
+
+def test_gpu_paper_one_launch_4096_envs_reward_term7_exact(monkeypatch):
+    """The bench batch (4096 envs: 256 workgroups, one per CU, every one
+    waiting on every other's term-7 block sum) takes the one-launch path and
+    agrees with the two-launch step as above over 60 steps."""
+    _cuda()
+    one, n_one = _paper_trace(monkeypatch, {}, n=4096, steps=60, timing_window=4)
+    two, _ = _paper_trace(monkeypatch, {"TG_PAPER_TWO_LAUNCH": "1"}, n=4096, steps=60)
+    assert n_one >= 40
+    for x, y, what in zip(one, two, PAPER_FIELDS):
+        if what in ("reset", "time_outs", "progress"):
+            assert torch.equal(x, y), what
+        else:
+            assert float((x.float() - y.float()).abs().max()) <= 1e-4, what
 
 
 def test_gpu_paper_inplace_seat_composites_equal_a_full_compose():

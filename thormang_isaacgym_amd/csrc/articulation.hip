@@ -53,6 +53,14 @@ int launch_step_walk(uint64_t hash, const StepArgs &a, const WalkPostArgs &pa, h
     return jit_has(hash) ? 1 : TG_ERR_MODEL;
 }
 
+int launch_step_paper(uint64_t hash, const StepArgs &a, const PaperPostArgs &pa, hipStream_t stream,
+                      hipEvent_t ev_begin, hipEvent_t ev_end) {
+    int rc = unit_launch_step_paper(hash, a, pa, stream, ev_begin, ev_end);
+    if (rc == TG_OTHER_UNIT) rc = tree_launch_step_paper(hash, a, pa, stream, ev_begin, ev_end);
+    if (rc != TG_OTHER_UNIT) return rc;
+    return jit_has(hash) ? 1 : TG_ERR_MODEL;
+}
+
 #ifdef TG_DUMP_ENV
 // developer build only: select the env whose contact solve the step kernels
 // dump (first-substep or the given substep), in BOTH units -- the scooters and
@@ -141,6 +149,11 @@ int launch_compose_only(uint64_t hash, const StepArgs &a, hipStream_t stream) {
 #define TG_FUSED(MODEL) if (hash == MODEL::hash) return MODEL::FUSED;
 int model_fused(uint64_t hash) {
     TG_FOR_EACH_MODEL(TG_FUSED)
+    return 0;
+}
+#define TG_EPB(MODEL) if (hash == MODEL::hash) return MODEL::EPB;
+int model_epb(uint64_t hash) {
+    TG_FOR_EACH_MODEL(TG_EPB)
     return 0;
 }
 #define TG_TL(MODEL) if (hash == MODEL::hash) return MODEL::NTL;

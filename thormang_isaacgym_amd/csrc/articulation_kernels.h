@@ -220,15 +220,26 @@ __device__ __forceinline__ float paper_t7_partial(const PaperPre &pp, int e, flo
     }
     return rs ? 0.0f : v[0];
 }
-// the block's sum of the partials (TG_PAPER_T7_BLK of them, env order, double)
-__device__ __forceinline__ void paper_t7_block(const PaperPre &pp, const float *part, int blk) {
+// the block's sum of the partials (TG_PAPER_T7_BLK of them, env order, double);
+// PUB (the one-launch step, PaperPost): stored with agent scope, the store
+// waited for, then the block's arrival added to *cnt (paper_t7_wait_sum)
+template <bool PUB = false>
+__device__ __forceinline__ void paper_t7_block(const PaperPre &pp, const float *part, int blk,
+                                               unsigned *cnt = nullptr) {
     double s = 0.0;
     {
 #pragma clang fp reassociate(off) contract(off)
 #pragma unroll
         for (int i = 0; i < TG_PAPER_T7_BLK; ++i) s = s + (double)part[i];
     }
-    pp.t7[blk] = s;
+    if constexpr (PUB) {
+        __hip_atomic_store(reinterpret_cast<unsigned long long *>(pp.t7 + blk),
+                           (unsigned long long)__double_as_longlong(s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        pp.t7[blk] = s;
+    }
 }
 
 template <class M>
@@ -1162,6 +1173,7 @@ namespace tg {
 // translation unit's (fast-math) ones.
 struct WalkPost {
     static constexpr bool on = true;
+    static constexpr bool T7_SYNC = false;
     static constexpr int NPRE = 0;
     static constexpr bool PM_OUT = true;   // stores the pre-physics' actions / targets (pm_in_step) below
     static constexpr bool TOUCH = true;
@@ -1493,6 +1505,7 @@ template <class M> __device__ __forceinline__ void tl_update(float *c, const flo
 // and fp32 operations (gogoro_math.h) as post_kernel.
 struct GogoroPost {
     static constexpr bool on = true;
+    static constexpr bool T7_SYNC = false;
     static constexpr bool PM_OUT = false;
     static constexpr bool TOUCH = false;
     using Args = GogoroPostArgs;
@@ -1731,6 +1744,464 @@ struct GogoroPost {
         if (prog == p.speed_freq_update) b.curent_speed[e] = u_aff(p.speed_range[0], p.speed_range[1], su);
         b.yaw_command[e] = yc;
         b.timeout_buf[e] = (prog >= p.max_episode_length - 1) && (reset != 0);
+    }
+};
+
+}  // namespace tg
+
+#include "paper_math.h"
+
+namespace tg {
+
+// ---------------------------------------------------------------- fused paper post-physics
+// Reward term 7 inside the step launch (PaperPost): every workgroup published
+// its block sum in the prologue (paper_t7_block<true>: an agent-scope store,
+// its completion waited for, then one agent-scope add to the arrival
+// counter).  Each wavefront polls the counter from one lane until every block
+// of this launch has arrived -- bounded: a timeout raises bit 2 of the sticky
+// error word (tg_sync reports it) and the sum goes on with what is there, so
+// no wave can spin forever -- then reads the block sums with agent-scope loads
+// (MI355X_MICROARCH.md's hand-off form: scope-1 stores, a waited store before
+// the counter add, scope-1 loads after the matched poll) and adds them in
+// t7_batch_sum's canonical order: virtual thread t < TG_PAPER_T7_THREADS adds
+// blocks t, t + TG_PAPER_T7_THREADS, ...; an xor butterfly per virtual
+// wavefront; the wavefront sums in order (the post launch's total bit for bit).
+// (A/B, profiles/r6/paper_one_launch_ab.txt: reading the count a substep
+// ahead measured no gain)
+__device__ __forceinline__ double paper_t7_wait_sum(const double *t7, unsigned *cnt, unsigned target, int nblk,
+                                                    int *err) {
+    const int lane = threadIdx.x & 63;
+    if (lane == 0) {
+        unsigned it = 0, c = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while ((int)(c - target) < 0) {
+            if (++it > (1u << 20)) {   // ~1 s: a workgroup never became resident
+                if (err) atomicOr(err, 2);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+            c = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    constexpr int VW = TG_PAPER_T7_THREADS / 64;
+    const unsigned long long *src = reinterpret_cast<const unsigned long long *>(t7);
+    double v[VW];
+#pragma unroll
+    for (int w = 0; w < VW; ++w) {
+        const int c = lane + 64 * w;
+        v[w] = c < nblk ? __longlong_as_double((long long)__hip_atomic_load(src + c, __ATOMIC_RELAXED,
+                                                                            __HIP_MEMORY_SCOPE_AGENT))
+                        : 0.0;
+    }
+    double tot = 0.0;
+    {
+#pragma clang fp contract(off) reassociate(off)
+#pragma unroll
+        for (int w = 0; w < VW; ++w) {
+            double x = 0.0;
+            x += v[w];   // (a virtual thread's one block: nblk <= TG_PAPER_T7_THREADS, checked by the host)
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
+            tot += x;
+        }
+    }
+    return tot;
+}
+
+// b.rb_forces [N*L,3] (world forces at the link coms) reduced to env e's
+// group wrenches [G,6] by the env's LN lanes -- rb_force_env's composite-cache
+// path (link = lane mod LN, group = lane), the same operations per link and
+// the same link order per group sum.  load(): the inputs no epilogue store
+// changes (the lane's link forces and coms, its group's joint placement, the
+// lock extension); finish(): the state the epilogue's stores change -- root
+// orientation, joint angles, lock windows -- and the one force row the
+// epilogue itself rewrote (the head push, plink: its link, -1 none), all read
+// after the stores (fence before); T: 9 x NG, F: 6 x NL floats of the env's
+// LDS.
+template <class M, int LN> struct RbLanes {
+    static_assert(M::LCOM && M::NG <= LN, "one group per lane");
+    static constexpr int NLL = (M::NL + LN - 1) / LN;
+    static constexpr int NT = M::NTL > 0 ? M::NTL : 1;
+    using CL = CompLayout<M>;
+    V3 f[NLL], lc[NLL], gc[NLL];
+    M3 Rpc;
+    float xk0[NT];
+    V3 xka[NT];
+    __device__ __forceinline__ void load(const float *comp, int e, const float *forces, int sub) {
+        const float *c = comp + (size_t)e * M::KC;
+#pragma unroll
+        for (int k = 0; k < NLL; ++k) {
+            const int l = sub + LN * k;
+            f[k] = lc[k] = gc[k] = v3(0, 0, 0);
+            if (l < M::NL) {
+                const int gl = M::link_group[l];
+                const size_t i = (size_t)e * M::NL + l;
+                f[k] = v3(forces[3 * i], forces[3 * i + 1], forces[3 * i + 2]);
+                lc[k] = v3(c[CL::lcom(l)], c[CL::lcom(l) + 1], c[CL::lcom(l) + 2]);
+                gc[k] = v3(c[CL::inertia(gl) + 1], c[CL::inertia(gl) + 2], c[CL::inertia(gl) + 3]);
+            }
+        }
+        const bool hg = sub > 0 && sub < M::NG;
+        const int g = hg ? sub : 1 % M::NG;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) Rpc.a[k] = hg ? c[CL::xtree(g) + k] : 0.f;
+        if constexpr (M::NTL > 0) {
+#pragma unroll
+            for (int k = 0; k < M::NTL; ++k) {
+                const float *xk = c + CL::xk(k);
+                xk0[k] = xk[0];
+                xka[k] = v3(xk[5], xk[6], xk[7]);
+            }
+        }
+    }
+    __device__ __forceinline__ void finish(const float *root, const float *dof, const float *forces, int plink,
+                                           int e, float *out, int sub, float *T, float *F, const float *props, int N,
+                                           bool store) {
+#pragma clang fp contract(off) reassociate(off)
+        auto wsync = [] {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        };
+        const float *r = root + 13 * (size_t)e;
+        const float *q = dof + 2 * (size_t)e * M::ND;
+        const bool hg = sub > 0 && sub < M::NG;
+        const int g = hg ? sub : 1 % M::NG;
+        float qj = 0.f;
+        if (hg && M::jtype[g] == TG_JOINT_REVOLUTE) qj = q[2 * M::gdof[g]];
+        const float qx = r[3], qy = r[4], qz = r[5], qw = r[6];
+        if (plink >= 0) {   // the row this epilogue rewrote, re-read by the lane that holds it
+            const size_t i = (size_t)e * M::NL + (plink < M::NL ? plink : 0);
+            const bool mine = plink % LN == sub;
+            const V3 fp = mine ? v3(forces[3 * i], forces[3 * i + 1], forces[3 * i + 2]) : v3(0, 0, 0);
+#pragma unroll
+            for (int k = 0; k < NLL; ++k) {   // (selects: a per-k branch folds to a dynamically indexed store)
+                const bool hit = mine && sub + LN * k == plink;
+                f[k].x = hit ? fp.x : f[k].x;
+                f[k].y = hit ? fp.y : f[k].y;
+                f[k].z = hit ? fp.z : f[k].z;
+            }
+        }
+        V3 ush[NT];
+        if constexpr (M::NTL > 0) {
+            const size_t ND = (size_t)N * M::ND;
+#pragma unroll
+            for (int k = 0; k < M::NTL; ++k) {
+                const size_t id = (size_t)e * M::ND + M::tl_dof[k];
+                const float qc = 0.5f * (props[TG_PROP_LOWER * ND + id] + props[TG_PROP_UPPER * ND + id]);
+                ush[k] = (qc - xk0[k]) * xka[k];
+            }
+        }
+        bool act = false;
+#pragma unroll
+        for (int k = 0; k < NLL; ++k)
+            act = act || f[k].x != 0.f || f[k].y != 0.f || f[k].z != 0.f;
+        // the env's lanes: any force at all (else zero wrenches, no kinematics)
+        const unsigned long long envm = ((LN == 64) ? ~0ull : ((1ull << LN) - 1)) << ((threadIdx.x & 63) / LN * LN);
+        if ((__ballot(act) & envm) == 0) {
+            if (store)
+                for (int k = sub; k < 6 * M::NG; k += LN) out[(size_t)e * 6 * M::NG + k] = 0.f;
+            return;
+        }
+        M3 R = Rpc;
+        if (hg && M::jtype[g] == TG_JOINT_REVOLUTE) {   // Rpc Rz(q), as step pass 1a
+            float sq, cq;
+            tg_sincos(qj, &sq, &cq);
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr) {
+                const float c0 = R.a[3 * rr], c1 = R.a[3 * rr + 1];
+                R.a[3 * rr] = c0 * cq + c1 * sq;
+                R.a[3 * rr + 1] = c1 * cq - c0 * sq;
+            }
+        }
+        constexpr int GD = max_group_depth<M>();
+        for (int lev = 0; lev <= GD; ++lev) {
+            if (lev == 0 && sub == 0) {
+                const float in = rsqrtf(qx * qx + qy * qy + qz * qz + qw * qw);
+                const M3 W = mul(quat_to_m3(qx * in, qy * in, qz * in, qw * in),
+                                 M3{{M::gq[0][0], M::gq[0][1], M::gq[0][2], M::gq[0][3], M::gq[0][4], M::gq[0][5],
+                                     M::gq[0][6], M::gq[0][7], M::gq[0][8]}});
+#pragma unroll
+                for (int k = 0; k < 9; ++k) T[k] = W.a[k];
+            } else if (lev > 0 && hg && group_depth<M>(g) == lev) {
+                M3 Wp;
+#pragma unroll
+                for (int k = 0; k < 9; ++k) Wp.a[k] = T[9 * M::parent[g] + k];
+                const M3 W = mul(Wp, R);
+#pragma unroll
+                for (int k = 0; k < 9; ++k) T[9 * g + k] = W.a[k];
+            }
+            wsync();
+        }
+#pragma unroll
+        for (int k = 0; k < NLL; ++k) {
+            const int l = sub + LN * k;
+            if (l < M::NL) {
+                const int gl = M::link_group[l];
+                M3 W;
+#pragma unroll
+                for (int j = 0; j < 9; ++j) W.a[j] = T[9 * gl + j];
+                V3 lck = lc[k];
+                if constexpr (M::NTL > 0) {
+                    if (gl == M::tl_group && M::link_tl[l]) {
+                        V3 sh = v3(0, 0, 0);
+#pragma unroll
+                        for (int j = 0; j < M::NTL; ++j)
+                            if ((M::link_tl[l] >> j) & 1) sh = sh + ush[j];
+                        const float *qg = M::gq[gl];
+                        lck = lck + mulT(M3{{qg[0], qg[1], qg[2], qg[3], qg[4], qg[5], qg[6], qg[7], qg[8]}}, sh);
+                    }
+                }
+                const V3 tq = v3(0, 0, 0) + cross(mul(W, lck - gc[k]), f[k]);
+                F[6 * l + 0] = f[k].x; F[6 * l + 1] = f[k].y; F[6 * l + 2] = f[k].z;
+                F[6 * l + 3] = tq.x; F[6 * l + 4] = tq.y; F[6 * l + 5] = tq.z;
+            }
+        }
+        wsync();
+        for (int j = sub; j < 6 * M::NG; j += LN) {
+            float acc = 0.f;
+            const int gsel = j / 6, cmp = j % 6;
+            rbf_for_groups<0, M::NG>([&](auto G) {
+                constexpr int gg = decltype(G)::value;
+                if (gsel == gg) {
+#pragma unroll
+                    for (int k = 0; k < M::group_nlinks[gg]; ++k) acc += F[6 * M::group_links[gg][k] + cmp];
+                }
+            });
+            if (store) out[(size_t)e * 6 * M::NG + j] = acc;
+        }
+    }
+};
+
+// tg_paper_step's simulate when the whole launch is resident at once: the
+// GogoroPaper post-physics (gogoro_paper_task.hip paper_post_kernel: masked
+// reset_idx, the 20-step clean / noisy histories, rewards with reward term 7's
+// batch mean, command changes, head pushes, the push tensor reduced to the
+// next simulate's group wrenches) as the step kernel's epilogue, LPE lanes per
+// env (lane = history entry / dof / link mod LPE) on the final state the
+// kernel holds: the whole GogoroPaper step in one launch.
+// The same helpers (paper_math.h), Philox blocks and sum order as the post
+// kernel; this unit's transcendentals and the physics' fp contraction in the
+// link kinematics are the differences (tests/test_gpu_paper.py).
+struct PaperPost {
+    static constexpr bool on = true;
+    static constexpr bool PM_OUT = false;
+    static constexpr bool TOUCH = false;
+    static constexpr bool T7_SYNC = true;
+    using Args = PaperPostArgs;
+    // the translating-lock extension of an env the previous step flagged for
+    // reset (its reset happens in this epilogue), as GogoroPost
+    static constexpr int NPRE = 5, NXP = 5;
+    template <class M, int LPE>
+    static __device__ __forceinline__ void prefetch(const Args &pa, const StepArgs &a, int e, int sub, float *x) {
+#pragma unroll
+        for (int k = 0; k < NPRE; ++k) x[k] = 0.f;
+        if constexpr (M::NTL > 0) {
+            static_assert(M::KX <= NXP * LPE, "extension prefetch: KX <= NXP x LPE");
+            if (pa.b.reset_buf[e] != 0) {
+                const float *xs = a.comp + (size_t)e * M::KC + CompLayout<M>::ext();
+#pragma unroll
+                for (int k = 0; k < NXP; ++k) {
+                    const int i = sub * NXP + k;
+                    if (i < M::KX) x[k] = xs[i];
+                }
+            }
+        }
+    }
+    template <class M, int LPE>
+    static __device__ __forceinline__ void epilogue(const Args &pa, const StepArgs &a, const LE &s, int e, bool owner,
+                                                    int sub, const float *rt0, float *root, float *dofs,
+                                                    const float *xpre) {
+        using namespace paper;
+        constexpr int D = M::ND;
+        constexpr int NR = (D + LPE - 1) / LPE;     // dof rows per lane
+        constexpr int NH = (PHO + LPE - 1) / LPE;   // history entries per lane
+        static_assert(LPE >= 8, "the 8 Philox blocks need 8 lanes per env");
+        static_assert(M::NTL > 0 && (M::FUSED & 4), "in-place seat composites (the paper model)");
+        using PL = ParLayout<M>;
+        // the env's LDS after the state stores: the extension at W (reset
+        // envs), the draws / newest entries after it; the force reduction's
+        // T / F from 0 once those are consumed
+        constexpr int XO = PL::W, SX = PL::W + ((M::KX + 3) & ~3);
+        constexpr int DR = SX, OB = SX + 32, NZ = SX + 40;
+        static_assert(NZ + PO <= PL::ES && 9 * M::NG + 6 * M::NL <= PL::ES, "epilogue scratch in the env's LDS");
+        const tg_paper_params &p = pa.p;
+        const tg_paper_buffers &b = pa.b;
+        const bool lead = sub == 0;
+        auto wsync = [] {   // the env's lanes share a wavefront
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        };
+        // ---- inputs, one batch
+        const bool rflag = b.reset_buf[e] != 0;
+        const int64_t prog0 = b.progress_buf[e] + 1;
+        float *bo = b.buffer_obs + (size_t)PHO * e, *bn = b.buffer_obs_noisy + (size_t)PHO * e;
+        float vc[NH], vn[NH];
+#pragma unroll
+        for (int j = 0; j < NH; ++j) {
+            const int i = sub + LPE * j;
+            vc[j] = vn[j] = 0.0f;
+            if (i < PHO - PO) {
+                vc[j] = bo[i + PO];
+                vn[j] = bn[i + PO];
+            }
+        }
+        float pose[NR];
+#pragma unroll
+        for (int rr = 0; rr < NR; ++rr) {
+            const int d = sub + LPE * rr;
+            pose[rr] = d < D ? b.thormang_pose[(size_t)e * D + d] : 0.f;
+        }
+        PaperLead L;
+        float tpl[13], old6 = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 13; ++k) L.root[k] = rt0[k];
+        L.speed = L.speed_off = L.imu_off = L.yaw_cmd = L.cmd = 0.f;
+        L.delay = 0;
+        if (lead) {
+            const float *tp = b.root_reset + 13 * (size_t)e;
+#pragma unroll
+            for (int k = 0; k < 13; ++k) tpl[k] = tp[k];
+            L.speed = b.curent_speed[e];
+            L.speed_off = b.curent_speed_offset[e];
+            L.imu_off = b.curent_imu_x_offset[e];
+            L.yaw_cmd = b.yaw_command[e];
+            L.cmd = b.curent_command[e];
+            L.delay = b.steer_delay[e];
+            old6 = bo[(PH - 1) * PO + 6];
+        }
+        // the step's 8 Philox blocks (reset 3, noise 2, speed, yaw, push), block l on lane l
+        float dv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (sub < 8) {
+            const U4 x = philox(U4{(uint32_t)e, pa.c_lo, pa.c_hi, post_block_tag(sub)}, (uint32_t)p.seed,
+                                (uint32_t)(p.seed >> 32));
+            dv[0] = u01(x.x);
+            dv[1] = u01(x.y);
+            dv[2] = u01(x.z);
+            dv[3] = u01(x.w);
+        }
+        // reward term 7's batch sum (every workgroup's prologue published its block)
+        const double tot = paper_t7_wait_sum(a.pp.t7, pa.t7_count, pa.t7_target, pa.nblk, a.err);
+        // ---- the extension and the draws to the env's LDS
+        if constexpr (M::NTL > 0) {
+#pragma unroll
+            for (int k = 0; k < NXP; ++k) {
+                const int i = sub * NXP + k;
+                if (i < M::KX) s(XO + i) = xpre[k];
+            }
+        }
+        if (sub < 8) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) s(DR + 4 * sub + k) = dv[k];
+        }
+        wsync();
+        auto draw = [&](int k, int blk) { return s(DR + 4 * (blk + (k >> 2)) + (k & 3)); };
+        const int64_t prog = rflag ? 0 : prog0;
+        // ---- the state: a reset env's reset values, else the simulated state
+        if (rflag) {
+            if (owner) {
+#pragma unroll
+                for (int rr = 0; rr < NR; ++rr) {
+                    const int d = sub + LPE * rr;
+                    if (d < D) {
+                        dofs[2 * d] = pose[rr];
+                        dofs[2 * d + 1] = 0.0f;
+                    }
+                }
+                for (int i = sub; i < PC; i += LPE) b.command_history[PC * (size_t)e + i] = 0.0f;
+            }
+#pragma unroll
+            for (int j = 0; j < NH; ++j) vc[j] = vn[j] = 0.0f;
+            if (lead) {
+                float r[9];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) r[k] = draw(k, 0);
+                if (owner) reset_lead<M>(p, b, e, r, tpl, L, a.comp, &s(XO));
+                old6 = 0.0f;
+            }
+        } else if (owner) {
+#pragma unroll
+            for (int rr = 0; rr < NR; ++rr) {
+                const int d = sub + LPE * rr;
+                if (d < D) {
+                    const int g = dof_group<M>(d);
+                    if (g > 0) {
+                        dofs[2 * d] = s(g * GF + F_Q);
+                        dofs[2 * d + 1] = s(g * GF + F_QD);
+                    } else {
+                        dofs[2 * d] = 0.5f * (prop(a, TG_PROP_LOWER, e, d) + prop(a, TG_PROP_UPPER, e, d));
+                        dofs[2 * d + 1] = 0.f;
+                    }
+                }
+            }
+            if (lead) {
+#pragma unroll
+                for (int k = 0; k < 13; ++k) root[k] = rt0[k];
+                b.progress_buf[e] = prog0;
+            }
+        }
+        // ---- the newest clean / noisy entries (lead lane) through LDS
+        if (lead) {
+            float u[6], o[PO], l[PO];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) u[k] = draw(k, 3);
+            entries(p, L, old6, u, o, l);
+#pragma unroll
+            for (int k = 0; k < PO; ++k) {
+                s(OB + k) = o[k];
+                s(NZ + k) = l[k];
+            }
+            if (owner) b.speed_no_noise[e] = o[4];
+        }
+        wsync();
+        // ---- both histories shifted by one entry, the new one appended
+#pragma unroll
+        for (int j = 0; j < NH; ++j) {
+            const int i = sub + LPE * j;
+            if (i < PHO) {
+                if (i >= PHO - PO) {
+                    vc[j] = s(OB + i - (PHO - PO));
+                    vn[j] = s(NZ + i - (PHO - PO));
+                }
+                if ((i % PO) == 1) vn[j] = 0.0f;   // noisy[:, :, 1] = 0
+                if (owner) {
+                    bo[i] = vc[j];
+                    bn[i] = vn[j];
+                    b.obs_buf[(size_t)PHO * e + i] = vn[j];
+                }
+            }
+        }
+        // ---- rewards, resets, time_outs, command changes, pushes (lead lane)
+        if (lead && owner) {
+            float last[PO];
+#pragma unroll
+            for (int k = 0; k < PO; ++k) last[k] = s(OB + k);
+            const float rew = reward15(p, last);
+            finish_env(p, b, e, tot, last[0], prog, rew);
+            commands(p, b, e, prog, L, last, draw(0, 5), draw(0, 6), draw(0, 7), draw(1, 7));
+        }
+        if (b.body_force && owner) {
+            float *wr = b.body_force + (size_t)6 * p.num_groups * e;
+            for (int i = 6 + sub; i < 6 * p.num_groups; i += LPE) wr[i] = 0.0f;
+        }
+        // ---- the push tensor reduced to the next simulate's group wrenches,
+        // on this epilogue's root / dofs / seat windows / pushes
+        if (pa.rb_out) {
+            // the head-push row, when the push tensor holds it (the task's
+            // [N, L, 3] tensor; perturbation = its head_p_link rows)
+            const long off = (long)(b.perturbation + (size_t)(p.perturbation_stride ? p.perturbation_stride : 3) * e -
+                                    (b.rb_forces + (size_t)3 * M::NL * e));
+            const int plink = (off >= 0 && off < 3 * M::NL && off % 3 == 0) ? (int)(off / 3) : -1;
+            wsync();   // (the LDS scratch above is consumed)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            // (every input after the stores: loading the static ones with the
+            // epilogue's first batch measured +0.45 us, paper_one_launch_ab.txt)
+            RbLanes<M, LPE> rb;
+            rb.load(a.comp, e, b.rb_forces, sub);
+            rb.finish(b.root, b.dof_state, b.rb_forces, plink, e, pa.rb_out, sub, s.b, s.b + 9 * M::NG, b.dof_props,
+                      p.num_envs, owner);
+        }
     }
 };
 

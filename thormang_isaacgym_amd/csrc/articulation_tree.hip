@@ -26,6 +26,10 @@ int tree_launch_step_walk(uint64_t hash, const StepArgs &a, const WalkPostArgs &
                           hipEvent_t ev_begin, hipEvent_t ev_end) {
     return unit_launch_step_walk(hash, a, pa, stream, ev_begin, ev_end);
 }
+int tree_launch_step_paper(uint64_t hash, const StepArgs &a, const PaperPostArgs &pa, hipStream_t stream,
+                           hipEvent_t ev_begin, hipEvent_t ev_end) {
+    return unit_launch_step_paper(hash, a, pa, stream, ev_begin, ev_end);
+}
 
 // developer builds: the section counters of this unit's step kernels
 // (articulation.hip's tg_prof_read / tg_cprof_read add them to its own)

@@ -62,7 +62,8 @@ std::mutex g_mu;
 std::map<uint64_t, JitCode> g_code;                            // by model hash
 std::map<std::pair<uint64_t, int>, JitLoaded> g_loaded;       // by (hash, device)
 
-const char *const HEADERS[] = {"articulation_kernels.h", "step_par.h", "tg_math.h", "gogoro_math.h", "tg_kernels.h",
+const char *const HEADERS[] = {"articulation_kernels.h", "step_par.h", "tg_math.h", "gogoro_math.h", "paper_math.h",
+                               "tg_kernels.h",
                                "../../include/tgsim.h", "../../include/tg_gogoro.h",
                                "../../include/tg_gogoro_paper.h", "../../include/tg_walk.h"};
 

@@ -123,6 +123,25 @@ int launch_model_gogoro(const StepArgs &a, const GogoroPostArgs &pa, hipStream_t
     }
 }
 
+// the fused GogoroPaper epilogue (one launch per step): the paper model with
+// in-place seat composites (codegen FUSED bit 4), flat ground
+template <class M>
+int launch_model_paper(const StepArgs &a, const PaperPostArgs &pa, hipStream_t stream, hipEvent_t ev_begin,
+                       hipEvent_t ev_end) {
+    if constexpr (!in_unit<M>()) {
+        return TG_OTHER_UNIT;
+    } else if constexpr ((M::FUSED & 4) == 0 || M::NTL == 0 || !M::LCOM || M::NG > M::LPE || M::LPE < 8) {
+        return 1;
+    } else {
+        if (a.hf || pa.p.num_dof != M::ND || a.N % M::EPB != 0) return 1;
+        launch_compose<M>(a, stream);
+        if (ev_begin && hipEventRecord(ev_begin, stream) != hipSuccess) return TG_ERR_HIP;
+        if (int rc = launch_par<M, false, PaperPost>(a, stream, pa)) return rc;
+        if (ev_end && hipEventRecord(ev_end, stream) != hipSuccess) return TG_ERR_HIP;
+        return hipGetLastError() == hipSuccess ? 0 : TG_ERR_HIP;
+    }
+}
+
 // this unit's dispatch (TG_OTHER_UNIT: a model this unit does not instantiate)
 #define TG_U_LAUNCH(MODEL) \
     if (in_unit<MODEL>() && hash == MODEL::hash) return launch_model<MODEL>(a, stream, ev_begin, ev_end);
@@ -140,6 +159,13 @@ static int unit_launch_step_gogoro(uint64_t hash, const StepArgs &a, const Gogor
     TG_FOR_EACH_MODEL(TG_U_LAUNCH_GOGORO)
     return TG_OTHER_UNIT;
 }
+#define TG_U_LAUNCH_PAPER(MODEL) \
+    if (in_unit<MODEL>() && hash == MODEL::hash) return launch_model_paper<MODEL>(a, pa, stream, ev_begin, ev_end);
+static int unit_launch_step_paper(uint64_t hash, const StepArgs &a, const PaperPostArgs &pa, hipStream_t stream,
+                                  hipEvent_t ev_begin, hipEvent_t ev_end) {
+    TG_FOR_EACH_MODEL(TG_U_LAUNCH_PAPER)
+    return TG_OTHER_UNIT;
+}
 static int unit_launch_step_walk(uint64_t hash, const StepArgs &a, const WalkPostArgs &pa, hipStream_t stream,
                                  hipEvent_t ev_begin, hipEvent_t ev_end) {
     TG_FOR_EACH_MODEL(TG_U_LAUNCH_WALK)
@@ -152,5 +178,7 @@ int tree_launch_step_gogoro(uint64_t hash, const StepArgs &a, const GogoroPostAr
                             hipEvent_t ev_begin, hipEvent_t ev_end);
 int tree_launch_step_walk(uint64_t hash, const StepArgs &a, const WalkPostArgs &pa, hipStream_t stream,
                           hipEvent_t ev_begin, hipEvent_t ev_end);
+int tree_launch_step_paper(uint64_t hash, const StepArgs &a, const PaperPostArgs &pa, hipStream_t stream,
+                           hipEvent_t ev_begin, hipEvent_t ev_end);
 
 }  // namespace tg

@@ -597,6 +597,7 @@ struct NoPost {
     static constexpr int NPRE = 0;   // floats per lane an epilogue prefetches at kernel start
     static constexpr bool PM_OUT = false;   // the epilogue stores the walk pre-physics outputs itself
     static constexpr bool TOUCH = false;    // touch_addr: a line of the epilogue's inputs per lane (below)
+    static constexpr bool T7_SYNC = false;  // publishes the term-7 block sum for an in-launch batch sum (PaperPost)
 };
 
 // inverse of the group -> dof map: group of dof d, -1 for a locked dof
@@ -961,7 +962,12 @@ __global__ TG_STEP_BOUNDS(M, EPB) void step_par_kernel(StepArgs a, typename P::A
     auto pdsc3 = [&](int t) { return pdsc_on(t, IntC<4>{}); };
     auto pdsc4 = [&](int t) { return pdsc_on(t, IntC<8>{}); };
     if constexpr ((M::FUSED & 4) != 0) {
-        if (a.pp_in_step && a.pp.t7 && tid == 0) paper_t7_block(a.pp, reinterpret_cast<const float *>(tab + PL::T_T7), chunk);
+        if (a.pp_in_step && a.pp.t7 && tid == 0) {
+            if constexpr (P::T7_SYNC)
+                paper_t7_block<true>(a.pp, reinterpret_cast<const float *>(tab + PL::T_T7), chunk, pa.t7_count);
+            else
+                paper_t7_block(a.pp, reinterpret_cast<const float *>(tab + PL::T_T7), chunk);
+        }
     }
     if constexpr (!EARLY && !OVL) {
 #pragma unroll

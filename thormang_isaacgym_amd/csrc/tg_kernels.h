@@ -135,7 +135,27 @@ struct GogoroPostArgs {
     // replayed draws (include/tg_gogoro.h layouts), each null for Philox
     const float *reset_draws, *obs_draws, *speed_draws, *yaw_draws;
 };
+// tg_paper_step's fused post-physics epilogue (articulation_kernels.h
+// PaperPost): the whole GogoroPaper step in one launch.  Reward term 7's
+// batch sum needs every workgroup's block sum: each workgroup publishes its
+// own in the prologue (PaperPre.t7) and adds one to *t7_count; the epilogue
+// waits until the count reaches t7_target (the host's running total, one
+// launch's worth of blocks more than before it), so every workgroup of the
+// launch must be resident at once (the host checks the grid against the CUs)
+struct PaperPostArgs {
+    tg_paper_params p;
+    tg_paper_buffers b;
+    uint32_t c_lo, c_hi;   // the post-physics call's Philox counter
+    float *rb_out;         // b.rb_forces reduced to the next simulate's group wrenches [N,G,6], or null
+    unsigned *t7_count;    // arrivals of the term-7 block sums (monotonic over launches)
+    unsigned t7_target;
+    int nblk;              // term-7 blocks (workgroups) of this launch
+};
 #ifndef __HIPCC_RTC__   // host launchers (not part of a hipRTC unit, jit.cpp)
+// compose + step kernel with the GogoroPaper post-physics fused in; returns 1
+// when the model has no such instantiation
+int launch_step_paper(uint64_t hash, const StepArgs &a, const PaperPostArgs &pa, hipStream_t stream,
+                      hipEvent_t ev_begin = nullptr, hipEvent_t ev_end = nullptr);
 // compose + step kernel with the Gogoro post-physics fused in; returns 1 when
 // the model has no such instantiation
 int launch_step_gogoro(uint64_t hash, const StepArgs &a, const GogoroPostArgs &pa, hipStream_t stream,
@@ -156,6 +176,7 @@ int launch_rb_forces(uint64_t hash, const float *root, const float *dof, const f
                      const float *props, hipStream_t stream);
 int model_kc(uint64_t hash);
 int model_tl(uint64_t hash);
+int model_epb(uint64_t hash);   // envs per step-kernel workgroup of a compiled model (0: not compiled in)
 int model_fused(uint64_t hash);   // codegen FUSED bits of a compiled model (0: none / not compiled in)
 int launch_compose_only(uint64_t hash, const StepArgs &a, hipStream_t stream);   // every dirty env, no step   // translating locks of a compiled model (codegen translating_locks), 0 otherwise
 

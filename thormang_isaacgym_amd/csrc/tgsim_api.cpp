@@ -93,6 +93,13 @@ struct tg_sim {
     bool no_inplace = false;     // tg_gogoro_step: reset envs re-composed, not updated in place (TG_SEAT_RECOMPOSE=1)
     bool paper_finish_launch = false;   // tg_paper_step: term 7 summed by the finish launch (TG_PAPER_FINISH=1)
     bool paper_rb_launch = false;       // tg_paper_step: rb_forces reduced by rb_force_kernel (TG_PAPER_RB_LAUNCH=1)
+    bool paper_two_launch = false;      // tg_paper_step: step kernel + post launch, never one launch (TG_PAPER_TWO_LAUNCH=1)
+    // tg_paper_step in one launch (PaperPost): the term-7 arrival counter and
+    // the total it reaches after the last launch; the device's CU count (the
+    // grid must be resident at once)
+    unsigned *t7cnt = nullptr;
+    unsigned t7_total = 0;
+    int num_cus = 0;
     int timing = 0;          // period (0: off; < 0: windows of -timing launches)
     int64_t timing_count = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending, ev_free;
@@ -240,6 +247,7 @@ int tg_sim_create(const tg_model_desc *m, const tg_sim_params *params, int32_t n
     if (const char *u = getenv("TG_SEAT_RECOMPOSE")) s->no_inplace = u[0] == '1';
     if (const char *u = getenv("TG_PAPER_FINISH")) s->paper_finish_launch = u[0] == '1';
     if (const char *u = getenv("TG_PAPER_RB_LAUNCH")) s->paper_rb_launch = u[0] == '1';
+    if (const char *u = getenv("TG_PAPER_TWO_LAUNCH")) s->paper_two_launch = u[0] == '1';
     // (TG_NO_SHARED_CACHE=1: every env reads its own block, the A/B control)
     const char *nsc = getenv("TG_NO_SHARED_CACHE");
     s->uni_ok = !(nsc && nsc[0] == '1') && (tg::model_fused(m->model_hash) & 6) == 0 && !tg::jit_has(m->model_hash);
@@ -512,7 +520,7 @@ struct DeviceGuard {
 };
 
 static int simulate_args(tg_sim *s, const tg::StepArgs &a_in, const tg::WalkPostArgs *wp = nullptr,
-                         const tg::GogoroPostArgs *gp = nullptr) {
+                         const tg::GogoroPostArgs *gp = nullptr, const tg::PaperPostArgs *pp = nullptr) {
     DeviceGuard dg(s->device);
     tg::StepArgs a = a_in;
     // the compose launch: every dirty env (host-side changes possible), the
@@ -580,6 +588,7 @@ static int simulate_args(tg_sim *s, const tg::StepArgs &a_in, const tg::WalkPost
     }
     int rc = wp   ? tg::launch_step_walk(s->hash, a, *wp, s->stream, ev.first, ev.second)
              : gp ? tg::launch_step_gogoro(s->hash, a, *gp, s->stream, ev.first, ev.second)
+             : pp ? tg::launch_step_paper(s->hash, a, *pp, s->stream, ev.first, ev.second)
                   : tg::launch_step(s->hash, a, s->stream, ev.first, ev.second);
     // the pair joins the pending list only once both events were recorded by a
     // launch that went through; otherwise it goes back to the free list
@@ -747,6 +756,9 @@ int tg_sync(tg_sim *s) {
     HIPCHK(hipMemcpy(&err, s->err, sizeof err, hipMemcpyDeviceToHost));
     if (err) {
         HIPCHK(hipMemset(s->err, 0, sizeof err));
+        if (err & 2)
+            return fail(TG_ERR_STATE, "tg_paper_step: a workgroup of the one-launch step never became resident "
+                                      "(reward term 7's batch sum timed out; set TG_PAPER_TWO_LAUNCH=1)");
         return fail(TG_ERR_STATE,
                     "a locked dof was given a [lower, upper] window wider than %g: locked joints are merged into "
                     "their parent's body in this model and stay rigid at the window centre (build the model "
@@ -991,11 +1003,76 @@ int tg_paper_pre_physics(tg_sim *s, const tg_paper_params *p, const tg_paper_buf
     return TG_OK;
 }
 
+// tg_paper_step in one launch: the pre-physics, the simulate and the
+// post-physics (PaperPost) in the step kernel.  Reward term 7's batch sum is
+// exchanged inside the launch, so every workgroup must be resident at once:
+// one workgroup per CU at most (TG_PAPER_T7_BLK envs each).  Returns 1 when
+// the launch does not apply (model, ground, batch size, residency): the
+// caller takes the two-launch path.
+static tg::PaperPre paper_pre_args(const tg_paper_params *p, const tg_paper_buffers *b, const float *actions) {
+    tg::PaperPre q{};
+    q.actions = actions;
+    q.command_history = b->command_history;
+    q.steer_delay = b->steer_delay;
+    q.curent_speed = b->curent_speed;
+    q.curent_command = b->curent_command;
+    q.pos_target = b->pos_target;
+    q.vel_target = b->vel_target;
+    q.max_steering = p->max_steering;
+    q.use_steer_delay = p->use_steer_delay;
+    q.dof_steer = p->dof_steer;
+    q.dof_rear = p->dof_rear;
+    return q;
+}
+static int paper_one_launch(tg_sim *s, const tg_paper_params *p, const tg_paper_buffers *b, const float *actions,
+                            uint64_t counter) {
+    if (s->paper_two_launch || s->pre_in_compose || s->paper_finish_launch || s->no_inplace || s->hf_rows > 0 ||
+        (b->rb_forces && s->paper_rb_launch) || !(tg::model_fused(s->hash) & 4) || tg::model_tl(s->hash) <= 0)
+        return 1;
+    const int epb = tg::model_epb(s->hash);
+    if (epb != TG_PAPER_T7_BLK || s->N % epb != 0) return 1;
+    if (s->num_cus == 0) {
+        DeviceGuard dg(s->device);
+        HIPCHK(hipDeviceGetAttribute(&s->num_cus, hipDeviceAttributeMultiprocessorCount, s->device));
+    }
+    const int nblk = s->N / epb;
+    if (nblk > s->num_cus || nblk > TG_PAPER_T7_THREADS) return 1;
+    if (!s->t7cnt) {
+        DeviceGuard dg(s->device);
+        if (s->alloc(&s->t7cnt, 1)) return TG_ERR_HIP;
+        s->t7_total = 0;
+    }
+    tg::StepArgs a = step_args(s);
+    a.pp = paper_pre_args(p, b, actions);
+    a.pp_in_step = 1;
+    a.pp.buffer_obs = b->buffer_obs;
+    a.pp.reset_buf = b->reset_buf;
+    a.pp.t7 = reinterpret_cast<double *>(b->scratch);   // (N floats hold N / 16 doubles)
+    const bool rb = b->rb_forces != nullptr;
+    const tg::PaperPostArgs pa{*p, *b, (uint32_t)counter, (uint32_t)(counter >> 32), rb ? s->force : nullptr,
+                               s->t7cnt, s->t7_total + (unsigned)nblk, nblk};
+    if (int rc = simulate_args(s, a, nullptr, nullptr, &pa)) return rc < 0 ? rc : 1;
+    s->t7_total += (unsigned)nblk;   // (the launch adds nblk arrivals)
+    if (rb) {   // the next simulate's rigid-body forces, reduced already
+        s->rbf_f = b->rb_forces;
+        s->rbf_t = nullptr;
+        s->rbf_space = TG_ENV_SPACE;
+        s->rbf_pending = false;
+        s->rbf_prereduced = true;
+        s->forces_pending = true;
+    }
+    return TG_OK;
+}
+
 int tg_paper_step(tg_sim *s, const tg_paper_params *p, const tg_paper_buffers *b, const float *actions,
                   int32_t n_simulate, uint64_t counter) {
     if (int rc = check_paper(s, p, b)) return rc;
     if (!actions) return fail(TG_ERR_ARG, "paper: null actions");
     if (n_simulate < 1) return fail(TG_ERR_ARG, "tg_paper_step: n_simulate %d < 1", n_simulate);
+    if (n_simulate == 1) {
+        const int rc = paper_one_launch(s, p, b, actions, counter);
+        if (rc != 1) return rc;
+    }
     bool fin = false;
     for (int i = 0; i < n_simulate; ++i) {
         tg::StepArgs a = step_args(s);
