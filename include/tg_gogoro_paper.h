@@ -104,7 +104,8 @@ typedef struct tg_paper_buffers {
      * to the next simulate exactly as tg_apply_rigid_body_force_tensors(sim,
      * rb_forces, NULL, TG_ENV_SPACE) right after the call would (the post_physics
      * pushes write head_p_link's rows first, paper.py:449-457), reduced to the
-     * group wrenches inside the post launch; the separate-call API ignores it */
+     * group wrenches inside the step's post-physics; the separate-call API
+     * ignores it */
     const float *rb_forces;
 } tg_paper_buffers;
 
@@ -118,7 +119,14 @@ int tg_paper_post_physics(tg_sim *sim, const tg_paper_params *p, const tg_paper_
 int tg_paper_reset_idx(tg_sim *sim, const tg_paper_params *p, const tg_paper_buffers *b, const int32_t *ids,
                        int32_t n, const float *reset_draws, uint64_t counter);
 /* pre_physics_step + n_simulate x simulate + post_physics_step with in-kernel
- * draws (counter: the post-physics call's) */
+ * draws (counter: the post-physics call's).  With n_simulate == 1, a compiled
+ * model with in-place seat composites, flat ground and a batch of at most one
+ * step-kernel workgroup (16 envs) per CU, the whole step is ONE kernel launch:
+ * the post-physics runs as the step kernel's epilogue and reward term 7's
+ * batch sum is exchanged between the launch's workgroups (a workgroup that
+ * never became resident makes tg_sync report TG_ERR_STATE).  Otherwise, or
+ * with TG_PAPER_TWO_LAUNCH=1 in the environment at tg_sim creation: the step
+ * kernel (pre-physics inside) and one post launch. */
 int tg_paper_step(tg_sim *sim, const tg_paper_params *p, const tg_paper_buffers *b, const float *actions,
                   int32_t n_simulate, uint64_t counter);
 
