@@ -1768,11 +1768,12 @@ namespace tg {
 // wavefront; the wavefront sums in order (the post launch's total bit for bit).
 // (A/B, profiles/r6/paper_one_launch_ab.txt: reading the count a substep
 // ahead measured no gain)
+// (c0: the count as lane 0 read it before, with the epilogue's first batch)
 __device__ __forceinline__ double paper_t7_wait_sum(const double *t7, unsigned *cnt, unsigned target, int nblk,
-                                                    int *err) {
+                                                    int *err, unsigned c0) {
     const int lane = threadIdx.x & 63;
     if (lane == 0) {
-        unsigned it = 0, c = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned it = 0, c = c0;
         while ((int)(c - target) < 0) {
             if (++it > (1u << 20)) {   // ~1 s: a workgroup never became resident
                 if (err) atomicOr(err, 2);
@@ -1982,6 +1983,9 @@ template <class M, int LN> struct RbLanes {
 // The same helpers (paper_math.h), Philox blocks and sum order as the post
 // kernel; this unit's transcendentals and the physics' fp contraction in the
 // link kinematics are the differences (tests/test_gpu_paper.py).
+#ifndef TG_PAPER_T7_END
+#define TG_PAPER_T7_END 1   // developer switch: 0 = reward term 7's batch sum before the histories (A/B)
+#endif
 struct PaperPost {
     static constexpr bool on = true;
     static constexpr bool PM_OUT = false;
@@ -2081,7 +2085,13 @@ struct PaperPost {
             dv[3] = u01(x.w);
         }
         // reward term 7's batch sum (every workgroup's prologue published its block)
-        const double tot = paper_t7_wait_sum(a.pp.t7, pa.t7_count, pa.t7_target, pa.nblk, a.err);
+        // the term-7 arrival count, read with the first batch; the batch sum
+        // itself waits until the end (TG_PAPER_T7_END), where its loads overlap
+        // the epilogue's store drain
+        const unsigned c0 = (threadIdx.x & 63) == 0 ? __hip_atomic_load(pa.t7_count, __ATOMIC_RELAXED,
+                                                                       __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        double tot = 0.0;
+        if (!TG_PAPER_T7_END) tot = paper_t7_wait_sum(a.pp.t7, pa.t7_count, pa.t7_target, pa.nblk, a.err, c0);
         // ---- the extension and the draws to the env's LDS
         if constexpr (M::NTL > 0) {
 #pragma unroll
@@ -2172,12 +2182,14 @@ struct PaperPost {
             }
         }
         // ---- rewards, resets, time_outs, command changes, pushes (lead lane)
+        float rew = 0.f, tilt = 0.f;
         if (lead && owner) {
             float last[PO];
 #pragma unroll
             for (int k = 0; k < PO; ++k) last[k] = s(OB + k);
-            const float rew = reward15(p, last);
-            finish_env(p, b, e, tot, last[0], prog, rew);
+            rew = reward15(p, last);
+            tilt = last[0];
+            if (!TG_PAPER_T7_END) finish_env(p, b, e, tot, tilt, prog, rew);
             commands(p, b, e, prog, L, last, draw(0, 5), draw(0, 6), draw(0, 7), draw(1, 7));
         }
         if (b.body_force && owner) {
@@ -2201,6 +2213,10 @@ struct PaperPost {
             rb.load(a.comp, e, b.rb_forces, sub);
             rb.finish(b.root, b.dof_state, b.rb_forces, plink, e, pa.rb_out, sub, s.b, s.b + 9 * M::NG, b.dof_props,
                       p.num_envs, owner);
+        }
+        if (TG_PAPER_T7_END) {   // reward term 7's batch sum, then the rewards / resets / time-outs
+            tot = paper_t7_wait_sum(a.pp.t7, pa.t7_count, pa.t7_target, pa.nblk, a.err, c0);
+            if (lead && owner) finish_env(p, b, e, tot, tilt, prog, rew);
         }
     }
 };
