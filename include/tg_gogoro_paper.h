@@ -126,7 +126,9 @@ int tg_paper_reset_idx(tg_sim *sim, const tg_paper_params *p, const tg_paper_buf
  * batch sum is exchanged between the launch's workgroups (a workgroup that
  * never became resident makes tg_sync report TG_ERR_STATE).  Otherwise, or
  * with TG_PAPER_TWO_LAUNCH=1 in the environment at tg_sim creation: the step
- * kernel (pre-physics inside) and one post launch. */
+ * kernel (pre-physics inside) and one post launch.  The one-launch form
+ * passes each launch its own arrival target: do not capture it into a HIP
+ * graph for replay (set TG_PAPER_TWO_LAUNCH=1 for that). */
 int tg_paper_step(tg_sim *sim, const tg_paper_params *p, const tg_paper_buffers *b, const float *actions,
                   int32_t n_simulate, uint64_t counter);
 
