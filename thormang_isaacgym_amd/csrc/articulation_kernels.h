@@ -2207,8 +2207,9 @@ struct PaperPost {
             wsync();   // (the LDS scratch above is consumed)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            // (every input after the stores: loading the static ones with the
-            // epilogue's first batch measured +0.45 us, paper_one_launch_ab.txt)
+            // (every input after the stores: the static ones with the
+            // epilogue's first batch, or behind the history stores, measured
+            // +0.45 us each, paper_one_launch_ab.txt)
             RbLanes<M, LPE> rb;
             rb.load(a.comp, e, b.rb_forces, sub);
             rb.finish(b.root, b.dof_state, b.rb_forces, plink, e, pa.rb_out, sub, s.b, s.b + 9 * M::NG, b.dof_props,
